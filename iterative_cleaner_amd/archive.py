@@ -1,0 +1,272 @@
+"""NumPy stand-in for the subset of the psrchive ``Archive`` API that the
+surgical cleaner touches (reference calls listed at
+iterative_cleaner.py:47-60, :66-125, :150-162, :262-272, :300-330).
+
+psrchive is not installed here (no network), so this module *defines* the
+archive semantics that both the reference-driven golden fixtures and the GPU
+path must follow.  Every floating-point reduction below has a fixed, written
+order so that the HIP kernels can reproduce it bit-for-bit:
+
+* samples and weights are float32 (``get_data``/``get_weights`` return f32
+  copies);
+* ``pscrunch``: total intensity = f32(pol0 + pol1);
+* ``dedisperse``/``dededisperse``: integer per-channel rotation by
+  ``dm_shift[c]`` bins, ``ded[i] = raw[(i + shift) % nbin]``;
+* channel sums (baseline total, fscrunch) use the CANONICAL CHANNEL ORDER
+  (:func:`chan_sum`): f64, sequential inside super-blocks of ``SUPER_BLOCK``
+  channels, partials added sequentially.  Shards that own whole super-blocks
+  therefore reproduce single-device bits;
+* ``remove_baseline``: per subint (psrchive Integration::remove_baseline),
+  the off-pulse window of width ``int(duty*nbin)`` is the first argmin of
+  the circular window sums of the weighted, dedispersed total profile; each
+  profile subtracts f32(mean of its own samples in that window) in f32;
+* ``fscrunch``/``tscrunch``: weighted means, f64 accumulation, f32 result,
+  weights summed.
+"""
+from __future__ import annotations
+
+import copy
+import os
+
+import numpy as np
+
+SUPER_BLOCK = 256          # channels per canonical-order super-block
+BASELINE_DUTY = 0.15       # psrchive BaselineWindow default duty cycle
+
+__all__ = ["Archive", "Archive_load", "Profile", "Integration", "chan_sum",
+           "baseline_width", "window_argmin", "SUPER_BLOCK", "BASELINE_DUTY"]
+
+
+def chan_sum(terms: np.ndarray, axis: int) -> np.ndarray:
+    """Canonical channel reduction of f64 ``terms`` along ``axis``.
+
+    result = 0.0; for each super-block b: part = 0.0; part += t[c] for c in b
+    (ascending); result += part.  Zero-size → 0.0.
+    """
+    t = np.moveaxis(np.asarray(terms, dtype=np.float64), axis, 0)
+    nchan = t.shape[0]
+    total = np.zeros(t.shape[1:], dtype=np.float64)
+    for b0 in range(0, nchan, SUPER_BLOCK):
+        part = np.zeros(t.shape[1:], dtype=np.float64)
+        for c in range(b0, min(b0 + SUPER_BLOCK, nchan)):
+            part = part + t[c]
+        total = total + part
+    return total
+
+
+def baseline_width(nbin: int, duty: float = BASELINE_DUTY) -> int:
+    return max(1, int(duty * nbin))
+
+
+def window_argmin(total: np.ndarray, width: int) -> np.ndarray:
+    """First argmin (numpy NaN semantics) over j of the circular window sums
+    m[j] = sum_{k<width} total[..., (j+k) % nbin], sequential over k, f64."""
+    total = np.asarray(total, dtype=np.float64)
+    m = np.zeros_like(total)
+    for k in range(width):
+        m = m + np.roll(total, -k, axis=-1)
+    return np.argmin(m, axis=-1)
+
+
+class _Epoch:
+    def __init__(self, mjd: float):
+        self.mjd = float(mjd)
+
+    def strtempo(self) -> str:
+        return "%.15f" % self.mjd
+
+    def in_days(self) -> float:
+        return self.mjd
+
+
+class Profile:
+    """``ar.get_Profile(isub, ipol, ichan)``: amps are a writable f32 view."""
+
+    def __init__(self, ar: "Archive", isub: int, ipol: int, ichan: int):
+        self._ar, self._isub, self._ipol, self._ichan = ar, isub, ipol, ichan
+
+    def get_amps(self) -> np.ndarray:
+        return self._ar._data[self._isub, self._ipol, self._ichan]
+
+    def get_weight(self) -> float:
+        return float(self._ar._weights[self._isub, self._ichan])
+
+    def set_weight(self, w: float) -> None:
+        self._ar._weights[self._isub, self._ichan] = w
+
+    def get_nbin(self) -> int:
+        return self._ar.get_nbin()
+
+
+class Integration:
+    def __init__(self, ar: "Archive", isub: int):
+        self._ar, self._isub = ar, isub
+
+    def set_weight(self, ichan: int, w: float) -> None:
+        self._ar._weights[self._isub, ichan] = w
+
+    def get_weight(self, ichan: int) -> float:
+        return float(self._ar._weights[self._isub, ichan])
+
+    def get_nchan(self) -> int:
+        return self._ar.get_nchan()
+
+
+class Archive:
+    """In-memory pulsar archive: data (nsub, npol, nchan, nbin) float32."""
+
+    def __init__(self, data, weights=None, dm_shift=None, dedispersed=False,
+                 filename="synthetic.ar", source="J0000+0000",
+                 centre_frequency=1400.0, mjd_start=60000.0, mjd_end=60000.01,
+                 baseline_duty=BASELINE_DUTY):
+        data = np.asarray(data, dtype=np.float32)
+        if data.ndim != 4:
+            raise ValueError("data must be (nsub, npol, nchan, nbin)")
+        self._data = np.ascontiguousarray(data)
+        nsub, _, nchan, nbin = data.shape
+        if weights is None:
+            weights = np.ones((nsub, nchan), dtype=np.float32)
+        self._weights = np.array(weights, dtype=np.float32).reshape(nsub, nchan)
+        if dm_shift is None:
+            dm_shift = np.zeros(nchan, dtype=np.int64)
+        self._shift = np.mod(np.asarray(dm_shift, dtype=np.int64), nbin).reshape(nchan)
+        self._dedispersed = bool(dedispersed)
+        self._filename = filename
+        self._source = source
+        self._cfreq = float(centre_frequency)
+        self._mjd = (float(mjd_start), float(mjd_end))
+        self._duty = float(baseline_duty)
+
+    # ---------------------------------------------------------------- shape
+    def get_nsubint(self): return self._data.shape[0]
+    def get_npol(self): return self._data.shape[1]
+    def get_nchan(self): return self._data.shape[2]
+    def get_nbin(self): return self._data.shape[3]
+
+    # ---------------------------------------------------------------- access
+    def get_data(self) -> np.ndarray:
+        return self._data.copy()
+
+    def get_weights(self) -> np.ndarray:
+        return self._weights.copy()
+
+    def get_Profile(self, isub, ipol, ichan) -> Profile:
+        return Profile(self, int(isub), int(ipol), int(ichan))
+
+    def get_Integration(self, isub) -> Integration:
+        return Integration(self, int(isub))
+
+    def get_dm_shift(self) -> np.ndarray:
+        return self._shift.copy()
+
+    def get_dedispersed(self) -> bool:
+        return self._dedispersed
+
+    def get_filename(self) -> str:
+        return self._filename
+
+    def get_source(self) -> str:
+        return self._source
+
+    def get_centre_frequency(self) -> float:
+        return self._cfreq
+
+    def start_time(self) -> _Epoch:
+        return _Epoch(self._mjd[0])
+
+    def end_time(self) -> _Epoch:
+        return _Epoch(self._mjd[1])
+
+    def get_baseline_duty(self) -> float:
+        return self._duty
+
+    def __str__(self) -> str:
+        # "<format>:<name>"; the CLI (iterative_cleaner.py:49) splits on the first ':'
+        return "NumPyArchive:%s" % os.path.splitext(self._filename)[0]
+
+    def clone(self) -> "Archive":
+        return copy.deepcopy(self)
+
+    # ---------------------------------------------------------------- transforms
+    def pscrunch(self) -> None:
+        if self.get_npol() > 1:
+            self._data = np.ascontiguousarray(self._data[:, 0:1] + self._data[:, 1:2])
+
+    def _ded_view(self) -> np.ndarray:
+        """Samples in the dedispersed frame (a copy if currently dispersed)."""
+        if self._dedispersed:
+            return self._data
+        out = np.empty_like(self._data)
+        n = self.get_nbin()
+        idx = (np.arange(n)[None, :] + self._shift[:, None]) % n
+        for c in range(self.get_nchan()):
+            out[:, :, c, :] = self._data[:, :, c, idx[c]]
+        return out
+
+    def dedisperse(self) -> None:
+        if not self._dedispersed:
+            self._data = self._ded_view()
+            self._dedispersed = True
+
+    def dededisperse(self) -> None:
+        if self._dedispersed:
+            n = self.get_nbin()
+            out = np.empty_like(self._data)
+            idx = (np.arange(n)[None, :] - self._shift[:, None]) % n
+            for c in range(self.get_nchan()):
+                out[:, :, c, :] = self._data[:, :, c, idx[c]]
+            self._data = out
+            self._dedispersed = False
+
+    def remove_baseline(self) -> None:
+        ded = self._ded_view()
+        if self.get_npol() > 1:
+            tot_src = ded[:, 0] + ded[:, 1]
+        else:
+            tot_src = ded[:, 0]
+        w64 = self._weights.astype(np.float64)
+        # total[s, i] = canonical chan sum of w[s,c] * x[s,c,i]
+        total = chan_sum(w64[:, :, None] * tot_src.astype(np.float64), axis=1)
+        width = baseline_width(self.get_nbin(), self._duty)
+        j0 = window_argmin(total, width)                          # (nsub,)
+        n = self.get_nbin()
+        acc = np.zeros(ded.shape[:3], dtype=np.float64)           # (nsub, npol, nchan)
+        for k in range(width):
+            cols = (j0 + k) % n
+            acc = acc + ded[np.arange(ded.shape[0]), :, :, cols].astype(np.float64)
+        base = (acc / width).astype(np.float32)
+        self._data = (self._data - base[..., None]).astype(np.float32)
+
+    def fscrunch(self) -> None:
+        w64 = self._weights.astype(np.float64)
+        wsum = chan_sum(w64, axis=1)                              # (nsub,)
+        num = chan_sum(w64[:, None, :, None] * self._data.astype(np.float64), axis=2)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            prof = np.where(wsum[:, None, None] != 0.0,
+                            num / wsum[:, None, None], 0.0).astype(np.float32)
+        self._data = np.ascontiguousarray(prof[:, :, None, :])
+        self._weights = wsum.astype(np.float32)[:, None]
+        self._shift = np.zeros(1, dtype=np.int64)
+
+    def tscrunch(self) -> None:
+        nsub = self.get_nsubint()
+        w64 = self._weights.astype(np.float64)                   # (nsub, nchan)
+        wt = np.zeros(w64.shape[1], dtype=np.float64)
+        num = np.zeros(self._data.shape[1:], dtype=np.float64)   # (npol, nchan, nbin)
+        for s in range(nsub):
+            wt = wt + w64[s]
+            num = num + w64[s][None, :, None] * self._data[s].astype(np.float64)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            prof = np.where(wt[None, :, None] != 0.0, num / wt[None, :, None], 0.0)
+        self._data = np.ascontiguousarray(prof.astype(np.float32)[None])
+        self._weights = wt.astype(np.float32)[None, :]
+
+    # ---------------------------------------------------------------- I/O
+    def unload(self, path: str) -> None:
+        from . import archive_io
+        archive_io.save(self, path)
+
+
+def Archive_load(path: str) -> Archive:
+    from . import archive_io
+    return archive_io.load(path)

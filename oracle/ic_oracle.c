@@ -1,0 +1,902 @@
+/*
+ * ic_oracle.c — CPU ORACLE, TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of one reference cleaning run
+ * (/root/reference/iterative_cleaner.py:65-146) under the repo's archive
+ * stand-in semantics (iterative_cleaner_amd/archive.py).  It is the checker
+ * for the HIP path; it is never linked into libicgpu.so.
+ *
+ *   orc_lmdif1        scipy 1.15.3 leastsq(err,[1.0]) for n = 1
+ *                     (scipy/optimize/_minpack_py.py:291-506 -> MINPACK lmdif,
+ *                      fdjac2, qrfac, lmpar, qrsolv, enorm), used at
+ *                     iterative_cleaner.py:277-279
+ *   orc_template      template build, iterative_cleaner.py:88-94
+ *   orc_fit_cube      fit-cube prep, iterative_cleaner.py:96-100
+ *   orc_fit_residual  remove_profile_inplace / remove_profile1d, :259-288
+ *   orc_diagnostics   comprehensive_stats diagnostics, :206-217
+ *   orc_test          scalers + combine, :219-256
+ *   orc_clean_loop    the while loop, :83-146
+ *
+ * Build: gcc -O2 -fPIC -shared -ffp-contract=off -fno-fast-math (oracle/Makefile)
+ * Pinned against the tests/golden npz fixtures (reference outputs) and live scipy.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define SUPER_BLOCK 256
+
+/* ------------------------------------------------------------------ enorm */
+/* MINPACK enorm (sequential, three-accumulator scaled sum of squares).      */
+static double enorm_d(int n, const double *x)
+{
+    const double rdwarf = 3.834e-20, rgiant = 1.304e19;
+    double s1 = 0.0, s2 = 0.0, s3 = 0.0, x1max = 0.0, x3max = 0.0;
+    double agiant = rgiant / (double)n;
+    for (int i = 0; i < n; ++i) {
+        double xabs = fabs(x[i]);
+        if (xabs > rdwarf && xabs < agiant) {
+            s2 += xabs * xabs;
+        } else if (xabs <= rdwarf) {
+            if (xabs > x3max) {
+                double t = x3max / xabs;
+                s3 = 1.0 + s3 * (t * t);
+                x3max = xabs;
+            } else if (xabs != 0.0) {
+                double t = xabs / x3max;
+                s3 += t * t;
+            }
+        } else {
+            if (xabs > x1max) {
+                double t = x1max / xabs;
+                s1 = 1.0 + s1 * (t * t);
+                x1max = xabs;
+            } else {
+                double t = xabs / x1max;
+                s1 += t * t;
+            }
+        }
+    }
+    if (s1 != 0.0) return x1max * sqrt(s1 + (s2 / x1max) / x1max);
+    if (s2 != 0.0) {
+        if (s2 >= x3max) return sqrt(s2 * (1.0 + (x3max / s2) * (x3max * s3)));
+        return sqrt(x3max * ((s2 / x3max) + (x3max * s3)));
+    }
+    return x3max * sqrt(s3);
+}
+
+static double enorm1(double v) { return enorm_d(1, &v); }
+static double dmax(double a, double b) { return a >= b ? a : b; }
+static double dmin(double a, double b) { return a <= b ? a : b; }
+
+/* err(a) = a*T - p  (iterative_cleaner.py:277), f64, no contraction */
+static void fcn(int m, double a, const float *T, const float *p, double *out)
+{
+    for (int i = 0; i < m; ++i) {
+        double t = a * (double)T[i];
+        out[i] = t - (double)p[i];
+    }
+}
+
+/* MINPACK qrsolv for n = 1. r: R(0,0); w = sqrt(par)*diag; qtb = qtf.
+ * returns x, writes sdiag. */
+static double qrsolv1(double r, double w, double qtb, double *sdiag)
+{
+    double rr = r, wa = qtb, sd;
+    if (w != 0.0) {
+        sd = w;
+        double qtbpj = 0.0;
+        if (sd != 0.0) {
+            double cs, sn;
+            if (fabs(rr) >= fabs(sd)) {
+                double tn = sd / rr;
+                cs = 0.5 / sqrt(0.25 + 0.25 * (tn * tn));
+                sn = cs * tn;
+            } else {
+                double ct = rr / sd;
+                sn = 0.5 / sqrt(0.25 + 0.25 * (ct * ct));
+                cs = sn * ct;
+            }
+            rr = cs * rr + sn * sd;
+            double temp = cs * wa + sn * qtbpj;
+            wa = temp;
+        }
+    }
+    sd = rr;
+    double x;
+    if (sd == 0.0) {
+        x = 0.0;
+    } else {
+        double sum = 0.0;
+        x = (wa - sum) / sd;
+    }
+    *sdiag = sd;
+    return x;
+}
+
+/* MINPACK lmpar for n = 1; returns the step x, updates *par. */
+static double lmpar1(double r, double diag, double qtb, double delta, double *par_io)
+{
+    const double p1 = 0.1, p001 = 0.001, dwarf = DBL_MIN;
+    double par = *par_io;
+    int nsing = (r == 0.0) ? 0 : 1;
+    double wa1 = qtb;
+    if (nsing < 1) wa1 = 0.0;
+    if (nsing >= 1) wa1 = wa1 / r;
+    double x = wa1;
+    int iter = 0;
+    double wa2 = diag * x;
+    double dxnorm = enorm1(wa2);
+    double fp = dxnorm - delta;
+    if (!(fp <= p1 * delta)) {
+        double parl = 0.0;
+        if (nsing >= 1) {
+            double t = diag * (wa2 / dxnorm);
+            double sum = 0.0;
+            t = (t - sum) / r;
+            double temp = enorm1(t);
+            parl = ((fp / delta) / temp) / temp;
+        }
+        double sum = 0.0;
+        sum += r * qtb;
+        double g = sum / diag;
+        double gnorm = enorm1(g);
+        double paru = gnorm / delta;
+        if (paru == 0.0) paru = dwarf / dmin(delta, p1);
+        par = dmax(par, parl);
+        par = dmin(par, paru);
+        if (par == 0.0) par = gnorm / dxnorm;
+        for (;;) {
+            ++iter;
+            if (par == 0.0) par = dmax(dwarf, p001 * paru);
+            double temp = sqrt(par);
+            double w = temp * diag;
+            double sdiag;
+            x = qrsolv1(r, w, qtb, &sdiag);
+            wa2 = diag * x;
+            dxnorm = enorm1(wa2);
+            temp = fp;
+            fp = dxnorm - delta;
+            if (fabs(fp) <= p1 * delta || (parl == 0.0 && fp <= temp && temp < 0.0) || iter == 10)
+                break;
+            double t = diag * (wa2 / dxnorm);
+            t = t / sdiag;
+            double tn = enorm1(t);
+            double parc = ((fp / delta) / tn) / tn;
+            if (fp > 0.0) parl = dmax(parl, par);
+            if (fp < 0.0) paru = dmin(paru, par);
+            par = dmax(parl, par + parc);
+        }
+    }
+    if (iter == 0) par = 0.0;
+    *par_io = par;
+    return x;
+}
+
+/* scipy.optimize.leastsq(err, [1.0]) with err(a) = a*T - p.
+ * Returns info; *x_out = solution; *nfev_out = evaluations inside lmdif.
+ * work: 3*m doubles (or NULL). */
+int orc_lmdif1(int m, const float *T, const float *p, double *x_out, int *nfev_out, double *work)
+{
+    const double ftol = 1.49012e-8, xtol = 1.49012e-8, gtol = 0.0;
+    const double epsfcn = DBL_EPSILON, epsmch = DBL_EPSILON, factor = 100.0;
+    const int maxfev = 400;
+    double *own = NULL;
+    if (!work) work = own = (double *)malloc(sizeof(double) * 3 * (size_t)(m > 0 ? m : 1));
+    double *fvec = work, *wa4 = work + m, *fjac = work + 2 * m;
+    int info = 0, nfev = 0;
+    double x = 1.0;
+
+    fcn(m, x, T, p, fvec);
+    nfev = 1;
+    double fnorm = enorm_d(m, fvec);
+    double par = 0.0, xnorm = 0.0, delta = 0.0, diag = 0.0;
+    int iter = 1;
+    for (;;) {
+        /* fdjac2 */
+        double eps = sqrt(dmax(epsfcn, epsmch));
+        double temp = x;
+        double h = eps * fabs(temp);
+        if (h == 0.0) h = eps;
+        double xh = temp + h;
+        fcn(m, xh, T, p, wa4);
+        for (int i = 0; i < m; ++i) fjac[i] = (wa4[i] - fvec[i]) / h;
+        nfev += 1;
+        /* qrfac, n = 1, pivoting */
+        double acnorm = enorm_d(m, fjac);
+        double ajnorm = enorm_d(m, fjac);
+        if (ajnorm != 0.0) {
+            if (fjac[0] < 0.0) ajnorm = -ajnorm;
+            for (int i = 0; i < m; ++i) fjac[i] = fjac[i] / ajnorm;
+            fjac[0] = fjac[0] + 1.0;
+        }
+        double rdiag = -ajnorm;
+        if (iter == 1) {
+            diag = acnorm;
+            if (diag == 0.0) diag = 1.0;
+            xnorm = enorm1(diag * x);
+            delta = factor * xnorm;
+            if (delta == 0.0) delta = factor;
+        }
+        /* qtf = (Q^T fvec)[0] */
+        double qtf = fvec[0];
+        if (fjac[0] != 0.0) {
+            double sum = 0.0;
+            for (int i = 0; i < m; ++i) sum += fjac[i] * fvec[i];
+            double t = -sum / fjac[0];
+            qtf = fvec[0] + fjac[0] * t;
+        }
+        double r = rdiag;
+        double gnorm = 0.0;
+        if (fnorm != 0.0 && acnorm != 0.0) {
+            double sum = 0.0;
+            sum += r * (qtf / fnorm);
+            gnorm = dmax(gnorm, fabs(sum / acnorm));
+        }
+        if (gnorm <= gtol) info = 4;
+        if (info != 0) break;
+        diag = dmax(diag, acnorm);
+        for (;;) {
+            double step = lmpar1(r, diag, qtf, delta, &par);
+            double wa1 = -step;
+            double x2 = x + wa1;
+            double pnorm = enorm1(diag * wa1);
+            if (iter == 1) delta = dmin(delta, pnorm);
+            fcn(m, x2, T, p, wa4);
+            nfev += 1;
+            double fnorm1 = enorm_d(m, wa4);
+            double actred = -1.0;
+            if (0.1 * fnorm1 < fnorm) {
+                double t = fnorm1 / fnorm;
+                actred = 1.0 - t * t;
+            }
+            double w3 = 0.0;
+            w3 += r * wa1;
+            double temp1 = enorm1(w3) / fnorm;
+            double temp2 = (sqrt(par) * pnorm) / fnorm;
+            double prered = temp1 * temp1 + temp2 * temp2 / 0.5;
+            double dirder = -(temp1 * temp1 + temp2 * temp2);
+            double ratio = 0.0;
+            if (prered != 0.0) ratio = actred / prered;
+            if (ratio <= 0.25) {
+                double tt = 0.0;
+                if (actred >= 0.0) tt = 0.5;
+                if (actred < 0.0) tt = 0.5 * dirder / (dirder + 0.5 * actred);
+                if (0.1 * fnorm1 >= fnorm || tt < 0.1) tt = 0.1;
+                delta = tt * dmin(delta, pnorm / 0.1);
+                par = par / tt;
+            } else if (par == 0.0 || ratio >= 0.75) {
+                delta = pnorm / 0.5;
+                par = 0.5 * par;
+            }
+            if (ratio >= 1e-4) {
+                x = x2;
+                double w2 = diag * x;
+                memcpy(fvec, wa4, sizeof(double) * (size_t)m);
+                xnorm = enorm1(w2);
+                fnorm = fnorm1;
+                iter += 1;
+            }
+            if (fabs(actred) <= ftol && prered <= ftol && 0.5 * ratio <= 1.0) info = 1;
+            if (delta <= xtol * xnorm) info = 2;
+            if (fabs(actred) <= ftol && prered <= ftol && 0.5 * ratio <= 1.0 && info == 2) info = 3;
+            if (info != 0) goto done;
+            if (nfev >= maxfev) info = 5;
+            if (fabs(actred) <= epsmch && prered <= epsmch && 0.5 * ratio <= 1.0) info = 6;
+            if (delta <= epsmch * xnorm) info = 7;
+            if (gnorm <= epsmch) info = 8;
+            if (info != 0) goto done;
+            if (ratio >= 1e-4) break;
+        }
+    }
+done:
+    *x_out = x;
+    if (nfev_out) *nfev_out = nfev;
+    free(own);
+    return info;
+}
+
+/* ---------------------------------------------------------- fit + residual */
+/* remove_profile1d (iterative_cleaner.py:275-288) + f32 store (:272).
+ * D: fit cube (P, m) dedispersed; R out (P, m) f32 dedispersed frame. */
+void orc_fit_residual(int P, int m, const float *T, const float *D,
+                      int pr_on, double pr_factor, int pr_start, int pr_end,
+                      double *amp, int32_t *info, float *R)
+{
+    double *work = (double *)malloc(sizeof(double) * 3 * (size_t)m);
+    for (int k = 0; k < P; ++k) {
+        const float *p = D + (size_t)k * m;
+        double x;
+        int st = orc_lmdif1(m, T, p, &x, NULL, work);
+        amp[k] = x;
+        info[k] = st;
+        float *o = R + (size_t)k * m;
+        if (st < 1 || st > 4) {
+            for (int i = 0; i < m; ++i) o[i] = 0.0f;
+            continue;
+        }
+        for (int i = 0; i < m; ++i) {
+            double t = x * (double)T[i];
+            double e = t - (double)p[i];
+            if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
+            o[i] = (float)e;
+        }
+    }
+    free(work);
+}
+
+/* ------------------------------------------------------- archive stand-in */
+static inline float ded_at(const float *prof, int n, int shift, int i)
+{
+    int j = i + shift;
+    if (j >= n) j -= n;
+    return prof[j];
+}
+
+/* remove_baseline (archive.py): per subint window from the weighted total.
+ * raw (nsub, nchan, n) dispersed frame; W weights; writes base (nsub*nchan). */
+void orc_baseline(int nsub, int nchan, int n, const float *raw, const float *W,
+                  const int32_t *shift, double duty, float *base, int32_t *win_out)
+{
+    int width = (int)(duty * (double)n);
+    if (width < 1) width = 1;
+    double *tot = (double *)malloc(sizeof(double) * (size_t)n);
+    double *part = (double *)malloc(sizeof(double) * (size_t)n);
+    for (int s = 0; s < nsub; ++s) {
+        for (int i = 0; i < n; ++i) tot[i] = 0.0;
+        for (int b0 = 0; b0 < nchan; b0 += SUPER_BLOCK) {
+            for (int i = 0; i < n; ++i) part[i] = 0.0;
+            int b1 = b0 + SUPER_BLOCK < nchan ? b0 + SUPER_BLOCK : nchan;
+            for (int c = b0; c < b1; ++c) {
+                const float *prof = raw + ((size_t)s * nchan + c) * n;
+                double w = (double)W[(size_t)s * nchan + c];
+                for (int i = 0; i < n; ++i) part[i] = part[i] + w * (double)ded_at(prof, n, shift[c], i);
+            }
+            for (int i = 0; i < n; ++i) tot[i] = tot[i] + part[i];
+        }
+        /* first argmin of circular window sums, numpy NaN semantics */
+        int best = 0;
+        double bestv = 0.0;
+        for (int j = 0; j < n; ++j) {
+            double msum = 0.0;
+            for (int k = 0; k < width; ++k) {
+                int q = j + k;
+                q %= n;
+                msum = msum + tot[q];
+            }
+            if (j == 0) { best = 0; bestv = msum; continue; }
+            if (isnan(bestv)) continue;
+            if (isnan(msum) || msum < bestv) { best = j; bestv = msum; }
+        }
+        if (win_out) win_out[s] = best;
+        for (int c = 0; c < nchan; ++c) {
+            const float *prof = raw + ((size_t)s * nchan + c) * n;
+            double acc = 0.0;
+            for (int k = 0; k < width; ++k) acc = acc + (double)ded_at(prof, n, shift[c], (best + k) % n);
+            base[(size_t)s * nchan + c] = (float)(acc / (double)width);
+        }
+    }
+    free(tot);
+    free(part);
+}
+
+/* fit cube (iterative_cleaner.py:96-100): D = f32(ded - base(w0)). */
+void orc_fit_cube(int nsub, int nchan, int n, const float *raw, const float *w0,
+                  const int32_t *shift, double duty, float *D)
+{
+    float *base = (float *)malloc(sizeof(float) * (size_t)nsub * nchan);
+    orc_baseline(nsub, nchan, n, raw, w0, shift, duty, base, NULL);
+    for (int s = 0; s < nsub; ++s)
+        for (int c = 0; c < nchan; ++c) {
+            const float *prof = raw + ((size_t)s * nchan + c) * n;
+            float b = base[(size_t)s * nchan + c];
+            float *o = D + ((size_t)s * nchan + c) * n;
+            for (int i = 0; i < n; ++i) o[i] = ded_at(prof, n, shift[c], i) - b;
+        }
+    free(base);
+}
+
+/* template (iterative_cleaner.py:88-94): remove_baseline(W), dedisperse,
+ * fscrunch, tscrunch, amps * 10000 (f32). */
+void orc_template(int nsub, int nchan, int n, const float *raw, const float *W,
+                  const int32_t *shift, double duty, float *T)
+{
+    float *base = (float *)malloc(sizeof(float) * (size_t)nsub * nchan);
+    orc_baseline(nsub, nchan, n, raw, W, shift, duty, base, NULL);
+    double *num = (double *)malloc(sizeof(double) * (size_t)n);
+    double *part = (double *)malloc(sizeof(double) * (size_t)n);
+    float *F = (float *)malloc(sizeof(float) * (size_t)nsub * n);
+    float *wf = (float *)malloc(sizeof(float) * (size_t)nsub);
+    for (int s = 0; s < nsub; ++s) {
+        double wsum = 0.0;
+        for (int i = 0; i < n; ++i) num[i] = 0.0;
+        for (int b0 = 0; b0 < nchan; b0 += SUPER_BLOCK) {
+            int b1 = b0 + SUPER_BLOCK < nchan ? b0 + SUPER_BLOCK : nchan;
+            double wpart = 0.0;
+            for (int i = 0; i < n; ++i) part[i] = 0.0;
+            for (int c = b0; c < b1; ++c) {
+                const float *prof = raw + ((size_t)s * nchan + c) * n;
+                double w = (double)W[(size_t)s * nchan + c];
+                float b = base[(size_t)s * nchan + c];
+                wpart = wpart + w;
+                for (int i = 0; i < n; ++i) {
+                    float y = ded_at(prof, n, shift[c], i) - b;
+                    part[i] = part[i] + w * (double)y;
+                }
+            }
+            wsum = wsum + wpart;
+            for (int i = 0; i < n; ++i) num[i] = num[i] + part[i];
+        }
+        for (int i = 0; i < n; ++i) F[(size_t)s * n + i] = (wsum != 0.0) ? (float)(num[i] / wsum) : 0.0f;
+        wf[s] = (float)wsum;
+    }
+    double wt = 0.0;
+    for (int i = 0; i < n; ++i) num[i] = 0.0;
+    for (int s = 0; s < nsub; ++s) {
+        double w = (double)wf[s];
+        wt = wt + w;
+        for (int i = 0; i < n; ++i) num[i] = num[i] + w * (double)F[(size_t)s * n + i];
+    }
+    for (int i = 0; i < n; ++i) {
+        float t = (wt != 0.0) ? (float)(num[i] / wt) : 0.0f;
+        T[i] = t * 10000.0f;
+    }
+    free(base); free(num); free(part); free(F); free(wf);
+}
+
+/* ------------------------------------------------------ pairwise sums */
+static float pw_f32(const float *a, int n, int stride)
+{
+    if (n < 8) {
+        float res = 0.0f;
+        for (int i = 0; i < n; ++i) res += a[(size_t)i * stride];
+        return res;
+    } else if (n <= 128) {
+        float r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[(size_t)j * stride];
+        int i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[(size_t)(i + j) * stride];
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[(size_t)i * stride];
+        return res;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw_f32(a, n2, stride) + pw_f32(a + (size_t)n2 * stride, n - n2, stride);
+}
+
+static double pw_f64(const double *a, int n)
+{
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; ++i) res += a[i];
+        return res;
+    } else if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw_f64(a, n2) + pw_f64(a + n2, n - n2);
+}
+
+float orc_sum_f32(const float *a, int n) { return 0.0f + pw_f32(a, n, 1); }
+double orc_sum_f64(const double *a, int n) { return 0.0 + pw_f64(a, n); }
+
+/* ------------------------------------------------------------ fft max */
+/* max_k |DFT(x)_k| for k = 0..n/2 (np.fft.rfft magnitude; tolerance-level
+ * agreement with pocketfft).  Radix-2 iterative for powers of two, direct
+ * DFT otherwise.  work: 4*n doubles. */
+static double fftmax(const double *x, int n, double *work)
+{
+    double best = 0.0;
+    int pow2 = n > 0 && (n & (n - 1)) == 0;
+    if (n == 1) return fabs(x[0]);
+    if (pow2) {
+        double *re = work, *im = work + n;
+        int lg = 0;
+        while ((1 << lg) < n) ++lg;
+        for (int i = 0; i < n; ++i) {
+            int rv = 0;
+            for (int b = 0; b < lg; ++b) rv |= ((i >> b) & 1) << (lg - 1 - b);
+            re[rv] = x[i];
+            im[rv] = 0.0;
+        }
+        for (int len = 2; len <= n; len <<= 1) {
+            int half = len >> 1;
+            int step = n / len;
+            for (int st = 0; st < n; st += len)
+                for (int k = 0; k < half; ++k) {
+                    /* twiddle exp(-2 pi i k/len) = exp(-2 pi i (k*step)/n) */
+                    int idx = k * step;
+                    double c = cos(2.0 * M_PI * (double)idx / (double)n);
+                    double s = -sin(2.0 * M_PI * (double)idx / (double)n);
+                    double ur = re[st + k], ui = im[st + k];
+                    double vr = re[st + k + half] * c - im[st + k + half] * s;
+                    double vi = re[st + k + half] * s + im[st + k + half] * c;
+                    re[st + k] = ur + vr; im[st + k] = ui + vi;
+                    re[st + k + half] = ur - vr; im[st + k + half] = ui - vi;
+                }
+        }
+        for (int k = 0; k <= n / 2; ++k) {
+            double a = hypot(re[k], im[k]);
+            if (isnan(a)) return a;
+            if (a > best) best = a;
+        }
+        return best;
+    }
+    for (int k = 0; k <= n / 2; ++k) {
+        double sr = 0.0, si = 0.0;
+        for (int j = 0; j < n; ++j) {
+            long q = ((long)k * j) % n;
+            double ang = 2.0 * M_PI * (double)q / (double)n;
+            sr += x[j] * cos(ang);
+            si -= x[j] * sin(ang);
+        }
+        double a = hypot(sr, si);
+        if (isnan(a)) return a;
+        if (a > best) best = a;
+    }
+    return best;
+}
+
+/* ----------------------------------------------------- diagnostics */
+/* X: weighted cube (P, n) f32, dispersed frame; valid (P).
+ * std/mean/fft f64, ptp f32, with numpy.ma data conventions. */
+void orc_diagnostics(int P, int n, const float *X, const uint8_t *valid,
+                     double *std_o, double *mean_o, float *ptp_o, double *fft_o)
+{
+    double *d = (double *)malloc(sizeof(double) * (size_t)n);
+    double *sq = (double *)malloc(sizeof(double) * (size_t)n);
+    double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
+    for (int k = 0; k < P; ++k) {
+        const float *x = X + (size_t)k * n;
+        if (!valid[k]) {
+            std_o[k] = 0.0;
+            mean_o[k] = 0.0;
+            ptp_o[k] = 1e20f;
+            for (int i = 0; i < n; ++i) d[i] = (double)x[i];
+            fft_o[k] = fftmax(d, n, work);
+            continue;
+        }
+        float s32 = orc_sum_f32(x, n);
+        double mean = (double)s32 / (double)n;
+        for (int i = 0; i < n; ++i) {
+            d[i] = (double)x[i] - mean;
+            sq[i] = d[i] * d[i];
+        }
+        double var = orc_sum_f64(sq, n) / (double)n;
+        float mx = x[0], mn = x[0];
+        int nan = 0;
+        for (int i = 0; i < n; ++i) {
+            if (isnan(x[i])) nan = 1;
+            if (x[i] > mx) mx = x[i];
+            if (x[i] < mn) mn = x[i];
+        }
+        std_o[k] = sqrt(var);
+        mean_o[k] = mean;
+        ptp_o[k] = nan ? NAN : (mx - mn);
+        fft_o[k] = fftmax(d, n, work);
+    }
+    free(d); free(sq); free(work);
+}
+
+/* ------------------------------------------------------ medians + scalers */
+static int cmp_d(const void *a, const void *b)
+{
+    double x = *(const double *)a, y = *(const double *)b;
+    return (x > y) - (x < y);
+}
+static int cmp_f(const void *a, const void *b)
+{
+    float x = *(const float *)a, y = *(const float *)b;
+    return (x > y) - (x < y);
+}
+
+/* median of cnt values (no NaN) already sorted, numpy arithmetic in dtype */
+static double mid_median_d(const double *s, int cnt)
+{
+    int idx = cnt / 2;
+    if (cnt % 2) return 0.0 + s[idx];
+    double t = (0.0 + s[idx - 1]) + s[idx];
+    return t / 2.0;
+}
+static float mid_median_f(const float *s, int cnt)
+{
+    int idx = cnt / 2;
+    if (cnt % 2) return 0.0f + s[idx];
+    float t = (0.0f + s[idx - 1]) + s[idx];
+    return t / 2.0f;
+}
+
+/* One line of a masked f64 diagnostic: out[i] = final scaled value. */
+static void scale_line_masked_d(int len, const double *d, const uint8_t *valid, int vstride,
+                                int dstride, double thr, double *out, int ostride, double *buf)
+{
+    const double tiny = DBL_MIN;
+    int cnt = 0, nan = 0;
+    for (int i = 0; i < len; ++i)
+        if (valid[(size_t)i * vstride]) {
+            double v = d[(size_t)i * dstride];
+            if (isnan(v)) nan = 1;
+            buf[cnt++] = v;
+        }
+    double med = NAN, mad = NAN;
+    if (cnt > 0) {
+        if (!nan) {
+            qsort(buf, (size_t)cnt, sizeof(double), cmp_d);
+            med = mid_median_d(buf, cnt);
+        }
+        int c2 = 0, nan2 = 0;
+        for (int i = 0; i < len; ++i)
+            if (valid[(size_t)i * vstride]) {
+                double r = d[(size_t)i * dstride] - med;
+                double a = fabs(r);
+                if (isnan(a)) nan2 = 1;
+                buf[c2++] = a;
+            }
+        if (!nan2) {
+            qsort(buf, (size_t)c2, sizeof(double), cmp_d);
+            mad = mid_median_d(buf, c2);
+        }
+    }
+    for (int i = 0; i < len; ++i) {
+        double dv = d[(size_t)i * dstride];
+        double v;
+        if (!valid[(size_t)i * vstride]) {
+            v = 0.0 + fabs(dv);
+        } else {
+            double r = dv - med;
+            double q = r / mad;
+            int dom = !isfinite(q) || (fabs(r) * tiny >= fabs(mad));
+            if (dom) {
+                v = 0.0 + fabs(0.0 + r);
+            } else {
+                double a = fabs(q);
+                double res = a / thr;
+                if (!isfinite(res) || a * tiny >= fabs(thr)) v = 0.0 + a;
+                else v = res;
+            }
+        }
+        out[(size_t)i * ostride] = v;
+    }
+}
+
+static void scale_line_masked_f(int len, const float *d, const uint8_t *valid, int vstride,
+                                int dstride, double thr, double *out, int ostride, float *buf)
+{
+    const double tiny = DBL_MIN;
+    int cnt = 0, nan = 0;
+    for (int i = 0; i < len; ++i)
+        if (valid[(size_t)i * vstride]) {
+            float v = d[(size_t)i * dstride];
+            if (isnan(v)) nan = 1;
+            buf[cnt++] = v;
+        }
+    float med = NAN, mad = NAN;
+    if (cnt > 0) {
+        if (!nan) {
+            qsort(buf, (size_t)cnt, sizeof(float), cmp_f);
+            med = mid_median_f(buf, cnt);
+        }
+        int c2 = 0, nan2 = 0;
+        for (int i = 0; i < len; ++i)
+            if (valid[(size_t)i * vstride]) {
+                float r = d[(size_t)i * dstride] - med;
+                float a = fabsf(r);
+                if (isnan(a)) nan2 = 1;
+                buf[c2++] = a;
+            }
+        if (!nan2) {
+            qsort(buf, (size_t)c2, sizeof(float), cmp_f);
+            mad = mid_median_f(buf, c2);
+        }
+    }
+    for (int i = 0; i < len; ++i) {
+        float dv = d[(size_t)i * dstride];
+        double v;
+        if (!valid[(size_t)i * vstride]) {
+            v = 0.0 + (double)fabsf(dv);
+        } else {
+            float r = dv - med;
+            float q = r / mad;
+            int dom = !isfinite(q) || ((double)fabsf(r) * tiny >= (double)fabsf(mad));
+            if (dom) {
+                v = 0.0 + (double)fabsf(0.0f + r);
+            } else {
+                float a = fabsf(q);
+                double res = (double)a / thr;
+                if (!isfinite(res) || (double)a * tiny >= fabs(thr)) v = 0.0 + (double)a;
+                else v = res;
+            }
+        }
+        out[(size_t)i * ostride] = v;
+    }
+}
+
+static void scale_line_plain(int len, const double *d, int dstride, double thr,
+                             double *out, int ostride, double *buf)
+{
+    int nan = 0;
+    for (int i = 0; i < len; ++i) {
+        buf[i] = d[(size_t)i * dstride];
+        if (isnan(buf[i])) nan = 1;
+    }
+    double med = NAN, mad = NAN;
+    if (!nan) {
+        qsort(buf, (size_t)len, sizeof(double), cmp_d);
+        med = mid_median_d(buf, len);
+    }
+    int nan2 = 0;
+    for (int i = 0; i < len; ++i) {
+        buf[i] = fabs(d[(size_t)i * dstride] - med);
+        if (isnan(buf[i])) nan2 = 1;
+    }
+    if (!nan2) {
+        qsort(buf, (size_t)len, sizeof(double), cmp_d);
+        mad = mid_median_d(buf, len);
+    }
+    for (int i = 0; i < len; ++i) {
+        double r = d[(size_t)i * dstride] - med;
+        double q = r / mad;
+        out[(size_t)i * ostride] = fabs(q) / thr;
+    }
+}
+
+static double nanmax2(double a, double b)
+{
+    if (isnan(a) || isnan(b)) return NAN;
+    return a > b ? a : b;
+}
+
+/* scalers + combine: test (nsub*nchan) from the 4 diagnostics. */
+void orc_test(int nsub, int nchan, const uint8_t *valid, const double *std_d,
+              const double *mean_d, const float *ptp_d, const double *fft_d,
+              double chanthresh, double subintthresh, double *test)
+{
+    size_t P = (size_t)nsub * nchan;
+    int L = nsub > nchan ? nsub : nchan;
+    double *ch = (double *)malloc(sizeof(double) * P);
+    double *sb = (double *)malloc(sizeof(double) * P);
+    double *S = (double *)malloc(sizeof(double) * 4 * P);
+    double *bufd = (double *)malloc(sizeof(double) * (size_t)L);
+    float *buff = (float *)malloc(sizeof(float) * (size_t)L);
+    for (int which = 0; which < 4; ++which) {
+        for (int c = 0; c < nchan; ++c) {
+            if (which == 0) scale_line_masked_d(nsub, std_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, bufd);
+            if (which == 1) scale_line_masked_d(nsub, mean_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, bufd);
+            if (which == 2) scale_line_masked_f(nsub, ptp_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, buff);
+            if (which == 3) scale_line_plain(nsub, fft_d + c, nchan, chanthresh, ch + c, nchan, bufd);
+        }
+        for (int s = 0; s < nsub; ++s) {
+            size_t o = (size_t)s * nchan;
+            if (which == 0) scale_line_masked_d(nchan, std_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, bufd);
+            if (which == 1) scale_line_masked_d(nchan, mean_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, bufd);
+            if (which == 2) scale_line_masked_f(nchan, ptp_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, buff);
+            if (which == 3) scale_line_plain(nchan, fft_d + o, 1, subintthresh, sb + o, 1, bufd);
+        }
+        for (size_t k = 0; k < P; ++k) S[which * P + k] = nanmax2(ch[k], sb[k]);
+    }
+    for (size_t k = 0; k < P; ++k) {
+        double v[4] = {S[k], S[P + k], S[2 * P + k], S[3 * P + k]};
+        if (isnan(v[0]) || isnan(v[1]) || isnan(v[2]) || isnan(v[3])) { test[k] = NAN; continue; }
+        qsort(v, 4, sizeof(double), cmp_d);
+        test[k] = ((0.0 + v[1]) + v[2]) / 2.0;
+    }
+    free(ch); free(sb); free(S); free(bufd); free(buff);
+}
+
+/* --------------------------------------------------------- the loop */
+typedef struct {
+    int32_t nsub, nchan, nbin, max_iter;
+    double chanthresh, subintthresh;
+    int32_t pr_on;
+    double pr_factor;
+    int32_t pr_start, pr_end;
+    double baseline_duty;
+} orc_params;
+
+/* One full clean loop (iterative_cleaner.py:83-146).
+ * raw: pscrunched cube (nsub,nchan,nbin) dispersed frame; w0 weights.
+ * Outputs: test (P), weights (P), loops, changed[max_iter], nzero[max_iter];
+ * optional (may be NULL): R_last (P*nbin, dispersed frame, unweighted),
+ * T_all (max_iter*nbin), amp_last/info_last (P),
+ * diag_last: std, mean (P f64), ptp (P f32), fft (P f64). */
+int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, const int32_t *shift,
+                   double *test, float *weights, int32_t *loops_out, int32_t *changed,
+                   int32_t *nzero, float *R_last, float *T_all, double *amp_last,
+                   int32_t *info_last, double *std_l, double *mean_l, float *ptp_l, double *fft_l)
+{
+    const int nsub = pp->nsub, nchan = pp->nchan, n = pp->nbin;
+    const size_t P = (size_t)nsub * nchan, N = P * (size_t)n;
+    float *D = (float *)malloc(sizeof(float) * N);
+    float *Rd = (float *)malloc(sizeof(float) * N);
+    float *X = (float *)malloc(sizeof(float) * N);
+    float *T = (float *)malloc(sizeof(float) * (size_t)n);
+    double *amp = (double *)malloc(sizeof(double) * P);
+    int32_t *info = (int32_t *)malloc(sizeof(int32_t) * P);
+    double *sd = (double *)malloc(sizeof(double) * P), *mn = (double *)malloc(sizeof(double) * P);
+    float *pt = (float *)malloc(sizeof(float) * P);
+    double *ff = (double *)malloc(sizeof(double) * P);
+    uint8_t *valid = (uint8_t *)malloc(P);
+    int maxit = pp->max_iter;
+    float *hist = (float *)malloc(sizeof(float) * P * (size_t)(maxit + 1));
+    float *Wcur = (float *)malloc(sizeof(float) * P);
+    for (size_t k = 0; k < P; ++k) valid[k] = (w0[k] != 0.0f);
+    memcpy(hist, w0, sizeof(float) * P);
+    memcpy(Wcur, w0, sizeof(float) * P);
+    int nhist = 1;
+    orc_fit_cube(nsub, nchan, n, raw, w0, shift, pp->baseline_duty, D);
+    int x = 0, loops = -1;
+    while (x < maxit) {
+        x += 1;
+        orc_template(nsub, nchan, n, raw, Wcur, shift, pp->baseline_duty, T);
+        if (T_all) memcpy(T_all + (size_t)(x - 1) * n, T, sizeof(float) * (size_t)n);
+        orc_fit_residual((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
+        /* dededisperse + apply_weights */
+        for (int s = 0; s < nsub; ++s)
+            for (int c = 0; c < nchan; ++c) {
+                size_t k = (size_t)s * nchan + c;
+                const float *r = Rd + k * n;
+                float *o = X + k * n;
+                float w = w0[k];
+                int sh = shift[c];
+                for (int j = 0; j < n; ++j) {
+                    int i = j - sh;
+                    if (i < 0) i += n;
+                    o[j] = r[i] * w;
+                }
+            }
+        orc_diagnostics((int)P, n, X, valid, sd, mn, pt, ff);
+        orc_test(nsub, nchan, valid, sd, mn, pt, ff, pp->chanthresh, pp->subintthresh, test);
+        int ndiff = 0, nz = 0;
+        for (size_t k = 0; k < P; ++k) {
+            float w = (test[k] >= 1.0) ? 0.0f : w0[k];
+            if (w != hist[(size_t)(nhist - 1) * P + k]) ++ndiff;
+            if (w == 0.0f) ++nz;
+            Wcur[k] = w;
+        }
+        changed[x - 1] = ndiff;
+        nzero[x - 1] = nz;
+        for (int h = 0; h < nhist; ++h) {
+            int eq = 1;
+            for (size_t k = 0; k < P && eq; ++k) if (!(Wcur[k] == hist[(size_t)h * P + k])) eq = 0;
+            if (eq) { loops = x; x = 1000000; }
+        }
+        memcpy(hist + (size_t)nhist * P, Wcur, sizeof(float) * P);
+        ++nhist;
+    }
+    if (x == maxit) loops = maxit;
+    memcpy(weights, Wcur, sizeof(float) * P);
+    if (R_last) {
+        /* dededispersed residual, unweighted (ic.py:104-108) */
+        for (int s = 0; s < nsub; ++s)
+            for (int c = 0; c < nchan; ++c) {
+                size_t k = (size_t)s * nchan + c;
+                for (int j = 0; j < n; ++j) {
+                    int i = j - shift[c];
+                    if (i < 0) i += n;
+                    R_last[k * n + j] = Rd[k * n + i];
+                }
+            }
+    }
+    if (amp_last) memcpy(amp_last, amp, sizeof(double) * P);
+    if (info_last) memcpy(info_last, info, sizeof(int32_t) * P);
+    if (std_l) memcpy(std_l, sd, sizeof(double) * P);
+    if (mean_l) memcpy(mean_l, mn, sizeof(double) * P);
+    if (ptp_l) memcpy(ptp_l, pt, sizeof(float) * P);
+    if (fft_l) memcpy(fft_l, ff, sizeof(double) * P);
+    *loops_out = loops;
+    free(D); free(Rd); free(X); free(T); free(amp); free(info); free(sd); free(mn);
+    free(pt); free(ff); free(valid); free(hist); free(Wcur);
+    return 0;
+}

@@ -1,0 +1,388 @@
+#!/usr/bin/env python
+"""Generate golden fixtures by running the REFERENCE implementation.
+
+Runs only in the build container (``/root/reference`` is absent on the GPU
+box).  The reference ``iterative_cleaner.py`` is imported with a stub
+``psrchive`` module whose ``Archive_load`` is this repo's NumPy stand-in
+(``iterative_cleaner_amd.archive``); nothing of the reference is copied.
+Its own functions are instrumented (wrapped, not modified) to record the
+per-iteration intermediates of ``clean()`` (iterative_cleaner.py:65-178):
+
+  T (template, :94), leastsq (x, info) per profile (:278), the f32
+  residual cube (:101), the weighted masked cube's diagnostics
+  (:206-217), channel/subint-scaled diagnostics (:222-223), test (:225),
+  weights after set_weights_archive (:125), loops and stdout.
+
+Also recorded: direct calls of ``comprehensive_stats`` on edge-case inputs
+and of ``scipy.optimize.leastsq`` through ``remove_profile1d`` on edge-case
+profiles.  Output: ``tests/golden/*.npz`` (plain arrays, no pickles).
+
+usage: python tests/golden/make_golden.py [--out tests/golden]
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import hashlib
+import io
+import json
+import os
+import sys
+import tempfile
+import types
+
+sys.dont_write_bytecode = True
+os.environ.setdefault("MPLBACKEND", "Agg")
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+import numpy as np                                   # noqa: E402
+import scipy.optimize                                # noqa: E402
+
+from iterative_cleaner_amd import archive as ica     # noqa: E402
+from iterative_cleaner_amd import synth              # noqa: E402
+
+REF_DIR = "/root/reference"
+
+
+def import_reference():
+    stub = types.ModuleType("psrchive")
+    stub.Archive_load = ica.Archive_load
+    sys.modules["psrchive"] = stub
+    if REF_DIR not in sys.path:
+        sys.path.insert(0, REF_DIR)
+    import iterative_cleaner as ic  # noqa: WPS433  (reference, read-only)
+    return ic
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def ref_args(ic, extra=()):
+    old = sys.argv
+    try:
+        sys.argv = ["iterative_cleaner.py", "dummy.ar", *extra]
+        return ic.parse_arguments()
+    finally:
+        sys.argv = old
+
+
+class Recorder:
+    """Wrap the reference's own functions to capture intermediates."""
+
+    def __init__(self, ic):
+        self.ic = ic
+        self.iters = []
+        self._cur = None
+        self._orig = {}
+
+    def __enter__(self):
+        ic = self.ic
+        for name in ("remove_profile_inplace", "comprehensive_stats",
+                     "set_weights_archive", "channel_scaler", "subint_scaler"):
+            self._orig[name] = getattr(ic, name)
+        self._orig["leastsq"] = scipy.optimize.leastsq
+        rec = self
+
+        def leastsq(func, x0, *a, **k):
+            res = rec._orig["leastsq"](func, x0, *a, **k)
+            if rec._cur is not None:
+                rec._cur["amp"].append(float(np.asarray(res[0])[0]))
+                rec._cur["info"].append(int(res[1]))
+            return res
+
+        def remove_profile_inplace(ar, template, pulse_region):
+            rec._cur = {"T": np.array(template, dtype=np.float32), "amp": [], "info": []}
+            out = rec._orig["remove_profile_inplace"](ar, template, pulse_region)
+            rec._cur["residual_ded"] = ar.get_data()[:, 0].copy()
+            return out
+
+        def comprehensive_stats(data, args, axis):
+            cur = rec._cur
+            cur["X"] = np.ma.getdata(data).copy()
+            cur["X_mask"] = np.ma.getmaskarray(data)[:, :, 0].copy()
+            diags = [np.ma.std(data, axis=2), np.ma.mean(data, axis=2),
+                     np.ma.ptp(data, axis=2),
+                     np.max(np.abs(np.fft.rfft(
+                         data - np.expand_dims(data.mean(axis=2), axis=2), axis=2)), axis=2)]
+            for nm, d in zip(("std", "mean", "ptp", "fft"), diags):
+                cur["diag_" + nm] = np.ma.getdata(d).copy()
+                cur["diag_" + nm + "_mask"] = np.ma.getmaskarray(d).copy()
+                cs = rec._orig["channel_scaler"](d)
+                ss = rec._orig["subint_scaler"](d)
+                cur["chan_" + nm] = np.ma.getdata(cs).copy()
+                cur["sub_" + nm] = np.ma.getdata(ss).copy()
+            out = rec._orig["comprehensive_stats"](data, args, axis)
+            cur["test"] = np.asarray(out).copy()
+            return out
+
+        def set_weights_archive(archive, test_results):
+            out = rec._orig["set_weights_archive"](archive, test_results)
+            if rec._cur is not None and "test" in rec._cur and "weights" not in rec._cur:
+                rec._cur["weights"] = archive.get_weights().copy()
+                rec.iters.append(rec._cur)
+                rec._cur = None
+            return out
+
+        ic.remove_profile_inplace = remove_profile_inplace
+        ic.comprehensive_stats = comprehensive_stats
+        ic.set_weights_archive = set_weights_archive
+        scipy.optimize.leastsq = leastsq
+        return self
+
+    def __exit__(self, *exc):
+        for name, fn in self._orig.items():
+            if name == "leastsq":
+                scipy.optimize.leastsq = fn
+            else:
+                setattr(self.ic, name, fn)
+        return False
+
+
+def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
+                   keep_cubes=True, npol=1, workdir=None, out_dir=HERE):
+    data, weights, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi, npol=npol)
+    path = os.path.join(workdir, "%s.ar" % name)
+    ar = ica.Archive(data, weights, shift, filename=path)
+    ar.unload(path)
+    ar = ica.Archive_load(path)
+    args = ref_args(ic, ["-l", *extra_args])
+    buf = io.StringIO()
+    cwd = os.getcwd()
+    os.chdir(workdir)
+    try:
+        with Recorder(ic) as rec, contextlib.redirect_stdout(buf):
+            out_ar = ic.clean(ar, args, path)
+    finally:
+        os.chdir(cwd)
+    stdout = buf.getvalue()
+    loops = None
+    for line in stdout.splitlines():
+        if line.startswith("RFI removal stops after"):
+            loops = int(line.split()[-2])
+        if line.startswith("Cleaning was interrupted"):
+            loops = int(line.split("(")[-1].rstrip(")"))
+    arrays = {
+        "input_sha256": np.array(sha(data)),
+        "final_weights": out_ar.get_weights(),
+        "stdout": np.array(stdout),
+        "n_iter": np.array(len(rec.iters)),
+        "loops": np.array(loops if loops is not None else -1),
+        "meta": np.array(json.dumps({
+            "name": name, "nsub": nsub, "nchan": nchan, "nbin": nbin, "seed": seed,
+            "rfi": rfi, "npol": npol, "extra_args": list(extra_args),
+            "args": {k: v for k, v in vars(args).items() if k != "archive"},
+            "numpy": np.__version__, "scipy": scipy.__version__})),
+    }
+    for k, it in enumerate(rec.iters, start=1):
+        arrays["T_%d" % k] = it["T"]
+        arrays["amp_%d" % k] = np.array(it["amp"], dtype=np.float64)
+        arrays["info_%d" % k] = np.array(it["info"], dtype=np.int32)
+        arrays["test_%d" % k] = it["test"]
+        arrays["weights_%d" % k] = it["weights"]
+        for nm in ("std", "mean", "ptp", "fft"):
+            arrays["diag_%s_%d" % (nm, k)] = it["diag_" + nm]
+            arrays["diag_%s_mask_%d" % (nm, k)] = it["diag_" + nm + "_mask"]
+            if keep_cubes:
+                arrays["chan_%s_%d" % (nm, k)] = it["chan_" + nm]
+                arrays["sub_%s_%d" % (nm, k)] = it["sub_" + nm]
+        if keep_cubes and k == 1:
+            arrays["residual_ded_%d" % k] = it["residual_ded"]
+            arrays["X_%d" % k] = it["X"]
+        else:
+            arrays["residual_ded_sha_%d" % k] = np.array(sha(it["residual_ded"]))
+            arrays["X_sha_%d" % k] = np.array(sha(it["X"]))
+    fn = os.path.join(out_dir, "clean_%s.npz" % name)
+    np.savez_compressed(fn, **arrays)
+    print("wrote %s  iters=%d loops=%s" % (fn, len(rec.iters), loops))
+
+
+def stats_cases(rng):
+    """Edge-case inputs for comprehensive_stats (iterative_cleaner.py:181-226)."""
+    cases = []
+    for ci in range(24):
+        nsub = int(rng.integers(3, 14))
+        nchan = int(rng.integers(4, 30))
+        nbin = int(rng.choice([8, 16, 24, 64, 100, 128, 136, 256]))
+        X = rng.standard_normal((nsub, nchan, nbin)).astype(np.float32)
+        X *= np.float32(10.0 ** rng.uniform(-3, 3))
+        w = np.ones((nsub, nchan), np.float32)
+        kind = ci % 8
+        if kind == 1:      # zero-weight channels and subints
+            w[:, rng.integers(0, nchan)] = 0
+            w[rng.integers(0, nsub), :] = 0
+        if kind == 2:      # dead all-zero channel with weight 1
+            X[:, rng.integers(0, nchan), :] = 0
+        if kind == 3:      # fractional weights
+            w = rng.choice([0.0, 0.25, 0.5, 1.0, 1.5], size=(nsub, nchan)).astype(np.float32)
+        if kind == 4:      # many identical profiles -> MAD == 0 lines
+            X[:, :, :] = X[0:1, 0:1, :]
+            X[rng.integers(0, nsub), rng.integers(0, nchan)] += 3
+        if kind == 5:      # strong RFI outliers
+            X[rng.integers(0, nsub, 4), rng.integers(0, nchan, 4)] *= 50
+        if kind == 6:      # more than half of a channel zero-weight
+            c = rng.integers(0, nchan)
+            w[: nsub // 2 + 1, c] = 0
+        if kind == 7:      # quantised data (ties in medians)
+            X = np.round(X * 2) / 2
+            X = X.astype(np.float32)
+        thr = [(5, 5), (3.0, 3.0), (1.5, 4.0), (5, 2.5)][ci % 4]
+        cases.append((X, w, thr))
+    return cases
+
+
+def run_stats_cases(ic, out_dir=HERE):
+    rng = np.random.default_rng(12345)
+    arrays = {}
+    for i, (X, w, (ct, st)) in enumerate(stats_cases(rng)):
+        args = argparse.Namespace(chanthresh=ct, subintthresh=st)
+        data = X.copy()
+        data = ic.apply_weights(data, w)
+        mask = np.bitwise_not(np.expand_dims(w, 2).astype(bool)).repeat(X.shape[2], axis=2)
+        mdata = np.ma.masked_array(data, mask=mask)
+        with np.errstate(all="ignore"):
+            test = ic.comprehensive_stats(mdata, args, axis=2)
+        arrays["X_%d" % i] = X
+        arrays["w_%d" % i] = w
+        arrays["thr_%d" % i] = np.array([ct, st], dtype=np.float64)
+        arrays["thr_is_int_%d" % i] = np.array([isinstance(ct, int), isinstance(st, int)])
+        arrays["test_%d" % i] = np.asarray(test)
+    arrays["n"] = np.array(len(stats_cases(np.random.default_rng(12345))))
+    fn = os.path.join(out_dir, "stats_cases.npz")
+    np.savez_compressed(fn, **arrays)
+    print("wrote", fn)
+
+
+def leastsq_cases(rng):
+    cases = []
+    for nbin in (64, 128, 256, 1024, 4096):
+        reps = {64: 60, 128: 60, 256: 60, 1024: 20, 4096: 8}[nbin]
+        phase = (np.arange(nbin) + 0.5) / nbin
+        pulse = np.exp(-0.5 * ((phase - 0.3) / 0.02) ** 2)
+        for r in range(reps):
+            T = (pulse * 10000 * rng.gamma(2, 0.5)).astype(np.float32)
+            p = (rng.gamma(2, 0.5) * pulse + rng.standard_normal(nbin)).astype(np.float32)
+            kind = r % 12
+            if kind == 1: p = np.zeros(nbin, np.float32)
+            if kind == 2: T = np.zeros(nbin, np.float32)
+            if kind == 3: p = np.full(nbin, 3.25, np.float32)
+            if kind == 4: p = (T * np.float32(rng.uniform(-2, 2))).astype(np.float32)
+            if kind == 5: p = (p * np.float32(10.0 ** rng.uniform(-6, 6))).astype(np.float32)
+            if kind == 6: T = (T * np.float32(10.0 ** rng.uniform(-6, 6))).astype(np.float32)
+            if kind == 7: p = (T * np.float32(1e-7) + p * np.float32(1e-12)).astype(np.float32)
+            if kind == 8: T = rng.standard_normal(nbin).astype(np.float32)
+            if kind == 9: p[rng.integers(0, nbin, 5)] += 1e4
+            if kind == 10: T = (T - T.mean()).astype(np.float32)
+            if kind == 11:
+                T = np.zeros(nbin, np.float32)
+                T[rng.integers(0, nbin)] = 1.0
+            cases.append((T, p))
+    return cases
+
+
+def run_leastsq_cases(ic, out_dir=HERE):
+    rng = np.random.default_rng(777)
+    Ts, ps, xs, infos, resid = [], [], [], [], []
+    for T, p in leastsq_cases(rng):
+        rec = {}
+        orig = scipy.optimize.leastsq
+
+        def spy(func, x0, *a, **k):
+            res = orig(func, x0, *a, **k)
+            rec["x"], rec["info"] = float(np.asarray(res[0])[0]), int(res[1])
+            return res
+        scipy.optimize.leastsq = spy
+        try:
+            with contextlib.redirect_stdout(io.StringIO()), np.errstate(all="ignore"):
+                _, r = ic.remove_profile1d(p, 0, 0, T, [0, 0, 1])
+        finally:
+            scipy.optimize.leastsq = orig
+        Ts.append(T); ps.append(p); xs.append(rec["x"]); infos.append(rec["info"])
+        resid.append(np.asarray(r, dtype=np.float64))
+    arrays = {"x": np.array(xs), "info": np.array(infos, np.int32)}
+    sizes = np.array([len(t) for t in Ts])
+    arrays["nbin"] = sizes
+    arrays["T"] = np.concatenate(Ts)
+    arrays["p"] = np.concatenate(ps)
+    arrays["resid"] = np.concatenate(resid)
+    fn = os.path.join(out_dir, "leastsq_cases.npz")
+    np.savez_compressed(fn, **arrays)
+    print("wrote %s (%d profiles)" % (fn, len(xs)))
+
+
+def run_pulse_region_case(ic, out_dir=HERE):
+    """remove_profile1d with an active pulse region (K6: (factor, start, end))."""
+    rng = np.random.default_rng(4242)
+    nbin = 128
+    T = (np.exp(-0.5 * (((np.arange(nbin) + .5) / nbin - .3) / .02) ** 2) * 1e4).astype(np.float32)
+    p = (0.7 * T / 1e4 + rng.standard_normal(nbin)).astype(np.float32)
+    out = {}
+    for i, pr in enumerate(([0.5, 30.0, 50.0], [0.0, 10.0, 20.0], [2.0, 100.0, 300.0])):
+        with contextlib.redirect_stdout(io.StringIO()):
+            _, r = ic.remove_profile1d(p, 0, 0, T, pr)
+        out["pr_%d" % i] = np.array(pr)
+        out["resid_%d" % i] = np.asarray(r, dtype=np.float64)
+    out["T"], out["p"] = T, p
+    fn = os.path.join(out_dir, "pulse_region_cases.npz")
+    np.savez_compressed(fn, **out)
+    print("wrote", fn)
+
+
+def run_cli_case(ic, out_dir=HERE):
+    """main() end to end: output naming, final weights, bad parts, log/no-log."""
+    with tempfile.TemporaryDirectory() as wd:
+        data, weights, shift = synth.make_cube(10, 40, 128, 21, 0.2)
+        path = os.path.join(wd, "cli.ar")
+        ica.Archive(data, weights, shift, filename=path).unload(path)
+        buf = io.StringIO()
+        old = sys.argv
+        cwd = os.getcwd()
+        os.chdir(wd)
+        try:
+            sys.argv = ["iterative_cleaner.py", "-l", "--bad_chan", "0.3",
+                        "--bad_subint", "0.3", "-c", "3", "-s", "3", path]
+            with contextlib.redirect_stdout(buf):
+                ic.main(ic.parse_arguments())
+        finally:
+            sys.argv = old
+            os.chdir(cwd)
+        outp = os.path.join(wd, "cli_cleaned.ar")
+        out_ar = ica.Archive_load(outp)
+        np.savez_compressed(os.path.join(out_dir, "cli_case.npz"),
+                            weights=out_ar.get_weights(),
+                            stdout=np.array(buf.getvalue().replace(wd, "<WD>")),
+                            input_sha256=np.array(sha(data)))
+        print("wrote cli_case.npz")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=HERE)
+    ap.add_argument("--skip-big", action="store_true")
+    a = ap.parse_args()
+    ic = import_reference()
+    with tempfile.TemporaryDirectory() as wd:
+        run_clean_case(ic, "s12x48x128", 12, 48, 128, 3, 0.05, workdir=wd, out_dir=a.out)
+        run_clean_case(ic, "s16x64x256_rfi30", 16, 64, 256, 4, 0.30, workdir=wd, out_dir=a.out)
+        run_clean_case(ic, "s10x40x100_thr3", 10, 40, 100, 7, 0.2,
+                       extra_args=("-c", "3", "-s", "3", "-m", "7"), workdir=wd, out_dir=a.out)
+        run_clean_case(ic, "s8x32x64_pol4", 8, 32, 64, 8, 0.2, npol=4,
+                       extra_args=("-p",), workdir=wd, out_dir=a.out)
+        run_clean_case(ic, "s12x40x128_pr", 12, 40, 128, 9, 0.1,
+                       extra_args=("-r", "0.5", "30", "50"), workdir=wd, out_dir=a.out)
+        if not a.skip_big:
+            run_clean_case(ic, "C1", 64, 256, 256, 0, 0.05, keep_cubes=False,
+                           workdir=wd, out_dir=a.out)
+            run_clean_case(ic, "s64x256x256_rfi30", 64, 256, 256, 0, 0.30, keep_cubes=False,
+                           workdir=wd, out_dir=a.out)
+    run_stats_cases(ic, a.out)
+    run_leastsq_cases(ic, a.out)
+    run_pulse_region_case(ic, a.out)
+    run_cli_case(ic, a.out)
+
+
+if __name__ == "__main__":
+    main()
