@@ -1,0 +1,249 @@
+"""Drop-in host for the surgical RFI cleaner: same CLI, same ``clean(ar, args,
+arch)``, same prints, log and files as the reference
+(/root/reference/iterative_cleaner.py), with the cleaning loop
+(iterative_cleaner.py:83-146) executed by libicgpu.so on an MI355X.
+
+Reference map
+  parse_arguments  iterative_cleaner.py:16-42   (flags and defaults kept,
+                   including the int default 5 of -c/-s and the -r order
+                   (factor, start, end) used at :281-283)
+  main             :45-62
+  clean            :65-178
+  set_weights_archive :300-305, find_bad_parts :308-335
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import os
+
+import numpy as np
+
+from . import _native
+
+__all__ = ["parse_arguments", "main", "clean", "set_weights_archive", "find_bad_parts",
+           "archive_backend", "run_loop"]
+
+
+def archive_backend():
+    """The archive module: real psrchive when importable, else the NumPy stand-in."""
+    try:
+        import psrchive  # noqa: F401
+        return psrchive
+    except ImportError:
+        from . import archive
+        return archive
+
+
+def parse_arguments(argv=None):
+    p = argparse.ArgumentParser(description="Commands for the cleaner")
+    p.add_argument("archive", nargs="+", help="The chosen archives")
+    p.add_argument("-c", "--chanthresh", type=float, default=5, metavar=("channel_threshold"),
+                   help="The threshold (in number of sigmas) a profile needs to stand out compared "
+                        "to others in the same channel for it to be removed.")
+    p.add_argument("-s", "--subintthresh", type=float, default=5, metavar=("subint_threshold"),
+                   help="The threshold (in number of sigmas) a profile needs to stand out compared "
+                        "to others in the same subint for it to be removed.")
+    p.add_argument("-m", "--max_iter", type=int, default=5, metavar=("maximum_iterations"),
+                   help="Maximum number of iterations.")
+    p.add_argument("-z", "--print_zap", action="store_true",
+                   help="Creates a plot that shows which profiles get zapped.")
+    p.add_argument("-u", "--unload_res", action="store_true",
+                   help="Creates an archive that contains the pulse free residual.")
+    p.add_argument("-p", "--pscrunch", action="store_true", help="Pscrunches the output archive.")
+    p.add_argument("-q", "--quiet", action="store_true", help="Do not print cleaning information.")
+    p.add_argument("-l", "--no_log", action="store_true", help="Do not create cleaning log.")
+    p.add_argument("-r", "--pulse_region", nargs=3, type=float, default=[0, 0, 1],
+                   metavar=("pulse_start", "pulse_end", "scaling_factor"),
+                   help="Defines the range of the pulse and a suppression factor.")
+    p.add_argument("-o", "--output", type=str, default="", metavar=("output_filename"),
+                   help="Name of the output file. If set to 'std' the pattern NAME.FREQ.MJD.ar "
+                        "will be used.")
+    p.add_argument("--memory", action="store_true",
+                   help="Do not pscrunch the archive while it is in memory. Costs RAM but prevents "
+                        "having to reload the archive.")
+    p.add_argument("--bad_chan", type=float, default=1,
+                   help="Fraction of subints that needs to be removed in order to remove the whole "
+                        "channel.")
+    p.add_argument("--bad_subint", type=float, default=1,
+                   help="Fraction of channels that needs to be removed in order to remove the whole "
+                        "subint.")
+    return p.parse_args(argv)
+
+
+def _output_name(ar, args):
+    if args.output == "":
+        return str(ar).split(":", 1)[1].strip() + "_cleaned.ar"
+    if args.output == "std":
+        mjd = (float(ar.start_time().strtempo()) + float(ar.end_time().strtempo())) / 2.0
+        return "%s.%.3f.%f.ar" % (ar.get_source(), ar.get_centre_frequency(), mjd)
+    return args.output
+
+
+def main(args):
+    backend = archive_backend()
+    for arch in args.archive:
+        ar = backend.Archive_load(arch)
+        o_name = _output_name(ar, args)
+        ar = clean(ar, args, arch)
+        ar.unload(o_name)
+        if not args.quiet:
+            print("Cleaned archive: %s" % o_name)
+
+
+def _dm_shift(ar) -> np.ndarray:
+    """Per-channel dedispersion delay in bins (ded[i] = raw[(i+shift)%nbin])."""
+    if hasattr(ar, "get_dm_shift"):
+        return np.asarray(ar.get_dm_shift(), dtype=np.int64)
+    # real psrchive: integer-bin approximation of its phase rotation
+    nbin, nchan = ar.get_nbin(), ar.get_nchan()
+    dm = ar.get_dispersion_measure()
+    fref = ar.get_centre_frequency()
+    period = ar.get_Integration(0).get_folding_period()
+    out = np.zeros(nchan, dtype=np.int64)
+    for c in range(nchan):
+        f = ar.get_Profile(0, 0, c).get_centre_frequency()
+        delay = 4.148808e3 * dm * (f ** -2 - fref ** -2)
+        out[c] = int(round(delay / period * nbin)) % nbin
+    return out
+
+
+def _total_intensity(ar) -> np.ndarray:
+    """(nsub, nchan, nbin) f32 total intensity as pscrunch defines it."""
+    data = ar.get_data()
+    if data.shape[1] == 1:
+        return np.ascontiguousarray(data[:, 0], dtype=np.float32)
+    return np.ascontiguousarray((data[:, 0] + data[:, 1]).astype(np.float32))
+
+
+def _device() -> int:
+    for key in ("IC_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(key, "") != "":
+            return int(os.environ[key])
+    return 0
+
+
+def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15):
+    """Run the GPU loop on a (nsub, nchan, nbin) f32 cube; returns the ic_run dict
+    (+ ``residual`` when requested)."""
+    nsub, nchan, nbin = cube.shape
+    with _native.GpuSession(nsub, nchan, nbin, args.max_iter, args.chanthresh, args.subintthresh,
+                            args.pulse_region, baseline_duty,
+                            device=_device() if device is None else device) as s:
+        s.upload(cube, w0, shift)
+        out = s.run()
+        if want_residual and out["n_iter"] > 0:
+            out["residual"] = s.residual()
+    return out
+
+
+def set_weights_archive(archive, test_results):
+    """Zero the weight of every profile whose test value is >= 1 (ic.py:300-305)."""
+    for isub, ichan in np.argwhere(test_results >= 1):
+        archive.get_Integration(int(isub)).set_weight(int(ichan), 0.0)
+
+
+def find_bad_parts(archive, args):
+    """Zap whole subints / channels whose zero-weight fraction exceeds the limit
+    (ic.py:308-335); both passes read the weights as they were on entry."""
+    weights = archive.get_weights()
+    n_subints = archive.get_nsubint()
+    n_channels = archive.get_nchan()
+    n_bad_channels = 0
+    n_bad_subints = 0
+    for i in range(n_subints):
+        bad_frac = 1 - np.count_nonzero(weights[i, :]) / float(n_channels)
+        if bad_frac > args.bad_subint:
+            for j in range(n_channels):
+                archive.get_Integration(int(i)).set_weight(int(j), 0.0)
+            n_bad_subints += 1
+    for j in range(n_channels):
+        bad_frac = 1 - np.count_nonzero(weights[:, j]) / float(n_subints)
+        if bad_frac > args.bad_chan:
+            for i in range(n_subints):
+                archive.get_Integration(int(i)).set_weight(int(j), 0.0)
+            n_bad_channels += 1
+    if not args.quiet and n_bad_channels + n_bad_subints != 0:
+        print("Removed %s bad subintegrations and %s bad channels." % (n_bad_subints, n_bad_channels))
+    return archive
+
+
+def _plot_zap(test, ar_name, args):
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.cm as cm
+    import matplotlib.pyplot as plt
+    plt.imshow(test.T, vmin=0.999, vmax=1.001, aspect="auto", interpolation="nearest",
+               cmap=cm.coolwarm)
+    plt.gca().invert_yaxis()
+    plt.title("%s cthresh=%s sthresh=%s" % (ar_name, args.chanthresh, args.subintthresh))
+    plt.savefig("%s_%s_%s.png" % (ar_name, args.chanthresh, args.subintthresh), bbox_inches="tight")
+
+
+def clean(ar, args, arch):
+    """Surgical cleaning of one archive (iterative_cleaner.py:65-178)."""
+    backend = archive_backend()
+    orig_weights = ar.get_weights()
+    if not (args.memory and not args.pscrunch):
+        ar.pscrunch()
+    ar_name = ar.get_filename().split()[-1]
+    max_iterations = args.max_iter
+    if not args.quiet:
+        print("Total number of profiles: %s" % orig_weights.size)
+
+    cube = _total_intensity(ar)
+    shift = _dm_shift(ar)
+    duty = ar.get_baseline_duty() if hasattr(ar, "get_baseline_duty") else 0.15
+    out = run_loop(cube, orig_weights, shift, args, want_residual=args.unload_res,
+                   baseline_duty=duty)
+
+    size = orig_weights.size
+    x = 0
+    loops = None
+    for k in range(out["n_iter"]):
+        x = k + 1
+        if not args.quiet:
+            print("Loop: %s" % x)
+            rfi_frac = out["nzero"][k] / float(size)
+            print("Differences to previous weights: %s  RFI fraction: %s"
+                  % (int(out["changed"][k]), rfi_frac))
+        if k == out["n_iter"] - 1 and out["converged"]:
+            if not args.quiet:
+                print("RFI removal stops after %s loops." % x)
+            loops = x
+            x = 1000000
+    if x == max_iterations:
+        if not args.quiet:
+            print("Cleaning was interrupted after the maximum amount of loops (%s)" % max_iterations)
+        loops = max_iterations
+    if out["n_iter"] == 0:
+        raise NameError("name 'avg_test_results' is not defined")
+    avg_test_results = out["test"]
+
+    if not args.pscrunch and not args.memory:
+        ar = backend.Archive_load(arch)
+    set_weights_archive(ar, avg_test_results)
+    if args.bad_chan != 1 or args.bad_subint != 1:
+        ar = find_bad_parts(ar, args)
+    if args.unload_res:
+        _residual_archive(ar, out["residual"], orig_weights, shift, backend).unload(
+            "%s_residual_%s.ar" % (ar_name, loops))
+    if args.print_zap:
+        _plot_zap(avg_test_results, ar_name, args)
+    if not args.no_log:
+        with open("clean.log", "a") as fh:
+            fh.write("\n %s: Cleaned %s with %s, required loops=%s"
+                     % (datetime.datetime.now(), ar_name, args, loops))
+    return ar
+
+
+def _residual_archive(ar, residual, weights, shift, backend):
+    """The pulse-free residual archive of the last loop (ic.py:106-108, :161-162)."""
+    from .archive import Archive
+    return Archive(residual[:, None], weights, shift, dedispersed=False,
+                   filename="residual.ar",
+                   source=ar.get_source() if hasattr(ar, "get_source") else "J0000+0000")
+
+
+if __name__ == "__main__":  # pragma: no cover
+    main(parse_arguments())

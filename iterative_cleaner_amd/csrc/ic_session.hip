@@ -1,0 +1,505 @@
+// ic_session.hip — host side of libicgpu.so: the C-ABI declared in
+// include/iterative_cleaner.h.  Owns device buffers and the HIP stream of a
+// session, prepares the fit cube once per upload, and drives the cleaning
+// loop of iterative_cleaner.py:83-146 (one launch sequence per iteration and
+// one small device->host read of the convergence counters).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/iterative_cleaner.h"
+#include "ic_internal.h"
+
+using namespace icgpu;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define CK(call)                                                                                  \
+    do {                                                                                          \
+        hipError_t e_ = (call);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail(IC_EHIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                                \
+    } while (0)
+
+const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",   "k_base",        "k_fitcube",
+                                     "k_fscrunch",      "k_tscrunch", "k_fit",         "k_diag",
+                                     "k_linestats",     "k_combine",  "k_residual"};
+
+struct Timed {
+    int kid;
+    hipEvent_t a, b;
+};
+
+struct Session {
+    ic_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    size_t P = 0, N = 0;
+    int nsb = 0, width = 0;
+    bool uploaded = false, ran = false;
+    int last_iter = 0;
+    // device buffers
+    float *raw = nullptr, *D = nullptr, *w0 = nullptr, *W = nullptr, *base = nullptr, *base0 = nullptr;
+    float *F = nullptr, *wf = nullptr, *T = nullptr, *ptp = nullptr, *hist = nullptr;
+    uint8_t *valid = nullptr;
+    int32_t *shift = nullptr, *win = nullptr, *info = nullptr, *counters = nullptr;
+    double *part = nullptr, *wpart = nullptr, *T64 = nullptr, *amp = nullptr, *std_ = nullptr,
+           *mean = nullptr, *fft = nullptr, *test = nullptr, *lstat = nullptr;
+    double2 *tw = nullptr;
+    PwPlan *plan = nullptr;
+    // timing
+    bool timing = false;
+    std::vector<Timed> events;
+    double kms[K_COUNT] = {0};
+    int klaunch[K_COUNT] = {0};
+};
+
+template <typename T>
+hipError_t dalloc(T **p, size_t n)
+{
+    return hipMalloc((void **)p, n * sizeof(T) + 16);
+}
+
+// numpy pairwise plan (loops_utils.h.src): leaves <= 128 in address order
+int plan_build(std::vector<int> &ls, std::vector<int> &ll, std::vector<int> &oa, std::vector<int> &ob,
+               int start, int n)
+{
+    if (n <= 128) {
+        ls.push_back(start);
+        ll.push_back(n);
+        return (int)ls.size() - 1;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    const int a = plan_build(ls, ll, oa, ob, start, n2);
+    const int b = plan_build(ls, ll, oa, ob, start + n2, n - n2);
+    oa.push_back(a);
+    ob.push_back(b);
+    return -(int)oa.size();  // op o encoded as -(o+1)
+}
+
+int make_plan(int n, PwPlan *pl)
+{
+    std::vector<int> ls, ll, oa, ob;
+    const int root = plan_build(ls, ll, oa, ob, 0, n);
+    if ((int)ls.size() > kMaxLeaves || (int)oa.size() > kMaxLeaves) return -1;
+    memset(pl, 0, sizeof *pl);
+    pl->n = n;
+    pl->nleaf = (int)ls.size();
+    pl->nops = (int)oa.size();
+    auto slot = [&](int id) { return id >= 0 ? id : pl->nleaf + (-id - 1); };
+    for (int q = 0; q < pl->nleaf; ++q) {
+        pl->leaf_start[q] = ls[q];
+        pl->leaf_len[q] = ll[q];
+    }
+    for (int q = 0; q < pl->nops; ++q) {
+        pl->op_a[q] = slot(oa[q]);
+        pl->op_b[q] = slot(ob[q]);
+    }
+    pl->root = slot(root);
+    return 0;
+}
+
+#define LAUNCH(S, KID, CALL)                                                   \
+    do {                                                                       \
+        Timed t_{KID, nullptr, nullptr};                                       \
+        if ((S)->timing) {                                                     \
+            CK(hipEventCreate(&t_.a));                                         \
+            CK(hipEventCreate(&t_.b));                                         \
+            CK(hipEventRecord(t_.a, (S)->stream));                             \
+        }                                                                      \
+        CK(CALL);                                                              \
+        if ((S)->timing) {                                                     \
+            CK(hipEventRecord(t_.b, (S)->stream));                             \
+            (S)->events.push_back(t_);                                         \
+        }                                                                      \
+    } while (0)
+
+int collect_timing(Session *s)
+{
+    if (!s->timing) return 0;
+    CK(hipStreamSynchronize(s->stream));
+    for (auto &e : s->events) {
+        float ms = 0.f;
+        CK(hipEventElapsedTime(&ms, e.a, e.b));
+        s->kms[e.kid] += ms;
+        s->klaunch[e.kid] += 1;
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    s->events.clear();
+    return 0;
+}
+
+void free_all(Session *s)
+{
+    void *bufs[] = {s->raw,  s->D,     s->w0,   s->W,   s->base, s->base0, s->F,   s->wf,
+                    s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->counters,
+                    s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
+                    s->lstat, s->tw,   s->plan};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    for (auto &e : s->events) {
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+}
+
+__global__ void k_valid(const float *w0, uint8_t *valid, float *W, float *hist0, size_t P)
+{
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < P) {
+        const float w = w0[k];
+        valid[k] = (w != 0.0f);
+        W[k] = w;
+        hist0[k] = w;
+    }
+}
+
+// fit-cube preparation (iterative_cleaner.py:96-100): baseline with w0, dedisperse
+int prepare(Session *s)
+{
+    const int nsub = s->p.nsub, nchan = s->p.nchan, nbin = s->p.nbin;
+    hipLaunchKernelGGL(k_valid, dim3((unsigned)((s->P + 255) / 256)), dim3(256), 0, s->stream, s->w0,
+                       s->valid, s->W, s->hist, s->P);
+    CK(hipGetLastError());
+    LAUNCH(s, K_CHAN_PARTIALS,
+           launch_chan_partials(s->stream, s->raw, s->w0, s->shift, nullptr, nsub, nchan, nbin, s->part,
+                                nullptr));
+    LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win));
+    LAUNCH(s, K_BASE, launch_base(s->stream, s->raw, s->shift, s->win, nsub, nchan, nbin, s->width, s->base0));
+    LAUNCH(s, K_FITCUBE, launch_fitcube(s->stream, s->raw, s->shift, s->base0, nsub, nchan, nbin, s->D));
+    CK(hipStreamSynchronize(s->stream));
+    s->uploaded = true;
+    s->ran = false;
+    return 0;
+}
+
+int iteration_template(Session *s)
+{
+    const int nsub = s->p.nsub, nchan = s->p.nchan, nbin = s->p.nbin;
+    // remove_baseline with the current weights (template stage)
+    LAUNCH(s, K_CHAN_PARTIALS,
+           launch_chan_partials(s->stream, s->raw, s->W, s->shift, nullptr, nsub, nchan, nbin, s->part,
+                                nullptr));
+    LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win));
+    LAUNCH(s, K_BASE, launch_base(s->stream, s->raw, s->shift, s->win, nsub, nchan, nbin, s->width, s->base));
+    // dedisperse + fscrunch + tscrunch
+    LAUNCH(s, K_CHAN_PARTIALS,
+           launch_chan_partials(s->stream, s->raw, s->W, s->shift, s->base, nsub, nchan, nbin, s->part,
+                                s->wpart));
+    LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->part, s->wpart, nsub, s->nsb, nbin, s->F, s->wf));
+    LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ic_abi_version(void) { return IC_ABI_VERSION; }
+
+int ic_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *ic_last_error(void) { return g_err.c_str(); }
+
+const char *ic_kernel_name(int kernel)
+{
+    if (kernel < 0 || kernel >= K_COUNT) return "";
+    return kKernelNames[kernel];
+}
+
+int ic_session_create(const ic_params *params, int device, void **out)
+{
+    if (!params || !out) return fail(IC_EINVAL, "null argument");
+    *out = nullptr;
+    const ic_params &p = *params;
+    if (p.nsub <= 0 || p.nchan <= 0 || p.nbin <= 0)
+        return fail(IC_EINVAL, "bad shape nsub=%d nchan=%d nbin=%d", p.nsub, p.nchan, p.nbin);
+    if (p.nbin > 32768) return fail(IC_EINVAL, "nbin=%d > 32768 unsupported", p.nbin);
+    if (p.nsub > 16384 || p.nchan > 16384)
+        return fail(IC_EINVAL, "line length > 16384 unsupported (nsub=%d nchan=%d)", p.nsub, p.nchan);
+    if (p.max_iter < 0) return fail(IC_EINVAL, "max_iter < 0");
+    if (p.fit_mode != 0) return fail(IC_EINVAL, "fit_mode %d unsupported", p.fit_mode);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(IC_EHIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
+    Session *s = new Session();
+    s->p = p;
+    s->device = device;
+    s->P = (size_t)p.nsub * p.nchan;
+    s->N = s->P * (size_t)p.nbin;
+    s->nsb = (p.nchan + kSuperBlock - 1) / kSuperBlock;
+    s->width = (int)(p.baseline_duty * (double)p.nbin);
+    if (s->width < 1) s->width = 1;
+    int rc = 0;
+    auto bail = [&](int code) {
+        free_all(s);
+        delete s;
+        return code;
+    };
+#define AL(ptr, n)                                                                                  \
+    do {                                                                                            \
+        if (dalloc(&(ptr), (n)) != hipSuccess) {                                                    \
+            rc = fail(IC_ENOMEM, "hipMalloc(%s, %zu elements) failed", #ptr, (size_t)(n));          \
+            return bail(rc);                                                                        \
+        }                                                                                           \
+    } while (0)
+    if (hipSetDevice(device) != hipSuccess) return bail(fail(IC_EHIP, "hipSetDevice(%d) failed", device));
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(IC_EHIP, "hipStreamCreate failed"));
+    const size_t P = s->P, N = s->N;
+    const int nsub = p.nsub, nchan = p.nchan, nbin = p.nbin;
+    AL(s->raw, N);
+    AL(s->D, N);
+    AL(s->w0, P);
+    AL(s->W, P);
+    AL(s->base, P);
+    AL(s->base0, P);
+    AL(s->valid, P);
+    AL(s->shift, (size_t)nchan);
+    AL(s->win, (size_t)nsub);
+    AL(s->part, (size_t)nsub * s->nsb * nbin);
+    AL(s->wpart, (size_t)nsub * s->nsb);
+    AL(s->F, (size_t)nsub * nbin);
+    AL(s->wf, (size_t)nsub);
+    AL(s->T, (size_t)nbin);
+    AL(s->T64, (size_t)nbin);
+    AL(s->amp, P);
+    AL(s->info, P);
+    AL(s->std_, P);
+    AL(s->mean, P);
+    AL(s->ptp, P);
+    AL(s->fft, P);
+    AL(s->test, P);
+    AL(s->hist, P * (size_t)(p.max_iter + 1));
+    AL(s->lstat, (size_t)16 * (nchan + nsub));
+    AL(s->counters, (size_t)(p.max_iter + 4));
+    AL(s->tw, (size_t)nbin);
+    AL(s->plan, 1);
+#undef AL
+    // twiddles exp(-2 pi i q / n) and the pairwise plan
+    std::vector<double2> tw(nbin);
+    for (int q = 0; q < nbin; ++q) {
+        const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)q / (long double)nbin;
+        tw[q] = make_double2((double)cosl(ang), (double)sinl(ang));
+    }
+    PwPlan plan;
+    if (make_plan(nbin, &plan) != 0) return bail(fail(IC_EINVAL, "pairwise plan too large for nbin=%d", nbin));
+    if (hipMemcpy(s->tw, tw.data(), sizeof(double2) * nbin, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s->plan, &plan, sizeof plan, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(IC_EHIP, "upload of constants failed"));
+    *out = s;
+    return IC_OK;
+}
+
+void ic_session_destroy(void *session)
+{
+    Session *s = (Session *)session;
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    free_all(s);
+    delete s;
+}
+
+int ic_upload(void *session, const float *cube, const float *w0, const int32_t *shift)
+{
+    Session *s = (Session *)session;
+    if (!s || !cube || !w0 || !shift) return fail(IC_EINVAL, "null argument");
+    CK(hipSetDevice(s->device));
+    for (int c = 0; c < s->p.nchan; ++c)
+        if (shift[c] < 0 || shift[c] >= s->p.nbin) return fail(IC_EINVAL, "shift[%d]=%d out of [0,nbin)", c, shift[c]);
+    CK(hipMemcpyAsync(s->raw, cube, sizeof(float) * s->N, hipMemcpyHostToDevice, s->stream));
+    CK(hipMemcpyAsync(s->w0, w0, sizeof(float) * s->P, hipMemcpyHostToDevice, s->stream));
+    CK(hipMemcpyAsync(s->shift, shift, sizeof(int32_t) * s->p.nchan, hipMemcpyHostToDevice, s->stream));
+    return prepare(s);
+}
+
+int ic_upload_device(void *session, const float *d_cube, const float *d_w0, const int32_t *d_shift)
+{
+    Session *s = (Session *)session;
+    if (!s || !d_cube || !d_w0 || !d_shift) return fail(IC_EINVAL, "null argument");
+    CK(hipSetDevice(s->device));
+    CK(hipMemcpyAsync(s->raw, d_cube, sizeof(float) * s->N, hipMemcpyDeviceToDevice, s->stream));
+    CK(hipMemcpyAsync(s->w0, d_w0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
+    CK(hipMemcpyAsync(s->shift, d_shift, sizeof(int32_t) * s->p.nchan, hipMemcpyDeviceToDevice, s->stream));
+    return prepare(s);
+}
+
+int ic_set_timing(void *session, int enabled)
+{
+    Session *s = (Session *)session;
+    if (!s) return fail(IC_EINVAL, "null session");
+    s->timing = enabled != 0;
+    for (int q = 0; q < K_COUNT; ++q) {
+        s->kms[q] = 0.0;
+        s->klaunch[q] = 0;
+    }
+    return IC_OK;
+}
+
+int ic_get_kernel_times(void *session, ic_kernel_time *out, int n)
+{
+    Session *s = (Session *)session;
+    if (!s || (!out && n > 0)) return fail(IC_EINVAL, "null argument");
+    int m = 0;
+    for (int q = 0; q < K_COUNT && m < n; ++q) {
+        out[m].kernel = q;
+        out[m].launches = s->klaunch[q];
+        out[m].ms = s->kms[q];
+        ++m;
+    }
+    return m;
+}
+
+int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_out, int32_t *changed_out,
+           int32_t *nzero_out, int32_t *n_iter_out, int32_t *converged_out)
+{
+    Session *s = (Session *)session;
+    if (!s) return fail(IC_EINVAL, "null session");
+    if (!s->uploaded) return fail(IC_ESTATE, "ic_run before ic_upload");
+    CK(hipSetDevice(s->device));
+    const ic_params &p = s->p;
+    const int nsub = p.nsub, nchan = p.nchan, nbin = p.nbin;
+    int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > nbin ? nbin : p.pr_start);
+    int pr_end = p.pr_end < 0 ? 0 : (p.pr_end > nbin ? nbin : p.pr_end);
+    // restore the initial weights (a session can be re-run)
+    CK(hipMemcpyAsync(s->W, s->w0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
+    CK(hipMemcpyAsync(s->hist, s->w0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
+    LineStatsArgs la;
+    la.nsub = nsub;
+    la.nchan = nchan;
+    la.valid = s->valid;
+    la.std_d = s->std_;
+    la.mean_d = s->mean;
+    la.fft_d = s->fft;
+    la.ptp_d = s->ptp;
+    la.col_med = s->lstat;
+    la.col_mad = s->lstat + 4 * nchan;
+    la.row_med = s->lstat + 8 * nchan;
+    la.row_mad = s->lstat + 8 * nchan + 4 * nsub;
+    std::vector<int32_t> cnt(p.max_iter + 4);
+    int x = 0, loops = -1, n_iter = 0, converged = 0;
+    while (x < p.max_iter) {
+        x += 1;
+        ++n_iter;
+        if (int rc = iteration_template(s)) return rc;
+        LAUNCH(s, K_FIT, launch_fit(s->stream, s->D, s->T64, (long)s->P, nbin, s->amp, s->info));
+        LAUNCH(s, K_DIAG,
+               launch_diag(s->stream, s->D, s->T64, s->amp, s->info, s->w0, s->shift, s->tw, s->plan, nsub,
+                           nchan, nbin, p.pr_on, p.pr_factor, pr_start, pr_end, s->std_, s->mean, s->ptp,
+                           s->fft));
+        LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, la));
+        CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t) * (p.max_iter + 4), s->stream));
+        LAUNCH(s, K_COMBINE,
+               launch_combine(s->stream, nsub, nchan, s->valid, s->w0, s->std_, s->mean, s->ptp, s->fft,
+                              la.col_med, la.col_mad, la.row_med, la.row_mad, p.chanthresh, p.subintthresh,
+                              s->test, s->W, s->hist, n_iter, s->counters));
+        CK(hipMemcpyAsync(cnt.data(), s->counters, sizeof(int32_t) * (n_iter + 2), hipMemcpyDeviceToHost,
+                          s->stream));
+        CK(hipStreamSynchronize(s->stream));
+        if (changed_out) changed_out[n_iter - 1] = cnt[0];
+        if (nzero_out) nzero_out[n_iter - 1] = cnt[1];
+        for (int h = 0; h < n_iter; ++h)
+            if (cnt[2 + h] == 0) {
+                loops = x;
+                converged = 1;
+                x = 1000000;
+            }
+    }
+    if (x == p.max_iter) loops = p.max_iter;
+    s->last_iter = n_iter;
+    if (test_out && n_iter > 0)
+        CK(hipMemcpyAsync(test_out, s->test, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
+    if (weights_out)
+        CK(hipMemcpyAsync(weights_out, s->W, sizeof(float) * s->P, hipMemcpyDeviceToHost, s->stream));
+    CK(hipStreamSynchronize(s->stream));
+    if (int rc = collect_timing(s)) return rc;
+    if (loops_out) *loops_out = loops;
+    if (n_iter_out) *n_iter_out = n_iter;
+    if (converged_out) *converged_out = converged;
+    s->ran = n_iter > 0;
+    return IC_OK;
+}
+
+int ic_get_residual(void *session, float *out)
+{
+    Session *s = (Session *)session;
+    if (!s || !out) return fail(IC_EINVAL, "null argument");
+    if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
+    CK(hipSetDevice(s->device));
+    const ic_params &p = s->p;
+    int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > p.nbin ? p.nbin : p.pr_start);
+    int pr_end = p.pr_end < 0 ? 0 : (p.pr_end > p.nbin ? p.nbin : p.pr_end);
+    // the fit cube buffer `base` is reused as scratch? no: allocate a temporary
+    float *R = nullptr;
+    CK(hipMalloc((void **)&R, sizeof(float) * s->N));
+    hipError_t e = launch_residual(s->stream, s->D, s->T64, s->amp, s->info, s->shift, p.nsub, p.nchan, p.nbin,
+                                   p.pr_on, p.pr_factor, pr_start, pr_end, R);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, R, sizeof(float) * s->N, hipMemcpyDeviceToHost, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    (void)hipFree(R);
+    if (e != hipSuccess) return fail(IC_EHIP, "residual: %s", hipGetErrorString(e));
+    return IC_OK;
+}
+
+int ic_get_template(void *session, float *T)
+{
+    Session *s = (Session *)session;
+    if (!s || !T) return fail(IC_EINVAL, "null argument");
+    if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
+    CK(hipMemcpyAsync(T, s->T, sizeof(float) * s->p.nbin, hipMemcpyDeviceToHost, s->stream));
+    CK(hipStreamSynchronize(s->stream));
+    return IC_OK;
+}
+
+int ic_get_fit(void *session, double *amp, int32_t *info)
+{
+    Session *s = (Session *)session;
+    if (!s) return fail(IC_EINVAL, "null argument");
+    if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
+    if (amp) CK(hipMemcpyAsync(amp, s->amp, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
+    if (info) CK(hipMemcpyAsync(info, s->info, sizeof(int32_t) * s->P, hipMemcpyDeviceToHost, s->stream));
+    CK(hipStreamSynchronize(s->stream));
+    return IC_OK;
+}
+
+int ic_get_diagnostics(void *session, double *std_o, double *mean_o, float *ptp_o, double *fftmax_o)
+{
+    Session *s = (Session *)session;
+    if (!s) return fail(IC_EINVAL, "null argument");
+    if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
+    if (std_o) CK(hipMemcpyAsync(std_o, s->std_, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
+    if (mean_o) CK(hipMemcpyAsync(mean_o, s->mean, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
+    if (ptp_o) CK(hipMemcpyAsync(ptp_o, s->ptp, sizeof(float) * s->P, hipMemcpyDeviceToHost, s->stream));
+    if (fftmax_o) CK(hipMemcpyAsync(fftmax_o, s->fft, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
+    CK(hipStreamSynchronize(s->stream));
+    return IC_OK;
+}
+
+}  // extern "C"

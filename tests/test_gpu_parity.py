@@ -1,0 +1,151 @@
+"""GPU parity: the HIP loop (through the C-ABI) against the reference's golden
+fixtures and the C oracle.  Bit-exact for masks, weights, loops, template,
+fit amplitudes/status and the std/mean/ptp diagnostics; fftmax within 1e-9
+relative (our FFT vs pocketfft) and test values within 1e-9 absolute (the
+fftmax tolerance propagated through median/MAD scaling)."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import bits_equal, clean_fixtures, load_clean_case, nan_equal
+
+pytestmark = pytest.mark.gpu
+
+FFT_RTOL = 1e-9
+TEST_ATOL = 1e-9
+
+
+def _session(shape, args, duty=0.15):
+    from iterative_cleaner_amd import _native
+    nsub, nchan, nbin = shape
+    return _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"],
+                              args["subintthresh"], args["pulse_region"], duty, device=0)
+
+
+def _close_fft(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    both_nan = np.isnan(a) & np.isnan(b)
+    ok = both_nan | (np.abs(a - b) <= FFT_RTOL * np.maximum(np.abs(b), 1e-300)) | (a == b)
+    return bool(ok.all())
+
+
+def _close_test(a, b):
+    both_nan = np.isnan(a) & np.isnan(b)
+    same_inf = np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b))
+    fin = np.isfinite(a) & np.isfinite(b)
+    ok = both_nan | same_inf | (fin & (np.abs(a - b) <= TEST_ATOL * np.maximum(1.0, np.abs(b))))
+    return bool(ok.all())
+
+
+@pytest.mark.parametrize("path", clean_fixtures(), ids=lambda p: os.path.basename(p)[6:-4])
+def test_loop_matches_reference(path):
+    z, meta, raw, w0, shift, args = load_clean_case(path)
+    nit = int(z["n_iter"])
+    with _session(raw.shape, args) as s:
+        s.upload(raw, w0, shift)
+        out = s.run()
+        T = s.template()
+        amp, info = s.fit()
+        sd, mn, pt, ff = s.diagnostics()
+    assert out["n_iter"] == nit
+    assert out["loops"] == int(z["loops"])
+    assert bits_equal(out["weights"], z["weights_%d" % nit]), "zap mask differs"
+    assert bits_equal(T, z["T_%d" % nit])
+    assert bits_equal(amp.ravel(), z["amp_%d" % nit]), "leastsq amplitudes differ"
+    assert bits_equal(info.ravel(), z["info_%d" % nit])
+    assert bits_equal(sd, z["diag_std_%d" % nit])
+    assert bits_equal(mn, z["diag_mean_%d" % nit])
+    assert bits_equal(pt, z["diag_ptp_%d" % nit])
+    assert _close_fft(ff, z["diag_fft_%d" % nit])
+    assert _close_test(out["test"], z["test_%d" % nit])
+    # per-iteration counters reproduce the reference's prints (ic.py:129-130)
+    prev = w0
+    for k in range(1, nit + 1):
+        wk = z["weights_%d" % k]
+        assert out["changed"][k - 1] == int(np.sum(wk != prev))
+        assert out["nzero"][k - 1] == int(wk.size - np.count_nonzero(wk))
+        prev = wk
+
+
+@pytest.mark.parametrize("path", clean_fixtures(), ids=lambda p: os.path.basename(p)[6:-4])
+def test_clean_stdout_matches_reference(path, tmp_path, monkeypatch, capsys):
+    """clean() prints exactly what the reference printed (ic.py:82-145)."""
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import cleaner
+    z, meta, raw, w0, shift, args = load_clean_case(path)
+    from iterative_cleaner_amd import synth
+    data, w0_, shift_ = synth.make_cube(meta["nsub"], meta["nchan"], meta["nbin"], meta["seed"],
+                                        meta["rfi"], npol=meta["npol"])
+    monkeypatch.chdir(tmp_path)
+    arpath = str(tmp_path / ("%s.ar" % meta["name"]))
+    ica.Archive(data, w0_, shift_, filename=arpath).unload(arpath)
+    ar = ica.Archive_load(arpath)
+    ns = cleaner.parse_arguments(["-l", *meta["extra_args"], arpath])
+    out_ar = cleaner.clean(ar, ns, arpath)
+    printed = capsys.readouterr().out
+    assert printed == str(z["stdout"])
+    assert bits_equal(out_ar.get_weights(), z["final_weights"])
+
+
+CASES = [
+    # (nsub, nchan, nbin, seed, rfi, extra)
+    (7, 300, 64, 11, 0.2, {}),                 # two channel super-blocks
+    (5, 33, 100, 12, 0.3, {}),                 # non power-of-two nbin (direct DFT)
+    (6, 40, 4096, 13, 0.1, {}),                # long profiles
+    (3, 20, 8, 14, 0.3, {}),                   # tiny profiles
+    (9, 70, 128, 15, 0.3, {"chanthresh": 3.0, "subintthresh": 2.5}),
+    (8, 64, 256, 16, 0.2, {"pulse_region": [0.25, 40, 90]}),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "%dx%dx%d" % c[:3])
+def test_loop_matches_c_oracle(case, oracle_lib):
+    from iterative_cleaner_amd import synth
+    nsub, nchan, nbin, seed, rfi, extra = case
+    data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
+    raw = np.ascontiguousarray(data[:, 0])
+    args = dict(max_iter=5, chanthresh=5, subintthresh=5, pulse_region=[0, 0, 1])
+    args.update(extra)
+    pr = None if args["pulse_region"] == [0, 0, 1] else args["pulse_region"]
+    ref = oracle_lib.clean_loop(raw, w0, shift, args["chanthresh"], args["subintthresh"],
+                                args["max_iter"], pr, want_residual=True, want_details=True)
+    with _session(raw.shape, args) as s:
+        s.upload(raw, w0, shift)
+        out = s.run()
+        amp, info = s.fit()
+        sd, mn, pt, ff = s.diagnostics()
+        R = s.residual()
+    assert out["loops"] == ref["loops"]
+    assert bits_equal(out["weights"], ref["weights"])
+    assert np.array_equal(out["changed"], ref["changed"][:out["n_iter"]])
+    assert bits_equal(amp, ref["amp"]) and bits_equal(info, ref["info"])
+    assert bits_equal(sd, ref["std"]) and bits_equal(mn, ref["mean"]) and bits_equal(pt, ref["ptp"])
+    assert _close_fft(ff, ref["fft"])
+    assert _close_test(out["test"], ref["test"])
+    assert bits_equal(R, ref["residual"])
+
+
+def test_edge_profiles_match_c_oracle(oracle_lib):
+    """Dead (all-zero) channels with weight 1, zero profiles, a NaN-free
+    constant channel, fractional weights (K2, K7, K10)."""
+    from iterative_cleaner_amd import synth
+    data, w0, shift = synth.make_cube(10, 48, 128, 99, 0.2)
+    raw = np.ascontiguousarray(data[:, 0])
+    raw[:, 3, :] = 0.0                       # dead channel, weight 1
+    raw[:, 5, :] = 2.5                       # constant channel
+    raw[4, :, :] = 0.0                       # zero subint
+    w0 = w0.copy()
+    w0[:, 7] = 0.5                           # fractional weights
+    w0[2, 9] = 0.0
+    ref = oracle_lib.clean_loop(raw, w0, shift, want_details=True)
+    args = dict(max_iter=5, chanthresh=5, subintthresh=5, pulse_region=[0, 0, 1])
+    with _session(raw.shape, args) as s:
+        s.upload(raw, w0, shift)
+        out = s.run()
+        amp, info = s.fit()
+    assert out["loops"] == ref["loops"]
+    assert bits_equal(out["weights"], ref["weights"])
+    assert bits_equal(amp, ref["amp"]) and bits_equal(info, ref["info"])
+    assert _close_test(out["test"], ref["test"])
