@@ -1,0 +1,224 @@
+#!/usr/bin/env python
+"""Benchmark: profiles cleaned per second on MI355X (BASELINE.json metric).
+
+A step = one complete surgical-cleaning run (iterative_cleaner.py:83-146:
+fit-cube preparation + every loop iteration until the zap mask repeats or
+max_iter) over one synthetic archive already resident in HBM.  Default
+workload: configs[1] of BASELINE.json, a LOFAR HBA-like archive
+360 subint x 3200 chan x 1024 bin, default thresholds, max_iter 5.
+
+Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): this workload
+is "replicas only" (SURVEY.md §8(e)): every rank cleans its own archive, no
+collective on the data path; value = all ranks' profiles / max-over-ranks
+time (weak scaling).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+``roofline`` for the dominant kernel (HIP events on the session stream) and
+``cpu_baseline`` (the reference-like NumPy/SciPy loop on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+F64_PEAK_TOPS = 39.3           # f64 vector ops/s (78.6 TFLOP/s FMA-counted / 2)
+
+WORKLOADS = {
+    # name: (nsub, nchan, nbin, seed, rfi_frac)
+    "C1": (64, 256, 256, 0, 0.05),
+    "C2": (360, 3200, 1024, 1, 0.05),
+    "C4": (128, 1024, 512, 1000, 0.05),
+    "C5": (256, 1024, 4096, 5, 0.30),
+}
+
+
+def make_cube_device(nsub, nchan, nbin, seed, rfi, device):
+    """SURVEY.md §8(d) synthetic archive generated directly in HBM (torch)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    f32 = torch.float32
+    phase = (torch.arange(nbin, device=device, dtype=torch.float64) + 0.5) / nbin
+    pulse = torch.exp(-0.5 * ((phase - 0.3) / 0.02) ** 2)
+    shift = (torch.arange(nchan, device=device) % 7).to(torch.int32)
+    idx = (torch.arange(nbin, device=device)[None, :] - shift[:, None].long()) % nbin
+    pulse_disp = pulse[idx].to(f32)                                     # (nchan, nbin)
+    u = torch.rand((2, nsub, nchan), generator=g, device=device, dtype=torch.float64)
+    gain = (0.5 * (-torch.log1p(-u[0]) - torch.log1p(-u[1]))).to(f32)  # Gamma(2, 0.5)
+    cube = torch.randn((nsub, nchan, nbin), generator=g, device=device, dtype=f32)
+    for s0 in range(0, nsub, 32):
+        cube[s0:s0 + 32] += gain[s0:s0 + 32, :, None] * pulse_disp[None]
+    n_nb = int(round(rfi * nchan))
+    if n_nb:
+        chans = torch.randperm(nchan, generator=g, device=device)[:n_nb]
+        nu = 1.0 + 19.0 * torch.rand(n_nb, generator=g, device=device, dtype=torch.float64)
+        amp = 5.0 * torch.randn((nsub, n_nb), generator=g, device=device, dtype=torch.float64)
+        wave = torch.sin(2.0 * math.pi * nu[:, None] * phase[None, :])
+        cube[:, chans, :] += (amp[:, :, None] * wave[None]).to(f32)
+    n_imp = int(round(rfi * nsub))
+    if n_imp:
+        subs = torch.randperm(nsub, generator=g, device=device)[:n_imp]
+        for s in subs.tolist():
+            hits = torch.rand((nchan, nbin), generator=g, device=device) < 0.01
+            cube[s] += hits.to(f32) * 20.0
+    w0 = torch.ones((nsub, nchan), device=device, dtype=f32)
+    n_dead = int(round(0.02 * nchan))
+    if n_dead:
+        w0[:, torch.randperm(nchan, generator=g, device=device)[:n_dead]] = 0.0
+    return cube.contiguous(), w0.contiguous(), shift.contiguous()
+
+
+def algorithmic_bytes(name, nsub, nchan, nbin):
+    """Bytes each kernel must move per launch."""
+    P = nsub * nchan
+    N = P * nbin
+    nsb = (nchan + 255) // 256
+    return {
+        "k_chan_partials": 4 * N + 8 * nsub * nsb * nbin,
+        "k_base": int(4 * P * max(1, int(0.15 * nbin))),
+        "k_fitcube": 8 * N,
+        "k_fit": 4 * N + 12 * P,
+        "k_diag": 4 * N + 44 * P,
+        "k_linestats": 2 * 4 * 8 * P,
+        "k_combine": 4 * 8 * P + 2 * 4 * P,
+    }.get(name)
+
+
+def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
+    """Reference-like loop (per-profile scipy leastsq + numpy.ma), one thread."""
+    from threadpoolctl import threadpool_limits
+
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import synth
+    from oracle import reference_like
+    nsub = 4
+    data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
+    ar = ica.Archive(data, w0, shift)
+    ar.pscrunch()
+    with threadpool_limits(1):
+        t0 = time.perf_counter()
+        _, _, loops = reference_like.clean_loop(ar, 5, 5, 5, [0, 0, 1])
+        dt = time.perf_counter() - t0
+    P = nsub * nchan
+    return {"value": P / dt, "unit": "profiles/s", "cores": 1, "kind": "port",
+            "sample": "%dx%dx%d subset of the workload shape, full loop to convergence "
+                      "(%d loops) in %.1f s, single thread (oracle/reference_like.py)"
+                      % (nsub, nchan, nbin, loops, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=30.0)
+    ap.add_argument("--kernel-report", action="store_true", help="print per-kernel times to stderr")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from iterative_cleaner_amd import _native
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    nsub, nchan, nbin, seed, rfi = WORKLOADS[a.workload]
+    cube, w0, shift = make_cube_device(nsub, nchan, nbin, seed + 7919 * rank, rfi, dev)
+    torch.cuda.synchronize()
+    P = nsub * nchan
+    sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local)
+    sess.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
+    del cube
+    torch.cuda.empty_cache()
+    for _ in range(a.warmup):
+        sess.run(fetch=False)
+    sess.set_timing(True)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    loops = []
+    for _ in range(a.steps):
+        out = sess.run(fetch=False)
+        loops.append(out["loops"])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ktimes = sess.kernel_times()
+    n_iter = out["n_iter"]
+    sess.close()
+
+    if rank == 0:
+        ms_step = 1000.0 * elapsed / a.steps
+        value = a.steps * P * world / elapsed
+        total_k = sum(v["ms"] for v in ktimes.values())
+        dom = max(ktimes, key=lambda k: ktimes[k]["ms"])
+        dk = ktimes[dom]
+        avg_s = dk["ms"] / 1000.0 / max(1, dk["launches"])
+        bytes_launch = algorithmic_bytes(dom, nsub, nchan, nbin)
+        achieved = bytes_launch / avg_s / 1e9
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None, "avg_launch_ms": round(1000 * avg_s, 3),
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "kernel_share": round(dk["ms"] / total_k, 3)}
+        iter_bytes = 8 * P * nbin + 64 * P    # SURVEY §8(d) B_iter
+        loop_gbs = iter_bytes * n_iter / (elapsed / a.steps) / 1e9
+        rec = {
+            "metric": "profiles cleaned/sec (whole node)", "value": round(value, 1),
+            "unit": "profiles/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "%s %dx%dx%d (nsub x nchan x nbin), max_iter 5, thresholds 5/5,"
+                                   " exact leastsq fit" % (a.workload, nsub, nchan, nbin),
+                       "profiles_per_archive": P, "loops": loops[-1], "iterations": n_iter,
+                       "parallelism": "replicas" if world > 1 else "single",
+                       "loop_hbm_gbs": round(loop_gbs, 1),
+                       "loop_hbm_frac": round(loop_gbs / HBM_PEAK_GBS, 4)},
+            "roofline": roof,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            try:
+                rec["cpu_baseline"] = cpu_baseline(nchan, nbin, seed, rfi, a.cpu_budget)
+            except Exception as e:  # pragma: no cover
+                rec["cpu_baseline"] = {"value": None, "error": repr(e)}
+        if a.kernel_report:
+            for k, v in sorted(ktimes.items(), key=lambda kv: -kv[1]["ms"]):
+                print("%-16s %9.3f ms  %4d launches  %.3f ms/launch" %
+                      (k, v["ms"], v["launches"], v["ms"] / max(1, v["launches"])), file=sys.stderr)
+        print(json.dumps(rec))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

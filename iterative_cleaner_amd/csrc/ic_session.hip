@@ -1,6 +1,6 @@
 // ic_session.hip — host side of libicgpu.so: the C-ABI declared in
 // include/iterative_cleaner.h.  Owns device buffers and the HIP stream of a
-// session, prepares the fit cube once per upload, and drives the cleaning
+// session, prepares the fit cube at the start of every run, and drives the cleaning
 // loop of iterative_cleaner.py:83-146 (one launch sequence per iteration and
 // one small device->host read of the convergence counters).
 #include <hip/hip_runtime.h>
@@ -189,9 +189,6 @@ int prepare(Session *s)
     LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win));
     LAUNCH(s, K_BASE, launch_base(s->stream, s->raw, s->shift, s->win, nsub, nchan, nbin, s->width, s->base0));
     LAUNCH(s, K_FITCUBE, launch_fitcube(s->stream, s->raw, s->shift, s->base0, nsub, nchan, nbin, s->D));
-    CK(hipStreamSynchronize(s->stream));
-    s->uploaded = true;
-    s->ran = false;
     return 0;
 }
 
@@ -337,7 +334,10 @@ int ic_upload(void *session, const float *cube, const float *w0, const int32_t *
     CK(hipMemcpyAsync(s->raw, cube, sizeof(float) * s->N, hipMemcpyHostToDevice, s->stream));
     CK(hipMemcpyAsync(s->w0, w0, sizeof(float) * s->P, hipMemcpyHostToDevice, s->stream));
     CK(hipMemcpyAsync(s->shift, shift, sizeof(int32_t) * s->p.nchan, hipMemcpyHostToDevice, s->stream));
-    return prepare(s);
+    CK(hipStreamSynchronize(s->stream));
+    s->uploaded = true;
+    s->ran = false;
+    return IC_OK;
 }
 
 int ic_upload_device(void *session, const float *d_cube, const float *d_w0, const int32_t *d_shift)
@@ -348,7 +348,10 @@ int ic_upload_device(void *session, const float *d_cube, const float *d_w0, cons
     CK(hipMemcpyAsync(s->raw, d_cube, sizeof(float) * s->N, hipMemcpyDeviceToDevice, s->stream));
     CK(hipMemcpyAsync(s->w0, d_w0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
     CK(hipMemcpyAsync(s->shift, d_shift, sizeof(int32_t) * s->p.nchan, hipMemcpyDeviceToDevice, s->stream));
-    return prepare(s);
+    CK(hipStreamSynchronize(s->stream));
+    s->uploaded = true;
+    s->ran = false;
+    return IC_OK;
 }
 
 int ic_set_timing(void *session, int enabled)
@@ -388,9 +391,8 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
     const int nsub = p.nsub, nchan = p.nchan, nbin = p.nbin;
     int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > nbin ? nbin : p.pr_start);
     int pr_end = p.pr_end < 0 ? 0 : (p.pr_end > nbin ? nbin : p.pr_end);
-    // restore the initial weights (a session can be re-run)
-    CK(hipMemcpyAsync(s->W, s->w0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
-    CK(hipMemcpyAsync(s->hist, s->w0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
+    // fit cube (ic.py:96-100) + initial weights/history; a session can be re-run
+    if (int rc = prepare(s)) return rc;
     LineStatsArgs la;
     la.nsub = nsub;
     la.nchan = nchan;

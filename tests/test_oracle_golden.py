@@ -129,3 +129,22 @@ def test_numpy_template_matches_c(oracle_lib):
     T_np = ar.get_Profile(0, 0, 0).get_amps() * 10000
     T_c = oracle_lib.template(data[:, 0], w, shift)
     assert bits_equal(T_np, T_c)
+
+
+@pytest.mark.parametrize("name", ["s12x48x128", "s8x32x64_pol4", "s12x40x128_pr"])
+def test_reference_like_cpu_baseline(name):
+    """The CPU baseline timed by bench.py reproduces the reference's result."""
+    from oracle import reference_like
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import synth
+    z, meta, raw, w0, shift, args = load_clean_case(os.path.join(GOLDEN, "clean_%s.npz" % name))
+    data, w0_, shift_ = synth.make_cube(meta["nsub"], meta["nchan"], meta["nbin"], meta["seed"],
+                                        meta["rfi"], npol=meta["npol"])
+    ar = ica.Archive(data, w0_, shift_)
+    ar.pscrunch()
+    test, weights, loops = reference_like.clean_loop(ar, args["chanthresh"], args["subintthresh"],
+                                                     args["max_iter"], args["pulse_region"])
+    nit = int(z["n_iter"])
+    assert loops == int(z["loops"])
+    assert bits_equal(weights, z["weights_%d" % nit])
+    assert nan_equal(test, z["test_%d" % nit])
