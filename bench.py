@@ -78,20 +78,27 @@ def make_cube_device(nsub, nchan, nbin, seed, rfi, device):
     return cube.contiguous(), w0.contiguous(), shift.contiguous()
 
 
-def algorithmic_bytes(name, nsub, nchan, nbin):
-    """Bytes each kernel must move per launch."""
+def algorithmic_bytes(name, nsub, nchan, nbin, launches, stats, steps):
+    """Algorithmic bytes a kernel must move, summed over the timed region
+    (kernel table).  k_fit_pass: every profile-sweep reads its
+    4*nbin-byte profile once (sweep counts come from ic_get_run_stats)."""
     P = nsub * nchan
     N = P * nbin
     nsb = (nchan + 255) // 256
-    return {
+    per_launch = {
         "k_chan_partials": 4 * N + 8 * nsub * nsb * nbin,
         "k_base": int(4 * P * max(1, int(0.15 * nbin))),
         "k_fitcube": 8 * N,
-        "k_fit": 4 * N + 12 * P,
         "k_diag": 4 * N + 44 * P,
         "k_linestats": 2 * 4 * 8 * P,
         "k_combine": 4 * 8 * P + 2 * 4 * P,
-    }.get(name)
+        "k_fit_state": 2 * 204 * P,
+    }
+    if name == "k_fit_pass":
+        return 4 * nbin * stats["fit_profile_sweeps"] * steps
+    if name in per_launch:
+        return per_launch[name] * launches
+    return None
 
 
 def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
@@ -174,6 +181,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ktimes = sess.kernel_times()
+    stats = sess.run_stats()
     n_iter = out["n_iter"]
     sess.close()
 
@@ -184,13 +192,25 @@ def main():
         dom = max(ktimes, key=lambda k: ktimes[k]["ms"])
         dk = ktimes[dom]
         avg_s = dk["ms"] / 1000.0 / max(1, dk["launches"])
-        bytes_launch = algorithmic_bytes(dom, nsub, nchan, nbin)
-        achieved = bytes_launch / avg_s / 1e9
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+        total_bytes = algorithmic_bytes(dom, nsub, nchan, nbin, dk["launches"], stats, a.steps)
+        bytes_launch = total_bytes / max(1, dk["launches"]) if total_bytes else None
+        achieved = bytes_launch / avg_s / 1e9 if bytes_launch else None
+        roof = {"bound": "hbm", "kernel": dom,
+                "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": None, "avg_launch_ms": round(1000 * avg_s, 3),
-                "algorithmic_bytes_per_launch": bytes_launch,
+                "algorithmic_bytes_per_launch": int(bytes_launch) if bytes_launch else None,
                 "kernel_share": round(dk["ms"] / total_k, 3)}
+        per_kernel = {}
+        for kname, kv in ktimes.items():
+            if kv["launches"] == 0:
+                continue
+            tb = algorithmic_bytes(kname, nsub, nchan, nbin, kv["launches"], stats, a.steps)
+            per_kernel[kname] = {"ms_per_step": round(kv["ms"] / a.steps, 3),
+                                 "launches_per_step": kv["launches"] // a.steps,
+                                 "gbs": round(tb / (kv["ms"] / 1000.0) / 1e9, 1) if tb else None}
+        roof["per_kernel"] = per_kernel
         iter_bytes = 8 * P * nbin + 64 * P    # SURVEY §8(d) B_iter
         loop_gbs = iter_bytes * n_iter / (elapsed / a.steps) / 1e9
         rec = {
@@ -201,6 +221,8 @@ def main():
             "config": {"workload": "%s %dx%dx%d (nsub x nchan x nbin), max_iter 5, thresholds 5/5,"
                                    " exact leastsq fit" % (a.workload, nsub, nchan, nbin),
                        "profiles_per_archive": P, "loops": loops[-1], "iterations": n_iter,
+                       "fit_rounds": stats["fit_rounds"],
+                       "fit_sweeps_per_profile": round(stats["fit_profile_sweeps"] / P / max(1, n_iter), 2),
                        "parallelism": "replicas" if world > 1 else "single",
                        "loop_hbm_gbs": round(loop_gbs, 1),
                        "loop_hbm_frac": round(loop_gbs / HBM_PEAK_GBS, 4)},

@@ -107,6 +107,14 @@ int ic_get_kernel_times(void *session, ic_kernel_time *out, int n);
 const char *ic_kernel_name(int kernel);
 int ic_set_timing(void *session, int enabled);
 
+/* Statistics of the last ic_run (measurement; see DESIGN.md roofline). */
+typedef struct {
+    int32_t iterations;          /* cleaning loops executed                        */
+    int32_t fit_rounds;          /* k_fit_pass launches, summed over iterations    */
+    int64_t fit_profile_sweeps;  /* profiles swept by k_fit_pass, summed (x nbin x 4 B = fit bytes) */
+} ic_run_stats;
+int ic_get_run_stats(void *session, ic_run_stats *out);
+
 const char *ic_last_error(void);
 
 #ifdef __cplusplus

@@ -18,7 +18,7 @@ ABI_VERSION = 1
 EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session_destroy",
            "ic_upload", "ic_upload_device", "ic_run", "ic_get_residual", "ic_get_template",
            "ic_get_fit", "ic_get_diagnostics", "ic_get_kernel_times", "ic_kernel_name",
-           "ic_set_timing", "ic_last_error")
+           "ic_set_timing", "ic_get_run_stats", "ic_last_error")
 
 
 class NativeError(RuntimeError):
@@ -31,6 +31,11 @@ class Params(C.Structure):
                 ("subintthresh", C.c_double), ("pr_on", C.c_int32), ("pr_factor", C.c_double),
                 ("pr_start", C.c_int32), ("pr_end", C.c_int32), ("baseline_duty", C.c_double),
                 ("fit_mode", C.c_int32)]
+
+
+class RunStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("fit_rounds", C.c_int32),
+                ("fit_profile_sweeps", C.c_int64)]
 
 
 class KernelTime(C.Structure):
@@ -70,6 +75,7 @@ def load_library(path: str = LIB_PATH):
     lib.ic_get_diagnostics.argtypes = [vp, vp, vp, vp, vp]
     lib.ic_get_kernel_times.argtypes = [vp, C.POINTER(KernelTime), C.c_int]
     lib.ic_set_timing.argtypes = [vp, C.c_int]
+    lib.ic_get_run_stats.argtypes = [vp, C.POINTER(RunStats)]
     if lib.ic_abi_version() != ABI_VERSION:
         raise NativeError("libicgpu ABI %d != expected %d" % (lib.ic_abi_version(), ABI_VERSION))
     _lib = lib
@@ -197,6 +203,12 @@ class GpuSession:
 
     def set_timing(self, on: bool):
         self._check(self.lib.ic_set_timing(self.h, 1 if on else 0), "ic_set_timing")
+
+    def run_stats(self):
+        st = RunStats()
+        self._check(self.lib.ic_get_run_stats(self.h, C.byref(st)), "ic_get_run_stats")
+        return dict(iterations=st.iterations, fit_rounds=st.fit_rounds,
+                    fit_profile_sweeps=int(st.fit_profile_sweeps))
 
     def kernel_times(self):
         buf = (KernelTime * 32)()

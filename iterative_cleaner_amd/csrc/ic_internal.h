@@ -8,6 +8,7 @@ namespace icgpu {
 
 constexpr int kSuperBlock = 256;    // canonical channel super-block (archive.py SUPER_BLOCK)
 constexpr int kMaxLeaves = 256;     // pairwise-sum leaves (nbin <= 32768)
+constexpr int kFitTile = 32;        // bins per k_fit_pass LDS tile (fit cube row padding)
 
 // numpy pairwise-summation plan for one nbin (numpy loops_utils.h.src order):
 // leaves in address order, then a post-order list of internal adds.
@@ -29,12 +30,22 @@ enum KernelId {
     K_FITCUBE,
     K_FSCRUNCH,
     K_TSCRUNCH,
-    K_FIT,
+    K_FIT_PASS,
+    K_FIT_STATE,
     K_DIAG,
     K_LINESTATS,
     K_COMBINE,
     K_RESIDUAL,
     K_COUNT
+};
+
+// lmdif per-profile state (structure of arrays, device memory)
+struct FitStateArrays {
+    double *x, *fnorm, *par, *delta, *diag, *xnorm, *acnorm, *J0, *f0, *aj, *r, *Jn0, *qtf, *gnorm,
+        *x2, *pnorm, *wa1, *xa;
+    int32_t *iter, *nfev, *mode, *slow;
+    double *o_fnorm, *o_acnorm, *o_f0, *o_J0, *o_sum;
+    int32_t *o_exact;
 };
 
 struct LineStatsArgs {
@@ -55,16 +66,19 @@ hipError_t launch_window(hipStream_t st, const double *part, int nsub, int nsb, 
 hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, const int32_t *win,
                        int nsub, int nchan, int nbin, int width, float *base);
 hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
-                          int nsub, int nchan, int nbin, float *D);
+                          int nsub, int nchan, int nbin, int ldD, float *D);
 hipError_t launch_fscrunch(hipStream_t st, const double *part, const double *wpart, int nsub, int nsb,
                            int nbin, float *F, float *wf);
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
                            double *T64);
-hipError_t launch_fit(hipStream_t st, const float *D, const double *T64, long P, int nbin, double *amp,
-                      int32_t *info);
+hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
+hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
+                           const FitStateArrays &S);
+hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, double *amp, int32_t *info,
+                            int32_t *active);
 hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const double *amp,
                        const int32_t *info, const float *w0, const int32_t *shift, const double2 *tw,
-                       const PwPlan *plan, int nsub, int nchan, int nbin, int pr_on, double pr_factor,
+                       const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
                        int pr_start, int pr_end, double *std_o, double *mean_o, float *ptp_o,
                        double *fft_o);
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a);
@@ -75,7 +89,7 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
                           double subintthresh, double *test, float *W, float *hist, int iter,
                           int32_t *counters);
 hipError_t launch_residual(hipStream_t st, const float *D, const double *T64, const double *amp,
-                           const int32_t *info, const int32_t *shift, int nsub, int nchan, int nbin,
+                           const int32_t *info, const int32_t *shift, int nsub, int nchan, int nbin, int ldD,
                            int pr_on, double pr_factor, int pr_start, int pr_end, float *R);
 
 }  // namespace icgpu

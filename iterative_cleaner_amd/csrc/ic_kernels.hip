@@ -21,6 +21,7 @@
 //   k_linestats      per channel / subint median & MAD (ic.py:229-256)
 //   k_combine        scale, max, median-of-4, threshold, new weights,
 //                    convergence counters (ic.py:221-225, :303-305, :127-141)
+#include <algorithm>
 #include <float.h>
 #include <math.h>
 #include <stdint.h>
@@ -31,6 +32,15 @@ namespace icgpu {
 
 __device__ constexpr double kRdwarf = 3.834e-20;
 __device__ constexpr double kRgiant = 1.304e19;
+
+// LDS ordering between lanes of ONE wave: DS instructions of a wave execute in
+// order, so only compiler reordering must be prevented (no s_barrier).
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // ============================================================ template stage
 
@@ -130,39 +140,65 @@ __global__ __launch_bounds__(256) void k_window(const double *__restrict__ part,
     if (threadIdx.x == 0) win[s] = bi[0];
 }
 
-// base[k] = f32( (sum_{k<width} f64(ded[(win+k)%n])) / width ), one lane per profile.
+// base[k] = f32( (sum_{t<width} f64(ded[(win+t)%n])) / width ), sequential in t.
+// One wave per 64 profiles; window chunks of 64 positions are loaded coalesced
+// (one profile row per load instruction) into a transposed LDS tile, then each
+// lane adds its own profile's column in order.
 __global__ __launch_bounds__(256) void k_base(const float *__restrict__ raw, const int32_t *__restrict__ shift,
                                               const int32_t *__restrict__ win, int nsub, int nchan,
                                               int nbin, int width, float *__restrict__ base)
 {
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= (size_t)nsub * nchan) return;
-    const int s = (int)(k / nchan);
-    const int c = (int)(k % nchan);
-    int q = win[s] + shift[c];
-    if (q >= nbin) q -= nbin;
-    const float *prof = raw + k * nbin;
-    double acc = 0.0;
-    for (int t = 0; t < width; ++t) {
-        acc = acc + (double)prof[q];
-        if (++q == nbin) q = 0;
+    __shared__ float buf[4][64][65];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const size_t P = (size_t)nsub * nchan;
+    const size_t k0 = ((size_t)blockIdx.x * 4 + wave) * 64;
+    if (k0 >= P) return;
+    const size_t k = k0 + lane;
+    const bool live = k < P;
+    int q0 = 0;
+    if (live) {
+        q0 = win[k / nchan] + shift[k % nchan];
+        if (q0 >= nbin) q0 -= nbin;
     }
-    base[k] = (float)(acc / (double)width);
+    float(*t)[65] = buf[wave];
+    double acc = 0.0;
+    for (int c0 = 0; c0 < width; c0 += 64) {
+        wave_sync();
+        for (int r = 0; r < 64; ++r) {
+            const size_t kr = k0 + r;
+            const int qr = __shfl(q0, r);
+            float v = 0.0f;
+            if (kr < P && c0 + lane < width) {
+                int q = qr + c0 + lane;
+                q %= nbin;
+                v = raw[kr * nbin + q];
+            }
+            t[lane][r] = v;
+        }
+        wave_sync();
+        const int cn = min(64, width - c0);
+        for (int q = 0; q < cn; ++q) acc = acc + (double)t[q][lane];
+    }
+    if (live) base[k] = (float)(acc / (double)width);
 }
 
-// D[k][i] = f32(ded[k][i] - base0[k])  (fit cube, dedispersed frame); grid-stride over N
+// D[k][i] = f32(ded[k][i] - base0[k])  (fit cube, dedispersed frame); one row per wave step
 __global__ __launch_bounds__(256) void k_fitcube(const float *__restrict__ raw, const int32_t *__restrict__ shift,
                                                  const float *__restrict__ base, int nsub, int nchan,
-                                                 int nbin, float *__restrict__ D)
+                                                 int nbin, int ldD, float *__restrict__ D)
 {
-    const size_t N = (size_t)nsub * nchan * nbin;
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += (size_t)gridDim.x * blockDim.x) {
-        const size_t k = e / nbin;
-        const int i = (int)(e - k * nbin);
-        const int c = (int)(k % nchan);
-        int j = i + shift[c];
-        if (j >= nbin) j -= nbin;
-        D[e] = raw[k * nbin + j] - base[k];
+    const size_t P = (size_t)nsub * nchan;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (size_t k = (size_t)blockIdx.x * 4 + wave; k < P; k += (size_t)gridDim.x * 4) {
+        const int sh = shift[k % nchan];
+        const float b = base[k];
+        const float *src = raw + k * nbin;
+        float *dst = D + k * ldD;
+        for (int i = lane; i < nbin; i += 64) {
+            int j = i + sh;
+            if (j >= nbin) j -= nbin;
+            dst[i] = src[j] - b;
+        }
     }
 }
 
@@ -470,113 +506,308 @@ __device__ int lm_after_a2(LmState &L, double fnorm1)
     return lm_outer(L);
 }
 
-#define FIT_TB 64
+#define FIT_TB kFitTile
 
-// One lane per profile, 64 profiles per block (one wave).  Each lane runs the
-// MINPACK lmdif state machine; the data passes it needs (A: f(xa) norm +
-// Jacobian norm at xa; B: sum_i Jn_i*fvec_i) are served by wave-wide sweeps
-// over the profiles' samples, staged through an LDS tile (transposed so
-// lane l reads column l conflict-free).
-__global__ __launch_bounds__(64) void k_fit(const float *__restrict__ D, const double *__restrict__ T64,
-                                            long P, int nbin, double *__restrict__ amp_o,
-                                            int32_t *__restrict__ info_o)
+// Exact fast path.  enorm: while every component is 0 or inside
+// (RDWARF, agiant) MINPACK's enorm reduces to sqrt(sum_seq a*a); that range is
+// verified per lane with integer compares on the high words (conservatively:
+// equal high words count as out of range).  Division: q = RN(a/b) from the
+// correctly rounded reciprocal y = RN(1/b) with two FMA corrections; after
+// the first, q1 is within one ulp, so the second (Markstein) correction is
+// exactly RN(a/b) barring over/underflow — which would push J out of the
+// verified enorm range and send the lane to the exact pass.
+struct FastAcc {
+    double s2;
+    uint32_t maxhi, minhm1;
+};
+
+__device__ __forceinline__ void fa_zero(FastAcc &a)
 {
-    __shared__ float tile[FIT_TB][65];
-    const int lane = threadIdx.x;
-    const long k0 = (long)blockIdx.x * 64;
-    const long k = k0 + lane;
-    const bool live = k < P;
-    const double agiant = kRgiant / (double)nbin;
-    const double eps = sqrt(DBL_EPSILON);  // sqrt(max(epsfcn, epsmch))
+    a.s2 = 0.0;
+    a.maxhi = 0u;
+    a.minhm1 = 0xffffffffu;
+}
 
-    LmState L;
-    L.x = 1.0; L.fnorm = 0.0; L.par = 0.0; L.delta = 0.0; L.diag = 0.0; L.xnorm = 0.0;
-    L.acnorm = 0.0; L.J0 = 0.0; L.f0 = 0.0; L.acn2 = 0.0; L.J02 = 0.0; L.f02 = 0.0;
-    L.aj = 0.0; L.r = 0.0; L.Jn0 = 0.0; L.qtf = 0.0; L.gnorm = 0.0; L.x2 = 0.0; L.pnorm = 0.0;
-    L.wa1 = 0.0; L.iter = 1; L.nfev = 0; L.info = 0;
-    int st = live ? ST_A0 : ST_DONE;
+__device__ __forceinline__ void fa_add(FastAcc &a, double v)
+{
+    const double av = fabs(v);
+    const double sq = av * av;
+    a.s2 = a.s2 + sq;
+    const uint32_t hi = (uint32_t)((unsigned long long)__double_as_longlong(av) >> 32);
+    a.maxhi = max(a.maxhi, hi);
+    a.minhm1 = min(a.minhm1, hi - 1u);   // zero -> 0xffffffff
+}
 
-    for (;;) {
-        const bool reqA = (st == ST_A0) || (st == ST_A2);
-        const bool reqB = (st == ST_B);
-        const bool anyA = __any(reqA);
-        const bool anyB = __any(reqB);
-        if (!anyA && !anyB) break;
-        const double xa = (st == ST_A0) ? L.x : L.x2;
-        double ha = eps * fabs(xa);
-        if (ha == 0.0) ha = eps;
-        const double xha = xa + ha;
-        double hb = eps * fabs(L.x);
-        if (hb == 0.0) hb = eps;
-        const double xhb = L.x + hb;
-        const double xb = L.x;
-        const double ajb = L.aj;
-        Enorm eF, eJ;
-        en_zero(eF);
-        en_zero(eJ);
-        double fa0 = 0.0, Ja0 = 0.0, sum = 0.0;
-        for (int b0 = 0; b0 < nbin; b0 += FIT_TB) {
-            const int tb = min(FIT_TB, nbin - b0);
-            __syncthreads();
-            for (int m = 0; m < 64; ++m) {
-                const long kk = k0 + m;
-                float v = 0.0f;
-                if (lane < tb && kk < P) v = D[kk * nbin + b0 + lane];
-                tile[lane][m] = v;
-            }
-            __syncthreads();
-            for (int ii = 0; ii < tb; ++ii) {
+__device__ __forceinline__ bool fa_ok(const FastAcc &a, uint32_t hr1, uint32_t hg)
+{
+    const bool lo_ok = (a.minhm1 == 0xffffffffu) || (a.minhm1 + 1u >= hr1);
+    return lo_ok && (a.maxhi < hg);
+}
+
+__device__ __forceinline__ double fa_fin(const FastAcc &a) { return a.s2 != 0.0 ? sqrt(a.s2) : 0.0; }
+
+__device__ __forceinline__ double mdiv(double a, double b, double y)
+{
+    const double q0 = a * y;
+    const double r0 = fma(-b, q0, a);
+    const double q1 = fma(r0, y, q0);
+    const double r1 = fma(-b, q1, a);
+    return fma(r1, y, q1);
+}
+
+__device__ __forceinline__ bool x_in_fast_range(double x)
+{
+    const double ax = fabs(x);
+    return ax >= 0x1p-500 && ax <= 0x1p500;
+}
+
+// Load a 64-profile x FIT_TB-bin tile of D into LDS, transposed to tile[bin][profile].
+// D is padded to [roundup(P,64)][ldD], ldD = roundup(nbin, FIT_TB): no guards.
+__device__ __forceinline__ void load_tile(float (*tile)[65], const float *__restrict__ D, long k0, int ldD,
+                                          int b0, int lane)
+{
+    const int c4 = (lane & 7) * 4;
+    const int r0 = lane >> 3;
+    const float *base = D + (size_t)(k0 + r0) * ldD + b0 + c4;
+    float4 v[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = *(const float4 *)(base + (size_t)m * 8 * ldD);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int r = m * 8 + r0;
+        tile[c4 + 0][r] = v[m].x;
+        tile[c4 + 1][r] = v[m].y;
+        tile[c4 + 2][r] = v[m].z;
+        tile[c4 + 3][r] = v[m].w;
+    }
+}
+
+struct PassIn {
+    bool A, B;                   // lane takes part in pass A / B
+    double xa, xha, ha, yha;     // A: f(xa) and J(xa)
+    double xb, xhb, hb, yhb, ajb, yaj;  // B: sum Jn*f at xb
+};
+
+struct PassOut {
+    double fnorm, acnorm, f0, J0, sum;
+    bool bad;                    // fast path left its verified range
+};
+
+template <bool EXACT>
+__device__ void fit_sweep(float (*tile)[65], const float *__restrict__ D, const double *__restrict__ T64,
+                          long k0, int ldD, int nbin, int lane, const PassIn &in, bool anyA, bool anyB,
+                          double agiant, PassOut &out)
+{
+    FastAcc fF, fJ;
+    fa_zero(fF);
+    fa_zero(fJ);
+    Enorm eF, eJ;
+    en_zero(eF);
+    en_zero(eJ);
+    double fa0 = 0.0, Ja0 = 0.0, sum = 0.0;
+    for (int b0 = 0; b0 < nbin; b0 += FIT_TB) {
+        __syncthreads();
+        load_tile(tile, D, k0, ldD, b0, lane);
+        __syncthreads();
+        const int tb = min(FIT_TB, nbin - b0);
+#pragma unroll 2
+        for (int ii = 0; ii < FIT_TB; ++ii) {
+            if (ii < tb) {
                 const int i = b0 + ii;
                 const double t = T64[i];
                 const double pv = (double)tile[ii][lane];
-                if (anyA && reqA) {
-                    const double u = xa * t;
+                if (anyA && in.A) {
+                    const double u = in.xa * t;
                     const double f = u - pv;
-                    en_add(eF, f, agiant);
-                    const double uh = xha * t;
+                    const double uh = in.xha * t;
                     const double wa = uh - pv;
                     const double d = wa - f;
-                    const double J = d / ha;
-                    en_add(eJ, J, agiant);
+                    double J;
+                    if (EXACT) {
+                        en_add(eF, f, agiant);
+                        J = d / in.ha;
+                        en_add(eJ, J, agiant);
+                    } else {
+                        fa_add(fF, f);
+                        J = mdiv(d, in.ha, in.yha);
+                        fa_add(fJ, J);
+                    }
                     if (i == 0) {
                         fa0 = f;
                         Ja0 = J;
                     }
                 }
-                if (anyB && reqB) {
-                    const double u = xb * t;
+                if (anyB && in.B) {
+                    const double u = in.xb * t;
                     const double f = u - pv;
-                    const double uh = xhb * t;
+                    const double uh = in.xhb * t;
                     const double wa = uh - pv;
                     const double d = wa - f;
-                    const double J = d / hb;
-                    double Jn = J / ajb;
+                    double J, Jn;
+                    if (EXACT) {
+                        J = d / in.hb;
+                        Jn = J / in.ajb;
+                    } else {
+                        J = mdiv(d, in.hb, in.yhb);
+                        Jn = mdiv(J, in.ajb, in.yaj);
+                    }
                     if (i == 0) Jn = Jn + 1.0;
                     const double pr = Jn * f;
                     sum = sum + pr;
                 }
             }
         }
-        if (st == ST_A0) {
-            L.fnorm = en_fin(eF);
-            L.nfev = 1;
-            L.acnorm = en_fin(eJ);
-            L.f0 = fa0;
-            L.J0 = Ja0;
-            st = lm_outer(L);
-        } else if (st == ST_A2) {
-            L.acn2 = en_fin(eJ);
-            L.f02 = fa0;
-            L.J02 = Ja0;
-            st = lm_after_a2(L, en_fin(eF));
-        } else if (st == ST_B) {
-            st = lm_after_b(L, sum);
+    }
+    out.f0 = fa0;
+    out.J0 = Ja0;
+    out.sum = sum;
+    if (EXACT) {
+        out.fnorm = en_fin(eF);
+        out.acnorm = en_fin(eJ);
+        out.bad = false;
+    } else {
+        const uint32_t hr1 = (uint32_t)((unsigned long long)__double_as_longlong(kRdwarf) >> 32) + 1u;
+        const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant) >> 32);
+        out.fnorm = fa_fin(fF);
+        out.acnorm = fa_fin(fJ);
+        out.bad = in.A && !(fa_ok(fF, hr1, hg) && fa_ok(fJ, hr1, hg));
+    }
+}
+
+// ---- split lmdif: state machine (k_fit_state) <-> data sweeps (k_fit_pass) ----
+// Per-profile state lives in HBM as structure-of-arrays (FitState below);
+// a round is one k_fit_pass (every profile with a pending request reads its
+// samples once) followed by one k_fit_state (each lane consumes its sweep
+// result and runs MINPACK's scalar logic up to its next data request).
+
+__device__ __forceinline__ void lm_load(LmState &L, const FitStateArrays &S, long k)
+{
+    L.x = S.x[k]; L.fnorm = S.fnorm[k]; L.par = S.par[k]; L.delta = S.delta[k]; L.diag = S.diag[k];
+    L.xnorm = S.xnorm[k]; L.acnorm = S.acnorm[k]; L.J0 = S.J0[k]; L.f0 = S.f0[k];
+    L.aj = S.aj[k]; L.r = S.r[k]; L.Jn0 = S.Jn0[k]; L.qtf = S.qtf[k]; L.gnorm = S.gnorm[k];
+    L.x2 = S.x2[k]; L.pnorm = S.pnorm[k]; L.wa1 = S.wa1[k];
+    L.iter = S.iter[k]; L.nfev = S.nfev[k]; L.info = 0;
+    L.acn2 = 0.0; L.J02 = 0.0; L.f02 = 0.0;
+}
+
+__device__ __forceinline__ void lm_store(const LmState &L, const FitStateArrays &S, long k)
+{
+    S.x[k] = L.x; S.fnorm[k] = L.fnorm; S.par[k] = L.par; S.delta[k] = L.delta; S.diag[k] = L.diag;
+    S.xnorm[k] = L.xnorm; S.acnorm[k] = L.acnorm; S.J0[k] = L.J0; S.f0[k] = L.f0;
+    S.aj[k] = L.aj; S.r[k] = L.r; S.Jn0[k] = L.Jn0; S.qtf[k] = L.qtf; S.gnorm[k] = L.gnorm;
+    S.x2[k] = L.x2; S.pnorm[k] = L.pnorm; S.wa1[k] = L.wa1;
+    S.iter[k] = L.iter; S.nfev[k] = L.nfev;
+}
+
+// request encoding in S.mode: ST_A0 / ST_A2 -> sweep A at S.xa; ST_B -> sweep B
+// at (S.x, S.aj); ST_DONE -> nothing.  S.slow: J at x came from an exact sweep.
+__global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
+{
+    const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P) return;
+    S.mode[k] = ST_A0;
+    S.xa[k] = 1.0;
+    S.x[k] = 1.0; S.par[k] = 0.0; S.iter[k] = 1; S.nfev[k] = 0; S.slow[k] = 0;
+}
+
+__global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, const double *__restrict__ T64,
+                                                 long P, int nbin, int ldD, FitStateArrays S)
+{
+    __shared__ float tile[FIT_TB][65];
+    const int lane = threadIdx.x;
+    const long k0 = (long)blockIdx.x * 64;
+    const long k = k0 + lane;
+    const int st = (k < P) ? S.mode[k] : ST_DONE;
+    const bool reqA = (st == ST_A0) || (st == ST_A2);
+    const bool reqB = (st == ST_B);
+    if (!__any(reqA || reqB)) return;
+    const double agiant = kRgiant / (double)nbin;
+    const double eps = sqrt(DBL_EPSILON);
+    PassIn in;
+    in.xa = reqA ? S.xa[k] : 1.0;
+    in.ha = eps * fabs(in.xa);
+    if (in.ha == 0.0) in.ha = eps;
+    in.xha = in.xa + in.ha;
+    in.yha = 1.0 / in.ha;
+    in.xb = reqB ? S.x[k] : 1.0;
+    in.hb = eps * fabs(in.xb);
+    if (in.hb == 0.0) in.hb = eps;
+    in.xhb = in.xb + in.hb;
+    in.yhb = 1.0 / in.hb;
+    in.ajb = reqB ? S.aj[k] : 1.0;
+    in.yaj = 1.0 / in.ajb;
+    const bool slow = reqB && S.slow[k];
+    const bool fastA = reqA && x_in_fast_range(in.xa);
+    const bool fastB = reqB && !slow && x_in_fast_range(in.xb) && x_in_fast_range(in.ajb);
+    in.A = fastA;
+    in.B = fastB;
+    PassOut o;
+    o.bad = false;
+    o.fnorm = o.acnorm = o.f0 = o.J0 = o.sum = 0.0;
+    if (__any(fastA || fastB))
+        fit_sweep<false>(tile, D, T64, k0, ldD, nbin, lane, in, __any(fastA), __any(fastB), agiant, o);
+    const bool exA = reqA && (!fastA || o.bad);
+    const bool exB = reqB && !fastB;
+    if (__any(exA || exB)) {
+        PassIn ie = in;
+        ie.A = exA;
+        ie.B = exB;
+        PassOut oe;
+        fit_sweep<true>(tile, D, T64, k0, ldD, nbin, lane, ie, __any(exA), __any(exB), agiant, oe);
+        if (exA || exB) o = oe;
+    }
+    if (reqA) {
+        S.o_fnorm[k] = o.fnorm;
+        S.o_acnorm[k] = o.acnorm;
+        S.o_f0[k] = o.f0;
+        S.o_J0[k] = o.J0;
+        S.o_exact[k] = exA ? 1 : 0;
+    }
+    if (reqB) S.o_sum[k] = o.sum;
+}
+
+// Consume the sweep result, run lmdif's scalar logic to the next request.
+// counters[0] += number of profiles still needing a sweep.
+__global__ __launch_bounds__(256) void k_fit_state(FitStateArrays S, long P, double *__restrict__ amp_o,
+                                                   int32_t *__restrict__ info_o, int32_t *__restrict__ active)
+{
+    const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    int still = 0;
+    if (k < P) {
+        int st = S.mode[k];
+        if (st != ST_DONE) {
+            LmState L;
+            lm_load(L, S, k);
+            if (st == ST_A0) {
+                L.fnorm = S.o_fnorm[k];
+                L.nfev = 1;
+                L.acnorm = S.o_acnorm[k];
+                L.f0 = S.o_f0[k];
+                L.J0 = S.o_J0[k];
+                S.slow[k] = S.o_exact[k];
+                st = lm_outer(L);
+            } else if (st == ST_A2) {
+                L.acn2 = S.o_acnorm[k];
+                L.f02 = S.o_f0[k];
+                L.J02 = S.o_J0[k];
+                st = lm_after_a2(L, S.o_fnorm[k]);
+                if (L.x == L.x2) S.slow[k] = S.o_exact[k];
+            } else {
+                st = lm_after_b(L, S.o_sum[k]);
+            }
+            lm_store(L, S, k);
+            S.mode[k] = st;
+            if (st == ST_A2) S.xa[k] = L.x2;
+            if (st == ST_DONE) {
+                amp_o[k] = L.x;
+                info_o[k] = L.info;
+            } else {
+                still = 1;
+            }
         }
     }
-    if (live) {
-        amp_o[k] = L.x;
-        info_o[k] = L.info;
-    }
+    for (int off = 32; off > 0; off >>= 1) still += __shfl_xor(still, off);
+    if ((threadIdx.x & 63) == 0 && still) atomicAdd(active, still);
 }
 
 // ============================================================ diagnostics
@@ -605,7 +836,7 @@ __device__ Tp wave_pairwise(const PwPlan &pl, Get get, Tp *scratch, int lane)
         for (int q = 8; q < main; q += 8) r = r + get(st + q + j);
         acc[task] = r;
     }
-    __syncthreads();
+    wave_sync();
     for (int Lf = lane; Lf < nl; Lf += 64) {
         const int st = pl.leaf_start[Lf], len = pl.leaf_len[Lf];
         const Tp *r = acc + Lf * 8;
@@ -620,198 +851,588 @@ __device__ Tp wave_pairwise(const PwPlan &pl, Get get, Tp *scratch, int lane)
         }
         slot[Lf] = res;
     }
-    __syncthreads();
+    wave_sync();
     Tp out = (Tp)0;
     if (lane == 0) {
         for (int o = 0; o < pl.nops; ++o) slot[nl + o] = slot[pl.op_a[o]] + slot[pl.op_b[o]];
         out = (Tp)0 + slot[pl.root];
         acc[0] = out;
     }
-    __syncthreads();
+    wave_sync();
     out = acc[0];
-    __syncthreads();
+    wave_sync();
     return out;
 }
 
-// One wave per profile.  LDS: X f32 [nbin] | complex f64 work [nbin/2 or nbin] |
-// pairwise scratch.  Computes the f32 residual (iterative_cleaner.py:279-288,
-// :272), dededisperses it (:104), applies the ORIGINAL weight (:296) and
-// the four diagnostics (:206-217) with numpy.ma data conventions.
-__global__ __launch_bounds__(64) void k_diag(
+// Persistent blocks of `wpb` independent waves; each wave cleans profiles
+// k = blockIdx.x*wpb + wave, += gridDim.x*wpb.  LDS: plan + twiddles (block-shared,
+// loaded once) | per wave: complex work [n/2] (pow2) | X f32 [n] | pairwise scratch.
+// Per profile: the f32 residual (iterative_cleaner.py:279-288, :272), dededispersion
+// (:104), the ORIGINAL weight (:296) and the four diagnostics (:206-217) with
+// numpy.ma data conventions.
+// ---- mixed-radix (8/4/2) Stockham FFT helpers (forward, exp(-2 pi i jk/N)) ----
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 w)
+{
+    return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+__device__ __forceinline__ double2 mul_mi(double2 a) { return make_double2(a.y, -a.x); }   // * (-i)
+
+template <int R>
+__device__ __forceinline__ void dft_small(double2 (&v)[R]);
+
+template <>
+__device__ __forceinline__ void dft_small<2>(double2 (&v)[2])
+{
+    const double2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+}
+
+template <>
+__device__ __forceinline__ void dft_small<4>(double2 (&v)[4])
+{
+    const double2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+    const double2 s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
+    v[0] = cadd(s02, s13);
+    v[2] = csub(s02, s13);
+    v[1] = cadd(d02, d13);
+    v[3] = csub(d02, d13);
+}
+
+template <>
+__device__ __forceinline__ void dft_small<8>(double2 (&v)[8])
+{
+    double2 e[4] = {v[0], v[2], v[4], v[6]};
+    double2 o[4] = {v[1], v[3], v[5], v[7]};
+    dft_small<4>(e);
+    dft_small<4>(o);
+    const double h = 0.70710678118654752440;   // sqrt(1/2)
+    // o_k * exp(-2 pi i k/8), k = 0..3
+    const double2 o1 = make_double2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
+    const double2 o2 = mul_mi(o[2]);
+    const double2 o3 = make_double2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
+    v[0] = cadd(e[0], o[0]);
+    v[4] = csub(e[0], o[0]);
+    v[1] = cadd(e[1], o1);
+    v[5] = csub(e[1], o1);
+    v[2] = cadd(e[2], o2);
+    v[6] = csub(e[2], o2);
+    v[3] = cadd(e[3], o3);
+    v[7] = csub(e[3], o3);
+}
+
+// exp(-2 pi i q/n) for 0 <= q < n from the half table tw[0..n/2)
+__device__ __forceinline__ double2 twid(const double2 *tw, int q, int half)
+{
+    if (q < half) return tw[q];
+    const double2 t = tw[q - half];
+    return make_double2(-t.x, -t.y);
+}
+
+// One radix-R Stockham stage over m points (src -> dst), Ns = product of earlier radices.
+// get(q) supplies src point q (lets the first stage read the real input directly).
+template <int R, typename Get>
+__device__ __forceinline__ void stockham_stage(Get get, double2 *dst, int m, int Ns, const double2 *tw, int n,
+                                               int lane)
+{
+    const int nb = m / R;
+    const int tmul = n / (R * Ns);
+    for (int b = lane; b < nb; b += 64) {
+        const int k = b & (Ns - 1);
+        double2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = get(b + r * nb);
+        if (Ns > 1) {
+#pragma unroll
+            for (int r = 1; r < R; ++r) v[r] = cmul(v[r], twid(tw, r * k * tmul, n / 2));
+        }
+        dft_small<R>(v);
+        const int idx = (b - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) dst[idx + r * Ns] = v[r];
+    }
+}
+
+struct DiagLayout {
+    int ntw;          // twiddles in LDS
+    size_t cw_off, x_off, scr_off, per_wave;
+};
+
+__host__ __device__ inline DiagLayout diag_layout(int n, int nleaf, int nops)
+{
+    DiagLayout L;
+    const bool pow2 = (n & (n - 1)) == 0 && n >= 4;
+    L.ntw = pow2 ? n / 2 : n;
+    L.cw_off = 0;                                            // buffer A: n/2 complex
+    const size_t cwb = (size_t)(pow2 ? n / 2 : 1) * 16;
+    L.x_off = cwb;                                           // buffer B (n/2 complex) aliases X (n f32)
+    const size_t xb = ((size_t)n * 4 + 15) & ~(size_t)15;
+    L.scr_off = L.x_off + (pow2 ? (cwb > xb ? cwb : xb) : xb);
+    L.per_wave = L.scr_off + (size_t)(nleaf * 9 + nops + 8) * 8;
+    L.per_wave = (L.per_wave + 15) & ~(size_t)15;
+    return L;
+}
+
+__global__ __launch_bounds__(256) void k_diag(
     const float *__restrict__ D, const double *__restrict__ T64, const double *__restrict__ amp,
     const int32_t *__restrict__ info, const float *__restrict__ w0, const int32_t *__restrict__ shift,
-    const double2 *__restrict__ tw, const PwPlan *__restrict__ plan_g, int nsub, int nchan, int nbin,
+    const double2 *__restrict__ tw_g, const PwPlan *__restrict__ plan_g, int nsub, int nchan, int nbin, int ldD,
     int pr_on, double pr_factor, int pr_start, int pr_end, double *__restrict__ std_o,
     double *__restrict__ mean_o, float *__restrict__ ptp_o, double *__restrict__ fft_o)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ PwPlan pl;
     const int n = nbin;
-    const int lane = threadIdx.x;
-    const size_t k = blockIdx.x;
-    const int c = (int)(k % nchan);
-    // plan -> LDS
+    const int wpb = blockDim.x >> 6;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     {
         const int32_t *src = (const int32_t *)plan_g;
         int32_t *dst = (int32_t *)&pl;
-        for (int q = lane; q < (int)(sizeof(PwPlan) / 4); q += 64) dst[q] = src[q];
+        for (int q = threadIdx.x; q < (int)(sizeof(PwPlan) / 4); q += blockDim.x) dst[q] = src[q];
     }
-    const bool pow2 = (n & (n - 1)) == 0 && n >= 4;
-    double2 *cw = (double2 *)smem;                                  // n/2 (pow2) or unused
-    float *X = (float *)(smem + (size_t)(pow2 ? n / 2 : 1) * 16);     // n
-    const size_t xoff = (size_t)(pow2 ? n / 2 : 1) * 16 + (((size_t)n * 4 + 15) & ~(size_t)15);
-    double *scr = (double *)(smem + xoff);
-
-    const double x = amp[k];
-    const int stt = info[k];
-    const bool ok = stt >= 1 && stt <= 4;
-    const float w = w0[k];
-    const bool valid = (w != 0.0f);
-    const int sh = shift[c];
-    const float *p = D + k * (size_t)n;
-    // residual -> X (dispersed frame): X[j] = f32(f32(r[i]) * w), i = (j - sh) mod n
-    for (int i = lane; i < n; i += 64) {
-        float R = 0.0f;
-        if (ok) {
-            const double u = x * T64[i];
-            double e = u - (double)p[i];
-            if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
-            R = (float)e;
-        }
-        int j = i + sh;
-        if (j >= n) j -= n;
-        X[j] = R * w;
-    }
+    const DiagLayout lay = diag_layout(n, plan_g->nleaf, plan_g->nops);
+    double2 *tw = (double2 *)smem;
+    for (int q = threadIdx.x; q < lay.ntw; q += blockDim.x) tw[q] = tw_g[q];
     __syncthreads();
-    double mean = 0.0, var = 0.0;
-    float ptp = 1e20f;
-    double sd = 0.0;
-    if (valid) {
-        const float s32 = wave_pairwise<float>(pl, [&](int q) { return X[q]; }, (float *)scr, lane);
-        mean = (double)s32 / (double)n;
-        const double mu = mean;
-        const double ss = wave_pairwise<double>(
-            pl,
-            [&](int q) {
-                const double d = (double)X[q] - mu;
-                return d * d;
-            },
-            scr, lane);
-        var = ss / (double)n;
-        sd = sqrt(var);
-        // ptp (NaN-propagating like ndarray.max/min)
-        float mx = -INFINITY, mn = INFINITY;
-        int nan = 0;
-        for (int q = lane; q < n; q += 64) {
-            const float v = X[q];
-            if (isnan(v)) nan = 1;
-            mx = fmaxf(mx, v);
-            mn = fminf(mn, v);
+    unsigned char *wb = smem + (size_t)lay.ntw * 16 + (size_t)wave * lay.per_wave;
+    double2 *cw = (double2 *)(wb + lay.cw_off);
+    float *X = (float *)(wb + lay.x_off);
+    double *scr = (double *)(wb + lay.scr_off);
+    const bool pow2 = (n & (n - 1)) == 0 && n >= 4;
+    const size_t P = (size_t)nsub * nchan;
+
+    for (size_t k = (size_t)blockIdx.x * wpb + wave; k < P; k += (size_t)gridDim.x * wpb) {
+        const int c = (int)((unsigned)k % (unsigned)nchan);
+        const double x = amp[k];
+        const int stt = info[k];
+        const bool ok = stt >= 1 && stt <= 4;
+        const float w = w0[k];
+        const bool valid = (w != 0.0f);
+        const int sh = shift[c];
+        const float *p = D + k * (size_t)ldD;
+        wave_sync();   // previous profile's LDS reads are done
+        // residual -> X (dispersed frame): X[j] = f32(f32(r[i]) * w), j = (i + sh) mod n
+        for (int i = lane; i < n; i += 64) {
+            float R = 0.0f;
+            if (ok) {
+                const double u = x * T64[i];
+                double e = u - (double)p[i];
+                if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
+                R = (float)e;
+            }
+            int j = i + sh;
+            if (j >= n) j -= n;
+            X[j] = R * w;
+        }
+        wave_sync();
+        double mean = 0.0, sd = 0.0;
+        float ptp = 1e20f;
+        if (valid) {
+            const float s32 = wave_pairwise<float>(pl, [&](int q) { return X[q]; }, (float *)scr, lane);
+            mean = (double)s32 / (double)n;
+            const double mu = mean;
+            const double ss = wave_pairwise<double>(
+                pl,
+                [&](int q) {
+                    const double d = (double)X[q] - mu;
+                    return d * d;
+                },
+                scr, lane);
+            sd = sqrt(ss / (double)n);
+            float mx = -INFINITY, mn = INFINITY;
+            int nan = 0;
+            for (int q = lane; q < n; q += 64) {
+                const float v = X[q];
+                if (isnan(v)) nan = 1;
+                mx = fmaxf(mx, v);
+                mn = fminf(mn, v);
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                mx = fmaxf(mx, __shfl_xor(mx, off));
+                mn = fminf(mn, __shfl_xor(mn, off));
+                nan |= __shfl_xor(nan, off);
+            }
+            ptp = nan ? NAN : (mx - mn);
+        }
+        // fftmax: max_k |rfft(v)_k|, v = f64(X) - mean (valid) or f64(X) (invalid)
+        const double mu = valid ? mean : 0.0;
+        double best = 0.0;
+        int nanf = 0;
+        if (pow2) {
+            const int m = n / 2;
+            double2 *bufA = cw;
+            double2 *bufB = (double2 *)X;    // X is dead once the first stage has read it
+            int lg = 0;
+            while ((1 << lg) < m) ++lg;
+            // stage radices: as many 8s as possible, then one 4 or 2
+            int Ns = 1, done = 0;
+            double2 *src = nullptr, *dst = bufA;
+            auto first = [&](int q) {
+                return valid ? make_double2((double)X[2 * q] - mu, (double)X[2 * q + 1] - mu)
+                             : make_double2((double)X[2 * q], (double)X[2 * q + 1]);
+            };
+            auto from = [&](int q) { return src[q]; };
+            while (done < lg) {
+                const int rem = lg - done;
+                const int rl = rem >= 3 ? 3 : rem;
+                if (Ns == 1) {
+                    if (rl == 3) stockham_stage<8>(first, dst, m, Ns, tw, n, lane);
+                    else if (rl == 2) stockham_stage<4>(first, dst, m, Ns, tw, n, lane);
+                    else stockham_stage<2>(first, dst, m, Ns, tw, n, lane);
+                } else {
+                    if (rl == 3) stockham_stage<8>(from, dst, m, Ns, tw, n, lane);
+                    else if (rl == 2) stockham_stage<4>(from, dst, m, Ns, tw, n, lane);
+                    else stockham_stage<2>(from, dst, m, Ns, tw, n, lane);
+                }
+                wave_sync();
+                Ns <<= rl;
+                done += rl;
+                src = dst;
+                dst = (dst == bufA) ? bufB : bufA;
+            }
+            const double2 *Z = (lg == 0) ? nullptr : src;
+            // X_k = (Z_k + conj(Z_{m-k}))/2 - i/2 W^k (Z_k - conj(Z_{m-k})), W = exp(-2 pi i/n)
+            for (int kk = lane; kk <= m; kk += 64) {
+                const double2 zk = Z[kk == m ? 0 : kk];
+                const double2 zm = Z[kk == 0 ? 0 : m - kk];
+                const double er = 0.5 * (zk.x + zm.x), ei = 0.5 * (zk.y - zm.y);
+                const double orr = 0.5 * (zk.y + zm.y), oi = -0.5 * (zk.x - zm.x);
+                double wr = -1.0, wi = 0.0;
+                if (kk < m) {
+                    const double2 wv = tw[kk];
+                    wr = wv.x;
+                    wi = wv.y;
+                }
+                const double re = er + (orr * wr - oi * wi);
+                const double im = ei + (orr * wi + oi * wr);
+                const double a = hypot(re, im);
+                if (isnan(a)) nanf = 1;
+                best = fmax(best, a);
+            }
+        } else {
+            for (int kk = lane; kk <= n / 2; kk += 64) {
+                double sr = 0.0, si = 0.0;
+                int q = 0;
+                for (int j = 0; j < n; ++j) {
+                    const double v = valid ? (double)X[j] - mu : (double)X[j];
+                    const double2 wv = tw[q];
+                    sr += v * wv.x;
+                    si += v * wv.y;
+                    q += kk;
+                    if (q >= n) q -= n;
+                }
+                const double a = hypot(sr, si);
+                if (isnan(a)) nanf = 1;
+                best = fmax(best, a);
+            }
         }
         for (int off = 32; off > 0; off >>= 1) {
-            mx = fmaxf(mx, __shfl_xor(mx, off));
-            mn = fminf(mn, __shfl_xor(mn, off));
-            nan |= __shfl_xor(nan, off);
+            best = fmax(best, __shfl_xor(best, off));
+            nanf |= __shfl_xor(nanf, off);
         }
-        ptp = nan ? NAN : (mx - mn);
-    }
-    // fftmax: max_k |rfft(v)_k|, v = f64(X) - mean (valid) or f64(X) (invalid)
-    const double mu = valid ? mean : 0.0;
-    double best = 0.0;
-    int nanf = 0;
-    if (pow2) {
-        const int m = n / 2;
-        int lg = 0;
-        while ((1 << lg) < m) ++lg;
-        // z_j = v_{2j} + i v_{2j+1}, bit-reversed into cw
-        for (int j = lane; j < m; j += 64) {
-            const int rv = lg ? (int)(__builtin_bitreverse32((unsigned)j) >> (32 - lg)) : 0;
-            const double re = valid ? (double)X[2 * j] - mu : (double)X[2 * j];
-            const double im = valid ? (double)X[2 * j + 1] - mu : (double)X[2 * j + 1];
-            cw[rv] = make_double2(re, im);
+        if (lane == 0) {
+            std_o[k] = valid ? sd : 0.0;
+            mean_o[k] = valid ? mean : 0.0;
+            ptp_o[k] = valid ? ptp : 1e20f;
+            fft_o[k] = nanf ? NAN : best;
         }
-        __syncthreads();
-        for (int len = 2; len <= m; len <<= 1) {
-            const int half = len >> 1;
-            const int tstep = (n / len);  // twiddle exp(-2 pi i k/len) = tw[k * n/len]
-            for (int b = lane; b < m / 2; b += 64) {
-                const int grp = b / half, kk = b % half;
-                const int i0 = grp * len + kk, i1 = i0 + half;
-                const double2 wv = tw[kk * tstep];
-                const double2 a = cw[i0], bb = cw[i1];
-                const double vr = bb.x * wv.x - bb.y * wv.y;
-                const double vi = bb.x * wv.y + bb.y * wv.x;
-                cw[i0] = make_double2(a.x + vr, a.y + vi);
-                cw[i1] = make_double2(a.x - vr, a.y - vi);
-            }
-            __syncthreads();
-        }
-        // split: X_k = (Z_k + conj(Z_{m-k}))/2 - i/2 * W^k (Z_k - conj(Z_{m-k})), W = exp(-2 pi i/n)
-        for (int kk = lane; kk <= m; kk += 64) {
-            const double2 zk = cw[kk == m ? 0 : kk];
-            const double2 zm = cw[(m - kk) % m];
-            const double er = 0.5 * (zk.x + zm.x), ei = 0.5 * (zk.y - zm.y);
-            const double orr = 0.5 * (zk.y + zm.y), oi = -0.5 * (zk.x - zm.x);
-            const double2 wv = tw[kk == m ? 0 : kk];
-            double wr = wv.x, wi = wv.y;
-            if (kk == m) { wr = -1.0; wi = 0.0; }
-            const double re = er + (orr * wr - oi * wi);
-            const double im = ei + (orr * wi + oi * wr);
-            const double a = hypot(re, im);
-            if (isnan(a)) nanf = 1;
-            best = fmax(best, a);
-        }
-    } else {
-        for (int kk = lane; kk <= n / 2; kk += 64) {
-            double sr = 0.0, si = 0.0;
-            long q = 0;
-            for (int j = 0; j < n; ++j) {
-                const double v = valid ? (double)X[j] - mu : (double)X[j];
-                const double2 wv = tw[q];
-                sr += v * wv.x;
-                si += v * wv.y;
-                q += kk;
-                if (q >= n) q -= n;
-            }
-            const double a = hypot(sr, si);
-            if (isnan(a)) nanf = 1;
-            best = fmax(best, a);
-        }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        best = fmax(best, __shfl_xor(best, off));
-        nanf |= __shfl_xor(nanf, off);
-    }
-    if (lane == 0) {
-        std_o[k] = valid ? sd : 0.0;
-        mean_o[k] = valid ? mean : 0.0;
-        ptp_o[k] = valid ? ptp : 1e20f;
-        fft_o[k] = nanf ? NAN : best;
     }
 }
 
-// residual cube on request (ic_get_residual): R (dispersed frame, unweighted); grid-stride
+// ---------------------------------------------------------------------------
+// k_diag_p2<N>: the same diagnostics for power-of-two nbin = N (64..2048).
+// numpy's pairwise sum for N = 2^k is a balanced tree over leaves of
+// min(N,128) samples, each leaf 8 strided chains of min(N,128)/8 samples:
+// chain c = (leaf c/8, accumulator c%8) lives in lane c%64, slot c/64, and the
+// tree is reproduced exactly by xor-shuffles (IEEE add is commutative) and a
+// balanced in-register add of the slots.  X sits in LDS at idx + 8*(idx>>7)
+// so the chain reads are bank-conflict free.  The rFFT is an in-place
+// mixed-radix Stockham FFT of N/2 complex points (all of a stage's inputs are
+// in registers before it writes), twiddle powers by recurrence.
+template <int N>
+struct P2 {
+    static constexpr int M = N / 2;
+    static constexpr int LEAF = N < 128 ? N : 128;
+    static constexpr int NL = N / LEAF;
+    static constexpr int CL = LEAF / 8;
+    static constexpr int CH = 8 * NL;
+    static constexpr int CPL = CH > 64 ? CH / 64 : 1;
+    static constexpr int ACT = CH < 64 ? CH : 64;
+    static constexpr int XPAD = N + 8 * NL;
+    static constexpr int XBYTES = ((XPAD * 4 + 15) / 16) * 16;
+    static constexpr int CBYTES = M * 16;
+    static constexpr int WAVE_BYTES = XBYTES > CBYTES ? XBYTES : CBYTES;
+    static constexpr int LG = __builtin_ctz(M);
+};
+
+__device__ __forceinline__ int xaddr(int idx) { return idx + 8 * (idx >> 7); }
+
+template <typename T>
+__device__ __forceinline__ T shfl_xor_t(T v, int m) { return __shfl_xor(v, m); }
+
+// xor-butterfly combine over lanes [0, act): levels 1,2,4,... < act
+template <typename T, int ACT>
+__device__ __forceinline__ T tree_lanes(T v)
+{
+#pragma unroll
+    for (int m = 1; m < ACT; m <<= 1) v = v + shfl_xor_t(v, m);
+    return v;
+}
+
+template <typename T, int CPL>
+__device__ __forceinline__ T tree_slots(const T (&v)[CPL])
+{
+    if (CPL == 1) return v[0];
+    if (CPL == 2) return v[0] + v[1];
+    if (CPL == 4) return (v[0] + v[1]) + (v[2] + v[3]);
+    // CPL == 8
+    return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+}
+
+template <int R, int BPL, int M, int N>
+__device__ __forceinline__ void p2_stage(double2 *C, const float *X, bool first, bool valid, double mu,
+                                         int Ns, const double2 *tw, int lane)
+{
+    constexpr int NB = M / R;
+    double2 v[BPL][R];
+    int kk[BPL];
+#pragma unroll
+    for (int u = 0; u < BPL; ++u) {
+        const int b = lane + 64 * u;
+        kk[u] = b & (Ns - 1);
+        if (b < NB) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int q = b + r * NB;
+                if (first) {
+                    const float2 xv = *(const float2 *)(X + xaddr(2 * q));
+                    v[u][r] = valid ? make_double2((double)xv.x - mu, (double)xv.y - mu)
+                                    : make_double2((double)xv.x, (double)xv.y);
+                } else {
+                    v[u][r] = C[q];
+                }
+            }
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < BPL; ++u) {
+        const int b = lane + 64 * u;
+        if (b < NB) {
+            const int k = kk[u];
+            if (Ns > 1) {
+                const double2 w1 = tw[k * (N / (R * Ns))];
+                double2 wp = w1;
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    v[u][r] = cmul(v[u][r], wp);
+                    if (r + 1 < R) wp = cmul(wp, w1);
+                }
+            }
+            dft_small<R>(v[u]);
+            const int idx = (b - k) * R + k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) C[idx + r * Ns] = v[u][r];
+        }
+    }
+    wave_sync();
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_diag_p2(
+    const float *__restrict__ D, const double *__restrict__ T64g, const double *__restrict__ amp,
+    const int32_t *__restrict__ info, const float *__restrict__ w0, const int32_t *__restrict__ shift,
+    const double2 *__restrict__ tw_g, int nsub, int nchan, int ldD, int pr_on, double pr_factor,
+    int pr_start, int pr_end, double *__restrict__ std_o, double *__restrict__ mean_o,
+    float *__restrict__ ptp_o, double *__restrict__ fft_o)
+{
+    using C = P2<N>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double2 *tw = (double2 *)smem;                     // N/2
+    double *T = (double *)(smem + (size_t)C::M * 16);  // N
+    const int wpb = blockDim.x >> 6;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    for (int q = threadIdx.x; q < C::M; q += blockDim.x) tw[q] = tw_g[q];
+    for (int q = threadIdx.x; q < N; q += blockDim.x) T[q] = T64g[q];
+    __syncthreads();
+    unsigned char *wb = smem + (size_t)C::M * 16 + (size_t)N * 8 + (size_t)wave * C::WAVE_BYTES;
+    float *X = (float *)wb;
+    double2 *Cb = (double2 *)wb;   // aliases X after the first FFT stage has read it
+    const unsigned P = (unsigned)nsub * (unsigned)nchan;
+    const unsigned stride = gridDim.x * wpb;
+
+    for (unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + wave); k < P; k += stride) {
+        const unsigned c = k % (unsigned)nchan;
+        const double x = amp[k];
+        const int stt = info[k];
+        const bool ok = stt >= 1 && stt <= 4;
+        const float w = w0[k];
+        const bool valid = (w != 0.0f);
+        const int sh = shift[c];
+        const float *p = D + (size_t)k * ldD;
+        wave_sync();
+        // residual -> X (dispersed frame, padded addresses)
+#pragma unroll 4
+        for (int i = lane; i < N; i += 64) {
+            float R = 0.0f;
+            if (ok) {
+                const double u = x * T[i];
+                double e = u - (double)p[i];
+                if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
+                R = (float)e;
+            }
+            const int j = (i + sh) & (N - 1);
+            X[xaddr(j)] = R * w;
+        }
+        wave_sync();
+        double mean = 0.0, sd = 0.0, fftv = 0.0;
+        float ptp = 1e20f;
+        if (valid) {
+            // chain values -> registers
+            float v[C::CPL][C::CL];
+            const bool act = lane < C::ACT;
+#pragma unroll
+            for (int sl = 0; sl < C::CPL; ++sl) {
+                const int ch = lane + 64 * sl;
+                const int base = (ch >> 3) * C::LEAF + (ch & 7);
+#pragma unroll
+                for (int q = 0; q < C::CL; ++q) v[sl][q] = act ? X[xaddr(base + 8 * q)] : 0.0f;
+            }
+            // mean: f32 pairwise sum
+            float fs[C::CPL];
+#pragma unroll
+            for (int sl = 0; sl < C::CPL; ++sl) {
+                float r = v[sl][0];
+#pragma unroll
+                for (int q = 1; q < C::CL; ++q) r = r + v[sl][q];
+                fs[sl] = tree_lanes<float, C::ACT>(r);
+            }
+            const float s32 = 0.0f + __shfl(tree_slots<float, C::CPL>(fs), 0);
+            mean = (double)s32 / (double)N;
+            // var: f64 pairwise sum of (f64(X) - mean)^2
+            double ds[C::CPL];
+#pragma unroll
+            for (int sl = 0; sl < C::CPL; ++sl) {
+                double d0 = (double)v[sl][0] - mean;
+                double r = d0 * d0;
+#pragma unroll
+                for (int q = 1; q < C::CL; ++q) {
+                    const double d = (double)v[sl][q] - mean;
+                    const double sq = d * d;
+                    r = r + sq;
+                }
+                ds[sl] = tree_lanes<double, C::ACT>(r);
+            }
+            const double ss = 0.0 + __shfl(tree_slots<double, C::CPL>(ds), 0);
+            sd = sqrt(ss / (double)N);
+            // ptp (NaN-propagating)
+            float mx = -INFINITY, mn = INFINITY;
+            int nan = 0;
+            if (act) {
+#pragma unroll
+                for (int sl = 0; sl < C::CPL; ++sl)
+#pragma unroll
+                    for (int q = 0; q < C::CL; ++q) {
+                        const float t = v[sl][q];
+                        nan |= isnan(t);
+                        mx = fmaxf(mx, t);
+                        mn = fminf(mn, t);
+                    }
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                mx = fmaxf(mx, __shfl_xor(mx, off));
+                mn = fminf(mn, __shfl_xor(mn, off));
+                nan |= __shfl_xor(nan, off);
+            }
+            ptp = nan ? NAN : (mx - mn);
+            // rFFT of f64(X) - mean: N/2-point complex Stockham, in place
+            {
+                int done = 0, Ns = 1;
+                bool first = true;
+                while (done < C::LG) {
+                    const int rem = C::LG - done;
+                    if (rem >= 3) {
+                        p2_stage<8, (C::M / 8 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw, lane);
+                        Ns <<= 3; done += 3;
+                    } else if (rem == 2) {
+                        p2_stage<4, (C::M / 4 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw, lane);
+                        Ns <<= 2; done += 2;
+                    } else {
+                        p2_stage<2, (C::M / 2 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw, lane);
+                        Ns <<= 1; done += 1;
+                    }
+                    first = false;
+                }
+            }
+            double best2 = 0.0;
+            int nanf = 0;
+            for (int kk = lane; kk <= C::M; kk += 64) {
+                const double2 zk = Cb[kk == C::M ? 0 : kk];
+                const double2 zm = Cb[kk == 0 ? 0 : C::M - kk];
+                const double er = 0.5 * (zk.x + zm.x), ei = 0.5 * (zk.y - zm.y);
+                const double orr = 0.5 * (zk.y + zm.y), oi = -0.5 * (zk.x - zm.x);
+                double wr = -1.0, wi = 0.0;
+                if (kk < C::M) {
+                    const double2 wv = tw[kk];
+                    wr = wv.x;
+                    wi = wv.y;
+                }
+                const double re = er + (orr * wr - oi * wi);
+                const double im = ei + (orr * wi + oi * wr);
+                const double a2 = re * re + im * im;
+                nanf |= isnan(a2);
+                best2 = fmax(best2, a2);
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                best2 = fmax(best2, __shfl_xor(best2, off));
+                nanf |= __shfl_xor(nanf, off);
+            }
+            fftv = nanf ? NAN : sqrt(best2);
+        } else {
+            // invalid: rfft of f64(X) = +-0 -> 0, unless R was non-finite (X NaN)
+            int nanx = 0;
+            for (int i = lane; i < N; i += 64) nanx |= isnan(X[xaddr(i)]);
+            for (int off = 32; off > 0; off >>= 1) nanx |= __shfl_xor(nanx, off);
+            fftv = nanx ? NAN : 0.0;
+        }
+        if (lane == 0) {
+            std_o[k] = valid ? sd : 0.0;
+            mean_o[k] = valid ? mean : 0.0;
+            ptp_o[k] = valid ? ptp : 1e20f;
+            fft_o[k] = fftv;
+        }
+    }
+}
+
+// residual cube on request (ic_get_residual): R (dispersed frame, unweighted)
 __global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, const double *__restrict__ T64,
                                                   const double *__restrict__ amp, const int32_t *__restrict__ info,
-                                                  const int32_t *__restrict__ shift, size_t N, int nchan, int nbin,
-                                                  int pr_on, double pr_factor, int pr_start, int pr_end,
+                                                  const int32_t *__restrict__ shift, size_t P, int nchan, int nbin,
+                                                  int ldD, int pr_on, double pr_factor, int pr_start, int pr_end,
                                                   float *__restrict__ R)
 {
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += (size_t)gridDim.x * blockDim.x) {
-        const size_t k = e / nbin;
-        const int i = (int)(e - k * nbin);
-        const int c = (int)(k % nchan);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (size_t k = (size_t)blockIdx.x * 4 + wave; k < P; k += (size_t)gridDim.x * 4) {
+        const int sh = shift[k % nchan];
         const int st = info[k];
-        float v = 0.0f;
-        if (st >= 1 && st <= 4) {
-            const double u = amp[k] * T64[i];
-            double ee = u - (double)D[e];
-            if (pr_on && i >= pr_start && i < pr_end) ee = ee * pr_factor;
-            v = (float)ee;
+        const bool ok = st >= 1 && st <= 4;
+        const double a = amp[k];
+        for (int i = lane; i < nbin; i += 64) {
+            float v = 0.0f;
+            if (ok) {
+                const double u = a * T64[i];
+                double e = u - (double)D[k * ldD + i];
+                if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
+                v = (float)e;
+            }
+            int j = i + sh;
+            if (j >= nbin) j -= nbin;
+            R[k * nbin + j] = v;
         }
-        int j = i + shift[c];
-        if (j >= nbin) j -= nbin;
-        R[k * nbin + j] = v;
     }
 }
 
@@ -1081,11 +1702,11 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
 }
 
 hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
-                          int nsub, int nchan, int nbin, float *D)
+                          int nsub, int nchan, int nbin, int ldD, float *D)
 {
-    const size_t N = (size_t)nsub * nchan * nbin;
-    const unsigned grid = (unsigned)(cdiv(N, 256) < 65536u * 8 ? cdiv(N, 256) : 65536u * 8);
-    hipLaunchKernelGGL(k_fitcube, dim3(grid), dim3(256), 0, st, raw, shift, base, nsub, nchan, nbin, D);
+    const size_t P = (size_t)nsub * nchan;
+    const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
+    hipLaunchKernelGGL(k_fitcube, dim3(grid), dim3(256), 0, st, raw, shift, base, nsub, nchan, nbin, ldD, D);
     return hipGetLastError();
 }
 
@@ -1105,35 +1726,59 @@ hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int 
     return hipGetLastError();
 }
 
-hipError_t launch_fit(hipStream_t st, const float *D, const double *T64, long P, int nbin, double *amp,
-                      int32_t *info)
+hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P)
 {
-    hipLaunchKernelGGL(k_fit, dim3(cdiv(P, 64)), dim3(64), 0, st, D, T64, P, nbin, amp, info);
+    hipLaunchKernelGGL(k_fit_init, dim3(cdiv(P, 256)), dim3(256), 0, st, S, P);
     return hipGetLastError();
 }
 
-size_t diag_lds_bytes(int nbin, int nleaf, int nops)
+hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
+                           const FitStateArrays &S)
 {
-    const bool pow2 = (nbin & (nbin - 1)) == 0 && nbin >= 4;
-    size_t b = (size_t)(pow2 ? nbin / 2 : 1) * 16;
-    b += ((size_t)nbin * 4 + 15) & ~(size_t)15;
-    b += (size_t)(nleaf * 9 + nops + 8) * 8;
-    return b;
+    hipLaunchKernelGGL(k_fit_pass, dim3(cdiv(P, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, double *amp, int32_t *info,
+                            int32_t *active)
+{
+    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(P, 256)), dim3(256), 0, st, S, P, amp, info, active);
+    return hipGetLastError();
 }
 
 hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const double *amp,
                        const int32_t *info, const float *w0, const int32_t *shift, const double2 *tw,
-                       const PwPlan *plan, int nsub, int nchan, int nbin, int pr_on, double pr_factor,
+                       const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
                        int pr_start, int pr_end, double *std_o, double *mean_o, float *ptp_o,
                        double *fft_o)
 {
-    (void)nsub;
+#define IC_P2(NN)                                                                                  \
+    if (nbin == NN) {                                                                              \
+        const size_t fixed = (size_t)(NN / 2) * 16 + (size_t)NN * 8;                               \
+        int wpb = 4;                                                                               \
+        while (wpb > 1 && fixed + wpb * (size_t)P2<NN>::WAVE_BYTES > 150 * 1024) --wpb;            \
+        const size_t shm = fixed + wpb * (size_t)P2<NN>::WAVE_BYTES;                               \
+        const size_t P = (size_t)nsub * nchan;                                                     \
+        const unsigned grid = (unsigned)std::min<size_t>((P + wpb - 1) / wpb, 4096);               \
+        hipLaunchKernelGGL(k_diag_p2<NN>, dim3(grid), dim3(64 * wpb), shm, st, D, T64, amp, info, w0, \
+                           shift, tw, nsub, nchan, ldD, pr_on, pr_factor, pr_start, pr_end, std_o,  \
+                           mean_o, ptp_o, fft_o);                                                  \
+        return hipGetLastError();                                                                  \
+    }
+    IC_P2(64) IC_P2(128) IC_P2(256) IC_P2(512) IC_P2(1024) IC_P2(2048)
+#undef IC_P2
     // nleaf/nops upper bound from nbin: leaves >= 64 samples except tiny n
     const int nleaf_ub = nbin <= 128 ? 1 : (nbin / 64 + 1);
-    const size_t shm = diag_lds_bytes(nbin, nleaf_ub, nleaf_ub);
+    const DiagLayout lay = diag_layout(nbin, nleaf_ub, nleaf_ub);
+    const size_t fixed = (size_t)lay.ntw * 16;
+    int wpb = 4;
+    while (wpb > 1 && fixed + wpb * lay.per_wave > 150 * 1024) --wpb;
+    const size_t shm = fixed + wpb * lay.per_wave;
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
     const size_t P = (size_t)nsub * nchan;
-    hipLaunchKernelGGL(k_diag, dim3((unsigned)P), dim3(64), shm, st, D, T64, amp, info, w0, shift, tw, plan,
-                       nsub, nchan, nbin, pr_on, pr_factor, pr_start, pr_end, std_o, mean_o, ptp_o, fft_o);
+    const unsigned grid = (unsigned)std::min<size_t>((P + wpb - 1) / wpb, 8192);
+    hipLaunchKernelGGL(k_diag, dim3(grid), dim3(64 * wpb), shm, st, D, T64, amp, info, w0, shift, tw, plan,
+                       nsub, nchan, nbin, ldD, pr_on, pr_factor, pr_start, pr_end, std_o, mean_o, ptp_o, fft_o);
     return hipGetLastError();
 }
 
@@ -1168,12 +1813,12 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
 }
 
 hipError_t launch_residual(hipStream_t st, const float *D, const double *T64, const double *amp,
-                           const int32_t *info, const int32_t *shift, int nsub, int nchan, int nbin,
+                           const int32_t *info, const int32_t *shift, int nsub, int nchan, int nbin, int ldD,
                            int pr_on, double pr_factor, int pr_start, int pr_end, float *R)
 {
-    const size_t N = (size_t)nsub * nchan * nbin;
-    const unsigned grid = (unsigned)(cdiv(N, 256) < 65536u * 8 ? cdiv(N, 256) : 65536u * 8);
-    hipLaunchKernelGGL(k_residual, dim3(grid), dim3(256), 0, st, D, T64, amp, info, shift, N, nchan, nbin,
+    const size_t P = (size_t)nsub * nchan;
+    const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
+    hipLaunchKernelGGL(k_residual, dim3(grid), dim3(256), 0, st, D, T64, amp, info, shift, P, nchan, nbin, ldD,
                        pr_on, pr_factor, pr_start, pr_end, R);
     return hipGetLastError();
 }

@@ -40,9 +40,9 @@ int fail(int code, const char *fmt, ...)
                         __LINE__);                                                                \
     } while (0)
 
-const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",   "k_base",        "k_fitcube",
-                                     "k_fscrunch",      "k_tscrunch", "k_fit",         "k_diag",
-                                     "k_linestats",     "k_combine",  "k_residual"};
+const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",   "k_base",      "k_fitcube",
+                                     "k_fscrunch",      "k_tscrunch", "k_fit_pass",  "k_fit_state",
+                                     "k_diag",          "k_linestats", "k_combine",  "k_residual"};
 
 struct Timed {
     int kid;
@@ -53,7 +53,8 @@ struct Session {
     ic_params p{};
     int device = 0;
     hipStream_t stream = nullptr;
-    size_t P = 0, N = 0;
+    size_t P = 0, N = 0, Ppad = 0;
+    int ldD = 0;                // fit-cube row stride (bins, padded to kFitTile)
     int nsb = 0, width = 0;
     bool uploaded = false, ran = false;
     int last_iter = 0;
@@ -66,6 +67,10 @@ struct Session {
            *mean = nullptr, *fft = nullptr, *test = nullptr, *lstat = nullptr;
     double2 *tw = nullptr;
     PwPlan *plan = nullptr;
+    FitStateArrays fs{};
+    void *fs_block = nullptr;   // one allocation backing fs
+    int fit_rounds = 0;
+    ic_run_stats stats{};
     // timing
     bool timing = false;
     std::vector<Timed> events;
@@ -155,7 +160,7 @@ void free_all(Session *s)
     void *bufs[] = {s->raw,  s->D,     s->w0,   s->W,   s->base, s->base0, s->F,   s->wf,
                     s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
-                    s->lstat, s->tw,   s->plan};
+                    s->lstat, s->tw,   s->plan, s->fs_block};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : s->events) {
@@ -188,7 +193,7 @@ int prepare(Session *s)
                                 nullptr));
     LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win));
     LAUNCH(s, K_BASE, launch_base(s->stream, s->raw, s->shift, s->win, nsub, nchan, nbin, s->width, s->base0));
-    LAUNCH(s, K_FITCUBE, launch_fitcube(s->stream, s->raw, s->shift, s->base0, nsub, nchan, nbin, s->D));
+    LAUNCH(s, K_FITCUBE, launch_fitcube(s->stream, s->raw, s->shift, s->base0, nsub, nchan, nbin, s->ldD, s->D));
     return 0;
 }
 
@@ -207,6 +212,31 @@ int iteration_template(Session *s)
                                 s->wpart));
     LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->part, s->wpart, nsub, s->nsb, nbin, s->F, s->wf));
     LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64));
+    return 0;
+}
+
+// exact scipy leastsq for every profile (ic.py:266-272): sweep/state rounds
+int run_fit(Session *s)
+{
+    const long P = (long)s->P;
+    const int nbin = s->p.nbin;
+    CK(launch_fit_init(s->stream, s->fs, P));
+    int32_t active = 0;
+    int round = 0;
+    int64_t swept = P;   // round 0 sweeps every profile
+    for (; round < 1000; ++round) {
+        LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, s->fs));
+        CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t), s->stream));
+        LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, s->amp, s->info, s->counters));
+        CK(hipMemcpyAsync(&active, s->counters, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+        CK(hipStreamSynchronize(s->stream));
+        if (active == 0) break;
+        swept += active;
+    }
+    if (active != 0) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", round);
+    s->fit_rounds = round + 1;
+    s->stats.fit_rounds += round + 1;
+    s->stats.fit_profile_sweeps += swept;
     return 0;
 }
 
@@ -252,6 +282,8 @@ int ic_session_create(const ic_params *params, int device, void **out)
     s->P = (size_t)p.nsub * p.nchan;
     s->N = s->P * (size_t)p.nbin;
     s->nsb = (p.nchan + kSuperBlock - 1) / kSuperBlock;
+    s->ldD = ((p.nbin + kFitTile - 1) / kFitTile) * kFitTile;
+    s->Ppad = ((s->P + 63) / 64) * 64;
     s->width = (int)(p.baseline_duty * (double)p.nbin);
     if (s->width < 1) s->width = 1;
     int rc = 0;
@@ -273,7 +305,9 @@ int ic_session_create(const ic_params *params, int device, void **out)
     const size_t P = s->P, N = s->N;
     const int nsub = p.nsub, nchan = p.nchan, nbin = p.nbin;
     AL(s->raw, N);
-    AL(s->D, N);
+    AL(s->D, s->Ppad * (size_t)s->ldD);
+    if (hipMemset(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD) != hipSuccess)
+        return bail(fail(IC_EHIP, "hipMemset(D) failed"));
     AL(s->w0, P);
     AL(s->W, P);
     AL(s->base, P);
@@ -300,6 +334,20 @@ int ic_session_create(const ic_params *params, int device, void **out)
     AL(s->tw, (size_t)nbin);
     AL(s->plan, 1);
 #undef AL
+    {
+        // fit state: 23 double arrays + 5 int arrays, each padded to 256 B
+        const size_t dstride = ((P * 8 + 255) / 256) * 256, istride = ((P * 4 + 255) / 256) * 256;
+        if (hipMalloc(&s->fs_block, 23 * dstride + 5 * istride) != hipSuccess)
+            return bail(fail(IC_ENOMEM, "hipMalloc(fit state) failed"));
+        char *b = (char *)s->fs_block;
+        double **dp[] = {&s->fs.x,     &s->fs.fnorm, &s->fs.par,   &s->fs.delta,   &s->fs.diag, &s->fs.xnorm,
+                         &s->fs.acnorm, &s->fs.J0,   &s->fs.f0,    &s->fs.aj,      &s->fs.r,    &s->fs.Jn0,
+                         &s->fs.qtf,   &s->fs.gnorm, &s->fs.x2,    &s->fs.pnorm,   &s->fs.wa1,  &s->fs.xa,
+                         &s->fs.o_fnorm, &s->fs.o_acnorm, &s->fs.o_f0, &s->fs.o_J0, &s->fs.o_sum};
+        for (auto *q : dp) { *q = (double *)b; b += dstride; }
+        int32_t **ip[] = {&s->fs.iter, &s->fs.nfev, &s->fs.mode, &s->fs.slow, &s->fs.o_exact};
+        for (auto *q : ip) { *q = (int32_t *)b; b += istride; }
+    }
     // twiddles exp(-2 pi i q / n) and the pairwise plan
     std::vector<double2> tw(nbin);
     for (int q = 0; q < nbin; ++q) {
@@ -392,6 +440,7 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
     int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > nbin ? nbin : p.pr_start);
     int pr_end = p.pr_end < 0 ? 0 : (p.pr_end > nbin ? nbin : p.pr_end);
     // fit cube (ic.py:96-100) + initial weights/history; a session can be re-run
+    s->stats = ic_run_stats{};
     if (int rc = prepare(s)) return rc;
     LineStatsArgs la;
     la.nsub = nsub;
@@ -411,10 +460,10 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
         x += 1;
         ++n_iter;
         if (int rc = iteration_template(s)) return rc;
-        LAUNCH(s, K_FIT, launch_fit(s->stream, s->D, s->T64, (long)s->P, nbin, s->amp, s->info));
+        if (int rc = run_fit(s)) return rc;
         LAUNCH(s, K_DIAG,
                launch_diag(s->stream, s->D, s->T64, s->amp, s->info, s->w0, s->shift, s->tw, s->plan, nsub,
-                           nchan, nbin, p.pr_on, p.pr_factor, pr_start, pr_end, s->std_, s->mean, s->ptp,
+                           nchan, nbin, s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, s->std_, s->mean, s->ptp,
                            s->fft));
         LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, la));
         CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t) * (p.max_iter + 4), s->stream));
@@ -444,6 +493,7 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
     if (int rc = collect_timing(s)) return rc;
     if (loops_out) *loops_out = loops;
     if (n_iter_out) *n_iter_out = n_iter;
+    s->stats.iterations = n_iter;
     if (converged_out) *converged_out = converged;
     s->ran = n_iter > 0;
     return IC_OK;
@@ -462,11 +512,19 @@ int ic_get_residual(void *session, float *out)
     float *R = nullptr;
     CK(hipMalloc((void **)&R, sizeof(float) * s->N));
     hipError_t e = launch_residual(s->stream, s->D, s->T64, s->amp, s->info, s->shift, p.nsub, p.nchan, p.nbin,
-                                   p.pr_on, p.pr_factor, pr_start, pr_end, R);
+                                   s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, R);
     if (e == hipSuccess) e = hipMemcpyAsync(out, R, sizeof(float) * s->N, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(R);
     if (e != hipSuccess) return fail(IC_EHIP, "residual: %s", hipGetErrorString(e));
+    return IC_OK;
+}
+
+int ic_get_run_stats(void *session, ic_run_stats *out)
+{
+    Session *s = (Session *)session;
+    if (!s || !out) return fail(IC_EINVAL, "null argument");
+    *out = s->stats;
     return IC_OK;
 }
 

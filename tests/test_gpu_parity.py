@@ -97,6 +97,10 @@ CASES = [
     (3, 20, 8, 14, 0.3, {}),                   # tiny profiles
     (9, 70, 128, 15, 0.3, {"chanthresh": 3.0, "subintthresh": 2.5}),
     (8, 64, 256, 16, 0.2, {"pulse_region": [0.25, 40, 90]}),
+    (6, 50, 512, 17, 0.2, {}),
+    (5, 70, 1024, 18, 0.2, {}),                # the C2 profile length
+    (4, 30, 2048, 19, 0.3, {}),
+    (4, 520, 32, 20, 0.2, {}),                 # three super-blocks, short profiles
 ]
 
 
