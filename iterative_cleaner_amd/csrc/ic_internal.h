@@ -73,9 +73,9 @@ hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int 
                            double *T64);
 hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           const FitStateArrays &S);
-hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, double *amp, int32_t *info,
-                            int32_t *active);
+                           const int32_t *list, int nlist, const FitStateArrays &S);
+hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list, int nlist,
+                            double *amp, int32_t *info, int32_t *next_list, int32_t *next_n);
 hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const double *amp,
                        const int32_t *info, const float *w0, const int32_t *shift, const double2 *tw,
                        const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,

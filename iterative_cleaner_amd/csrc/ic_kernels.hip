@@ -563,15 +563,15 @@ __device__ __forceinline__ bool x_in_fast_range(double x)
 
 // Load a 64-profile x FIT_TB-bin tile of D into LDS, transposed to tile[bin][profile].
 // D is padded to [roundup(P,64)][ldD], ldD = roundup(nbin, FIT_TB): no guards.
-__device__ __forceinline__ void load_tile(float (*tile)[65], const float *__restrict__ D, long k0, int ldD,
-                                          int b0, int lane)
+// rows[m] = D + row(8m + lane/8) * ldD + (lane%8)*4: 8 row pointers per lane
+// (profiles of a compacted active list).
+__device__ __forceinline__ void load_tile(float (*tile)[65], const float *const (&rows)[8], int b0, int lane)
 {
     const int c4 = (lane & 7) * 4;
     const int r0 = lane >> 3;
-    const float *base = D + (size_t)(k0 + r0) * ldD + b0 + c4;
     float4 v[8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) v[m] = *(const float4 *)(base + (size_t)m * 8 * ldD);
+    for (int m = 0; m < 8; ++m) v[m] = *(const float4 *)(rows[m] + b0);
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
         const int r = m * 8 + r0;
@@ -593,10 +593,58 @@ struct PassOut {
     bool bad;                    // fast path left its verified range
 };
 
+// Per-sample work of one sweep.  Zero-padded samples (p = 0, T = 0) are exact
+// no-ops: f = J = 0 adds nothing to either enorm, and Jn*f = 0 to the dot.
+template <bool EXACT, bool FIRST>
+__device__ __forceinline__ void fit_sample(double t, double pv, const PassIn &in, bool anyA, bool anyB,
+                                           double agiant, FastAcc &fF, FastAcc &fJ, Enorm &eF, Enorm &eJ,
+                                           double &fa0, double &Ja0, double &sum)
+{
+    if (anyA && in.A) {
+        const double u = in.xa * t;
+        const double f = u - pv;
+        const double uh = in.xha * t;
+        const double wa = uh - pv;
+        const double d = wa - f;
+        double J;
+        if (EXACT) {
+            en_add(eF, f, agiant);
+            J = d / in.ha;
+            en_add(eJ, J, agiant);
+        } else {
+            fa_add(fF, f);
+            J = mdiv(d, in.ha, in.yha);
+            fa_add(fJ, J);
+        }
+        if (FIRST) {
+            fa0 = f;
+            Ja0 = J;
+        }
+    }
+    if (anyB && in.B) {
+        const double u = in.xb * t;
+        const double f = u - pv;
+        const double uh = in.xhb * t;
+        const double wa = uh - pv;
+        const double d = wa - f;
+        double J, Jn;
+        if (EXACT) {
+            J = d / in.hb;
+            Jn = J / in.ajb;
+        } else {
+            J = mdiv(d, in.hb, in.yhb);
+            Jn = mdiv(J, in.ajb, in.yaj);
+        }
+        if (FIRST) Jn = Jn + 1.0;
+        const double pr = Jn * f;
+        sum = sum + pr;
+    }
+}
+
 template <bool EXACT>
-__device__ void fit_sweep(float (*tile)[65], const float *__restrict__ D, const double *__restrict__ T64,
-                          long k0, int ldD, int nbin, int lane, const PassIn &in, bool anyA, bool anyB,
-                          double agiant, PassOut &out)
+__device__ void fit_sweep(float (*tile)[65], const float *const (&rows)[8], const double *__restrict__ T64,
+                          int ldD, int lane, const PassIn &in, bool anyA, bool anyB, double agiant,
+                          PassOut &out)
 {
     FastAcc fF, fJ;
     fa_zero(fF);
@@ -605,57 +653,33 @@ __device__ void fit_sweep(float (*tile)[65], const float *__restrict__ D, const 
     en_zero(eF);
     en_zero(eJ);
     double fa0 = 0.0, Ja0 = 0.0, sum = 0.0;
-    for (int b0 = 0; b0 < nbin; b0 += FIT_TB) {
+    for (int b0 = 0; b0 < ldD; b0 += FIT_TB) {
         __syncthreads();
-        load_tile(tile, D, k0, ldD, b0, lane);
+        load_tile(tile, rows, b0, lane);
         __syncthreads();
-        const int tb = min(FIT_TB, nbin - b0);
-#pragma unroll 2
-        for (int ii = 0; ii < FIT_TB; ++ii) {
-            if (ii < tb) {
-                const int i = b0 + ii;
-                const double t = T64[i];
+        if (EXACT) {
+            for (int ii = 0; ii < FIT_TB; ++ii) {
+                const double t = T64[b0 + ii];
                 const double pv = (double)tile[ii][lane];
-                if (anyA && in.A) {
-                    const double u = in.xa * t;
-                    const double f = u - pv;
-                    const double uh = in.xha * t;
-                    const double wa = uh - pv;
-                    const double d = wa - f;
-                    double J;
-                    if (EXACT) {
-                        en_add(eF, f, agiant);
-                        J = d / in.ha;
-                        en_add(eJ, J, agiant);
-                    } else {
-                        fa_add(fF, f);
-                        J = mdiv(d, in.ha, in.yha);
-                        fa_add(fJ, J);
-                    }
-                    if (i == 0) {
-                        fa0 = f;
-                        Ja0 = J;
-                    }
-                }
-                if (anyB && in.B) {
-                    const double u = in.xb * t;
-                    const double f = u - pv;
-                    const double uh = in.xhb * t;
-                    const double wa = uh - pv;
-                    const double d = wa - f;
-                    double J, Jn;
-                    if (EXACT) {
-                        J = d / in.hb;
-                        Jn = J / in.ajb;
-                    } else {
-                        J = mdiv(d, in.hb, in.yhb);
-                        Jn = mdiv(J, in.ajb, in.yaj);
-                    }
-                    if (i == 0) Jn = Jn + 1.0;
-                    const double pr = Jn * f;
-                    sum = sum + pr;
-                }
+                if (b0 + ii == 0)
+                    fit_sample<true, true>(t, pv, in, anyA, anyB, agiant, fF, fJ, eF, eJ, fa0, Ja0, sum);
+                else
+                    fit_sample<true, false>(t, pv, in, anyA, anyB, agiant, fF, fJ, eF, eJ, fa0, Ja0, sum);
             }
+        } else {
+            double tv[FIT_TB];
+#pragma unroll
+            for (int ii = 0; ii < FIT_TB; ++ii) tv[ii] = T64[b0 + ii];
+            if (b0 == 0)
+                fit_sample<false, true>(tv[0], (double)tile[0][lane], in, anyA, anyB, agiant, fF, fJ, eF, eJ,
+                                        fa0, Ja0, sum);
+            else
+                fit_sample<false, false>(tv[0], (double)tile[0][lane], in, anyA, anyB, agiant, fF, fJ, eF, eJ,
+                                         fa0, Ja0, sum);
+#pragma unroll
+            for (int ii = 1; ii < FIT_TB; ++ii)
+                fit_sample<false, false>(tv[ii], (double)tile[ii][lane], in, anyA, anyB, agiant, fF, fJ, eF, eJ,
+                                         fa0, Ja0, sum);
         }
     }
     out.f0 = fa0;
@@ -710,17 +734,33 @@ __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
     S.x[k] = 1.0; S.par[k] = 0.0; S.iter[k] = 1; S.nfev[k] = 0; S.slow[k] = 0;
 }
 
+// list == nullptr: profiles [0, P) in order (first round); else list[0..nlist).
 __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, const double *__restrict__ T64,
-                                                 long P, int nbin, int ldD, FitStateArrays S)
+                                                 long P, int nbin, int ldD, const int32_t *__restrict__ list,
+                                                 int nlist, FitStateArrays S)
 {
     __shared__ float tile[FIT_TB][65];
     const int lane = threadIdx.x;
-    const long k0 = (long)blockIdx.x * 64;
-    const long k = k0 + lane;
-    const int st = (k < P) ? S.mode[k] : ST_DONE;
+    const long slot = (long)blockIdx.x * 64 + lane;
+    const long nact = list ? (long)nlist : P;
+    const bool in_range = slot < nact;
+    const long k = in_range ? (list ? (long)list[slot] : slot) : 0;
+    const int st = in_range ? S.mode[k] : ST_DONE;
     const bool reqA = (st == ST_A0) || (st == ST_A2);
     const bool reqB = (st == ST_B);
     if (!__any(reqA || reqB)) return;
+    // row pointers of the tile's 64 profiles (row 0 for empty slots: D's padding keeps it valid)
+    const float *rows[8];
+    {
+        const int r0 = lane >> 3, c4 = (lane & 7) * 4;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const long sl = (long)blockIdx.x * 64 + m * 8 + r0;
+            long kr = 0;
+            if (sl < nact) kr = list ? (long)list[sl] : sl;
+            rows[m] = D + (size_t)kr * ldD + c4;
+        }
+    }
     const double agiant = kRgiant / (double)nbin;
     const double eps = sqrt(DBL_EPSILON);
     PassIn in;
@@ -745,7 +785,7 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     o.bad = false;
     o.fnorm = o.acnorm = o.f0 = o.J0 = o.sum = 0.0;
     if (__any(fastA || fastB))
-        fit_sweep<false>(tile, D, T64, k0, ldD, nbin, lane, in, __any(fastA), __any(fastB), agiant, o);
+        fit_sweep<false>(tile, rows, T64, ldD, lane, in, __any(fastA), __any(fastB), agiant, o);
     const bool exA = reqA && (!fastA || o.bad);
     const bool exB = reqB && !fastB;
     if (__any(exA || exB)) {
@@ -753,7 +793,7 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
         ie.A = exA;
         ie.B = exB;
         PassOut oe;
-        fit_sweep<true>(tile, D, T64, k0, ldD, nbin, lane, ie, __any(exA), __any(exB), agiant, oe);
+        fit_sweep<true>(tile, rows, T64, ldD, lane, ie, __any(exA), __any(exB), agiant, oe);
         if (exA || exB) o = oe;
     }
     if (reqA) {
@@ -767,13 +807,19 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 }
 
 // Consume the sweep result, run lmdif's scalar logic to the next request.
-// counters[0] += number of profiles still needing a sweep.
-__global__ __launch_bounds__(256) void k_fit_state(FitStateArrays S, long P, double *__restrict__ amp_o,
-                                                   int32_t *__restrict__ info_o, int32_t *__restrict__ active)
+// Survivors (profiles still needing a sweep) are appended to next_list;
+// *next_n counts them (order within the list is irrelevant: profiles are independent).
+__global__ __launch_bounds__(256) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
+                                                   int nlist, double *__restrict__ amp_o,
+                                                   int32_t *__restrict__ info_o, int32_t *__restrict__ next_list,
+                                                   int32_t *__restrict__ next_n)
 {
-    const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long slot = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long nact = list ? (long)nlist : P;
     int still = 0;
-    if (k < P) {
+    long k = 0;
+    if (slot < nact) {
+        k = list ? (long)list[slot] : slot;
         int st = S.mode[k];
         if (st != ST_DONE) {
             LmState L;
@@ -806,8 +852,19 @@ __global__ __launch_bounds__(256) void k_fit_state(FitStateArrays S, long P, dou
             }
         }
     }
-    for (int off = 32; off > 0; off >>= 1) still += __shfl_xor(still, off);
-    if ((threadIdx.x & 63) == 0 && still) atomicAdd(active, still);
+    // wave-aggregated append
+    const unsigned long long m = __ballot(still);
+    const int cnt = __popcll(m);
+    int base = 0;
+    const int lane = threadIdx.x & 63;
+    if (cnt) {
+        if (lane == __ffsll((long long)m) - 1) base = atomicAdd(next_n, cnt);
+        base = __shfl(base, __ffsll((long long)m) - 1);
+        if (still) {
+            const int rank = __popcll(m & ((1ull << lane) - 1ull));
+            next_list[base + rank] = (int32_t)k;
+        }
+    }
 }
 
 // ============================================================ diagnostics
@@ -1733,16 +1790,21 @@ hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P)
 }
 
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           const FitStateArrays &S)
+                           const int32_t *list, int nlist, const FitStateArrays &S)
 {
-    hipLaunchKernelGGL(k_fit_pass, dim3(cdiv(P, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, S);
+    const long n = list ? (long)nlist : P;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fit_pass, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, list, nlist, S);
     return hipGetLastError();
 }
 
-hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, double *amp, int32_t *info,
-                            int32_t *active)
+hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list, int nlist,
+                            double *amp, int32_t *info, int32_t *next_list, int32_t *next_n)
 {
-    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(P, 256)), dim3(256), 0, st, S, P, amp, info, active);
+    const long n = list ? (long)nlist : P;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, 256)), dim3(256), 0, st, S, P, list, nlist, amp, info,
+                       next_list, next_n);
     return hipGetLastError();
 }
 

@@ -68,6 +68,7 @@ struct Session {
     double2 *tw = nullptr;
     PwPlan *plan = nullptr;
     FitStateArrays fs{};
+    int32_t *lists = nullptr;   // two active-profile lists of P entries
     void *fs_block = nullptr;   // one allocation backing fs
     int fit_rounds = 0;
     ic_run_stats stats{};
@@ -160,7 +161,7 @@ void free_all(Session *s)
     void *bufs[] = {s->raw,  s->D,     s->w0,   s->W,   s->base, s->base0, s->F,   s->wf,
                     s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
-                    s->lstat, s->tw,   s->plan, s->fs_block};
+                    s->lstat, s->tw,   s->plan, s->fs_block, s->lists};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &e : s->events) {
@@ -215,27 +216,33 @@ int iteration_template(Session *s)
     return 0;
 }
 
-// exact scipy leastsq for every profile (ic.py:266-272): sweep/state rounds
+// exact scipy leastsq for every profile (ic.py:266-272): sweep/state rounds over a
+// compacted list of the profiles that still need a data sweep.
 int run_fit(Session *s)
 {
     const long P = (long)s->P;
     const int nbin = s->p.nbin;
     CK(launch_fit_init(s->stream, s->fs, P));
-    int32_t active = 0;
+    const int32_t *cur = nullptr;       // first round: all profiles
+    int32_t ncur = (int32_t)P;
+    int32_t *bufs[2] = {s->lists, s->lists + P};
+    int which = 0;
     int round = 0;
-    int64_t swept = P;   // round 0 sweeps every profile
-    for (; round < 1000; ++round) {
-        LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, s->fs));
+    int64_t swept = 0;
+    for (; round < 1000 && ncur > 0; ++round) {
+        swept += ncur;
+        LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, cur, ncur, s->fs));
         CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t), s->stream));
-        LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, s->amp, s->info, s->counters));
-        CK(hipMemcpyAsync(&active, s->counters, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+        int32_t *next = bufs[which];
+        LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, ncur, s->amp, s->info, next, s->counters));
+        CK(hipMemcpyAsync(&ncur, s->counters, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
         CK(hipStreamSynchronize(s->stream));
-        if (active == 0) break;
-        swept += active;
+        cur = next;
+        which ^= 1;
     }
-    if (active != 0) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", round);
-    s->fit_rounds = round + 1;
-    s->stats.fit_rounds += round + 1;
+    if (ncur != 0) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", round);
+    s->fit_rounds = round;
+    s->stats.fit_rounds += round;
     s->stats.fit_profile_sweeps += swept;
     return 0;
 }
@@ -320,7 +327,9 @@ int ic_session_create(const ic_params *params, int device, void **out)
     AL(s->F, (size_t)nsub * nbin);
     AL(s->wf, (size_t)nsub);
     AL(s->T, (size_t)nbin);
-    AL(s->T64, (size_t)nbin);
+    AL(s->T64, (size_t)s->ldD);
+    if (hipMemset(s->T64, 0, sizeof(double) * s->ldD) != hipSuccess)
+        return bail(fail(IC_EHIP, "hipMemset(T64) failed"));   // zero tail: padded samples are no-ops
     AL(s->amp, P);
     AL(s->info, P);
     AL(s->std_, P);
@@ -333,6 +342,7 @@ int ic_session_create(const ic_params *params, int device, void **out)
     AL(s->counters, (size_t)(p.max_iter + 4));
     AL(s->tw, (size_t)nbin);
     AL(s->plan, 1);
+    AL(s->lists, 2 * P);
 #undef AL
     {
         // fit state: 23 double arrays + 5 int arrays, each padded to 256 B
