@@ -101,14 +101,40 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, stats, steps):
     return None
 
 
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC
+    summary (tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes of
+    this bench at --steps 1, FETCH_SIZE x2 for gfx950), only when it was
+    measured on the HIP sources being timed (source_sha)."""
+    import glob
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from pmc_traffic import source_sha
+    sha = source_sha()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+        with open(path) as f:
+            rec = json.load(f)
+        if rec.get("workload") == workload and rec.get("source_sha") == sha and kernel in rec["kernels"]:
+            return rec["kernels"][kernel]["traffic_bytes_per_launch"], os.path.basename(path)
+    return None, None
+
+
 def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
-    """Reference-like loop (per-profile scipy leastsq + numpy.ma), one thread."""
+    """Reference-like loop (per-profile scipy leastsq + numpy.ma), one thread,
+    on the first subints of the workload shape: a 2-subint probe sizes the
+    sample to about half of ``budget_s``."""
     from threadpoolctl import threadpool_limits
 
     from iterative_cleaner_amd import archive as ica
     from iterative_cleaner_amd import synth
     from oracle import reference_like
-    nsub = 4
+    with threadpool_limits(1):
+        data, w0, shift = synth.make_cube(2, nchan, nbin, seed, rfi)
+        ar = ica.Archive(data, w0, shift)
+        ar.pscrunch()
+        t0 = time.perf_counter()
+        reference_like.clean_loop(ar, 5, 5, 5, [0, 0, 1])
+        probe = time.perf_counter() - t0
+    nsub = int(max(2, min(64, 2 * 0.5 * budget_s / max(probe, 1e-3))))
     data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
     ar = ica.Archive(data, w0, shift)
     ar.pscrunch()
@@ -210,6 +236,9 @@ def main():
             per_kernel[kname] = {"ms_per_step": round(kv["ms"] / a.steps, 3),
                                  "launches_per_step": kv["launches"] // a.steps,
                                  "gbs": round(tb / (kv["ms"] / 1000.0) / 1e9, 1) if tb else None}
+        traffic, src = pmc_traffic(a.workload, dom)
+        roof["traffic"] = traffic
+        roof["traffic_source"] = src if traffic else "no PMC summary for these HIP sources"
         roof["per_kernel"] = per_kernel
         iter_bytes = 8 * P * nbin + 64 * P    # SURVEY §8(d) B_iter
         loop_gbs = iter_bytes * n_iter / (elapsed / a.steps) / 1e9

@@ -506,8 +506,6 @@ __device__ int lm_after_a2(LmState &L, double fnorm1)
     return lm_outer(L);
 }
 
-#define FIT_TB kFitTile
-
 // Exact fast path.  enorm: while every component is 0 or inside
 // (RDWARF, agiant) MINPACK's enorm reduces to sqrt(sum_seq a*a); that range is
 // verified per lane with integer compares on the high words (conservatively:
@@ -561,24 +559,75 @@ __device__ __forceinline__ bool x_in_fast_range(double x)
     return ax >= 0x1p-500 && ax <= 0x1p500;
 }
 
-// Load a 64-profile x FIT_TB-bin tile of D into LDS, transposed to tile[bin][profile].
-// D is padded to [roundup(P,64)][ldD], ldD = roundup(nbin, FIT_TB): no guards.
-// rows[m] = D + row(8m + lane/8) * ldD + (lane%8)*4: 8 row pointers per lane
-// (profiles of a compacted active list).
-__device__ __forceinline__ void load_tile(float (*tile)[65], const float *const (&rows)[8], int b0, int lane)
+// ---- data movement of a sweep: LDS-DMA, double buffered ----------------------
+// A wave owns 64 profiles (one per lane) and streams their rows of D through
+// two 4-KiB LDS buffers, 16 bins per tile, with global_load_lds_dwordx4: the
+// next tile is in flight while the current one is consumed, and no VGPRs hold
+// it on the way.  A DMA writes 1 KiB lane-linearly (slot = lane), so the
+// transpose to "lane p reads its own profile" is done on the SOURCE side:
+// instruction m, lane l fetches chunk c = (l&3) ^ ((l>>4)&3) (4 bins) of
+// profile 16m + l/4.  Profile p's chunk c then sits in slot
+// 64(p>>4) + 4(p&15) + (c ^ ((p>>2)&3)), and the ds_read_b128 of one chunk by
+// all 64 lanes hits 16 distinct 16-B slots in each 16-lane bank group.
+// D is padded to [roundup(P,64)][ldD], ldD a multiple of 32: no guards.
+#define FIT_TB 16
+#define FIT_BUF 4096
+
+typedef float fv4 __attribute__((ext_vector_type(4)));
+
+struct DmaTiles {
+    const float *src[4];   // this lane's DMA source for instruction m at bin 0
+    uint32_t rd[4];        // LDS byte address of this lane's chunk c in buffer 0
+    char *lds;             // buffer 0 (buffer 1 at +FIT_BUF)
+};
+
+__device__ __forceinline__ uint32_t lds_u32(const void *p)
 {
-    const int c4 = (lane & 7) * 4;
-    const int r0 = lane >> 3;
-    float4 v[8];
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+__device__ __forceinline__ void dma_tile(const DmaTiles &d, char *buf, int b0)
+{
 #pragma unroll
-    for (int m = 0; m < 8; ++m) v[m] = *(const float4 *)(rows[m] + b0);
+    for (int m = 0; m < 4; ++m)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(d.src[m] + b0),
+                                         (__attribute__((address_space(3))) void *)(buf + m * 1024), 16, 0, 0);
+}
+
+// ds_read in asm: the compiler would otherwise order every LDS read behind a
+// vmcnt(0) for the DMAs, draining the prefetch.  Ordering against the DMA is
+// the explicit counted vmcnt in sweep_dma; the lgkmcnt wait ties the values.
+template <int OFF>
+__device__ __forceinline__ void read_tile(const DmaTiles &d, fv4 (&v)[4])
+{
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const int r = m * 8 + r0;
-        tile[c4 + 0][r] = v[m].x;
-        tile[c4 + 1][r] = v[m].y;
-        tile[c4 + 2][r] = v[m].z;
-        tile[c4 + 3][r] = v[m].w;
+    for (int c = 0; c < 4; ++c) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[c]) : "v"(d.rd[c]), "i"(OFF));
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+}
+
+template <typename Body>
+__device__ __forceinline__ void sweep_dma(const DmaTiles &d, int ldD, Body &body)
+{
+    const int nt = ldD / FIT_TB;   // even
+    dma_tile(d, d.lds, 0);
+    for (int t = 0; t < nt; t += 2) {
+        fv4 v[4];
+        dma_tile(d, d.lds + FIT_BUF, (t + 1) * FIT_TB);
+        body.load_T(t * FIT_TB);   // scalar loads issued ahead of the waits
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        read_tile<0>(d, v);
+        body(t * FIT_TB, v);
+        body.fence();   // keep tile t's arithmetic ahead of the next wait
+        body.load_T((t + 1) * FIT_TB);
+        if (t + 2 < nt) {
+            dma_tile(d, d.lds, (t + 2) * FIT_TB);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        read_tile<FIT_BUF>(d, v);
+        body((t + 1) * FIT_TB, v);
+        body.fence();
     }
 }
 
@@ -593,109 +642,156 @@ struct PassOut {
     bool bad;                    // fast path left its verified range
 };
 
-// Per-sample work of one sweep.  Zero-padded samples (p = 0, T = 0) are exact
-// no-ops: f = J = 0 adds nothing to either enorm, and Jn*f = 0 to the dot.
-template <bool EXACT, bool FIRST>
-__device__ __forceinline__ void fit_sample(double t, double pv, const PassIn &in, bool anyA, bool anyB,
-                                           double agiant, FastAcc &fF, FastAcc &fJ, Enorm &eF, Enorm &eJ,
-                                           double &fa0, double &Ja0, double &sum)
-{
-    if (anyA && in.A) {
-        const double u = in.xa * t;
-        const double f = u - pv;
-        const double uh = in.xha * t;
-        const double wa = uh - pv;
-        const double d = wa - f;
-        double J;
-        if (EXACT) {
-            en_add(eF, f, agiant);
-            J = d / in.ha;
-            en_add(eJ, J, agiant);
-        } else {
-            fa_add(fF, f);
-            J = mdiv(d, in.ha, in.yha);
-            fa_add(fJ, J);
-        }
-        if (FIRST) {
-            fa0 = f;
-            Ja0 = J;
-        }
-    }
-    if (anyB && in.B) {
-        const double u = in.xb * t;
-        const double f = u - pv;
-        const double uh = in.xhb * t;
-        const double wa = uh - pv;
-        const double d = wa - f;
-        double J, Jn;
-        if (EXACT) {
-            J = d / in.hb;
-            Jn = J / in.ajb;
-        } else {
-            J = mdiv(d, in.hb, in.yhb);
-            Jn = mdiv(J, in.ajb, in.yaj);
-        }
-        if (FIRST) Jn = Jn + 1.0;
-        const double pr = Jn * f;
-        sum = sum + pr;
-    }
-}
-
-template <bool EXACT>
-__device__ void fit_sweep(float (*tile)[65], const float *const (&rows)[8], const double *__restrict__ T64,
-                          int ldD, int lane, const PassIn &in, bool anyA, bool anyB, double agiant,
-                          PassOut &out)
-{
+// Fast sweep body: straight-line over a 16-bin tile, wave-uniform predicates
+// only (lanes that did not request the sweep compute on defaults; their
+// results are discarded).  Zero-padded samples (p = 0, T = 0) are exact
+// no-ops: f = J = 0 adds nothing to either norm, and Jn*f = 0 to the dot.
+template <bool DA, bool DB>
+struct FastBody {
+    const PassIn &in;
+    const double *__restrict__ T64;
     FastAcc fF, fJ;
-    fa_zero(fF);
-    fa_zero(fJ);
-    Enorm eF, eJ;
-    en_zero(eF);
-    en_zero(eJ);
-    double fa0 = 0.0, Ja0 = 0.0, sum = 0.0;
-    for (int b0 = 0; b0 < ldD; b0 += FIT_TB) {
-        __syncthreads();
-        load_tile(tile, rows, b0, lane);
-        __syncthreads();
-        if (EXACT) {
-            for (int ii = 0; ii < FIT_TB; ++ii) {
-                const double t = T64[b0 + ii];
-                const double pv = (double)tile[ii][lane];
-                if (b0 + ii == 0)
-                    fit_sample<true, true>(t, pv, in, anyA, anyB, agiant, fF, fJ, eF, eJ, fa0, Ja0, sum);
-                else
-                    fit_sample<true, false>(t, pv, in, anyA, anyB, agiant, fF, fJ, eF, eJ, fa0, Ja0, sum);
+    double fa0, Ja0, sum;
+
+    __device__ __forceinline__ FastBody(const PassIn &i, const double *T) : in(i), T64(T)
+    {
+        fa_zero(fF);
+        fa_zero(fJ);
+        fa0 = Ja0 = sum = 0.0;
+    }
+
+    __device__ __forceinline__ void sample(double t, double pv, bool first)
+    {
+        if (DA) {
+            const double u = in.xa * t;
+            const double f = u - pv;
+            const double uh = in.xha * t;
+            const double wa = uh - pv;
+            const double d = wa - f;
+            fa_add(fF, f);
+            const double J = mdiv(d, in.ha, in.yha);
+            fa_add(fJ, J);
+            if (first) {
+                fa0 = f;
+                Ja0 = J;
             }
-        } else {
-            double tv[FIT_TB];
-#pragma unroll
-            for (int ii = 0; ii < FIT_TB; ++ii) tv[ii] = T64[b0 + ii];
-            if (b0 == 0)
-                fit_sample<false, true>(tv[0], (double)tile[0][lane], in, anyA, anyB, agiant, fF, fJ, eF, eJ,
-                                        fa0, Ja0, sum);
-            else
-                fit_sample<false, false>(tv[0], (double)tile[0][lane], in, anyA, anyB, agiant, fF, fJ, eF, eJ,
-                                         fa0, Ja0, sum);
-#pragma unroll
-            for (int ii = 1; ii < FIT_TB; ++ii)
-                fit_sample<false, false>(tv[ii], (double)tile[ii][lane], in, anyA, anyB, agiant, fF, fJ, eF, eJ,
-                                         fa0, Ja0, sum);
+        }
+        if (DB) {
+            const double u = in.xb * t;
+            const double f = u - pv;
+            const double uh = in.xhb * t;
+            const double wa = uh - pv;
+            const double d = wa - f;
+            const double J = mdiv(d, in.hb, in.yhb);
+            double Jn = mdiv(J, in.ajb, in.yaj);
+            if (first) Jn = Jn + 1.0;
+            const double pr = Jn * f;
+            sum = sum + pr;
         }
     }
-    out.f0 = fa0;
-    out.J0 = Ja0;
-    out.sum = sum;
-    if (EXACT) {
-        out.fnorm = en_fin(eF);
-        out.acnorm = en_fin(eJ);
-        out.bad = false;
-    } else {
-        const uint32_t hr1 = (uint32_t)((unsigned long long)__double_as_longlong(kRdwarf) >> 32) + 1u;
-        const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant) >> 32);
-        out.fnorm = fa_fin(fF);
-        out.acnorm = fa_fin(fJ);
-        out.bad = in.A && !(fa_ok(fF, hr1, hg) && fa_ok(fJ, hr1, hg));
+
+    // empty asm on the accumulators: the compiler may not sink a tile's
+    // arithmetic below the following s_waitcnt (asm statements keep their order)
+    __device__ __forceinline__ void fence()
+    {
+        asm volatile("" : "+v"(fF.s2), "+v"(fF.maxhi), "+v"(fF.minhm1), "+v"(fJ.s2), "+v"(fJ.maxhi),
+                     "+v"(fJ.minhm1), "+v"(sum));
     }
+
+    double tv[FIT_TB];   // the tile's template values (wave-uniform: SGPRs)
+    __device__ __forceinline__ void load_T(int b0)
+    {
+#pragma unroll
+        for (int i = 0; i < FIT_TB; ++i) tv[i] = T64[b0 + i];
+    }
+
+    __device__ __forceinline__ void operator()(int b0, const fv4 (&v)[4])
+    {
+        sample(tv[0], (double)v[0].x, b0 == 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c) sample(tv[4 * c], (double)v[c].x, false);
+            sample(tv[4 * c + 1], (double)v[c].y, false);
+            sample(tv[4 * c + 2], (double)v[c].z, false);
+            sample(tv[4 * c + 3], (double)v[c].w, false);
+        }
+    }
+};
+
+// Exact sweep body: MINPACK's branchy enorm and true divisions, per lane.
+struct ExactBody {
+    const PassIn &in;
+    const double *__restrict__ T64;
+    double agiant;
+    Enorm eF, eJ;
+    double fa0, Ja0, sum;
+
+    __device__ __forceinline__ ExactBody(const PassIn &i, const double *T, double ag) : in(i), T64(T), agiant(ag)
+    {
+        en_zero(eF);
+        en_zero(eJ);
+        fa0 = Ja0 = sum = 0.0;
+    }
+
+    __device__ void sample(double t, double pv, bool first)
+    {
+        if (in.A) {
+            const double u = in.xa * t;
+            const double f = u - pv;
+            const double uh = in.xha * t;
+            const double wa = uh - pv;
+            const double d = wa - f;
+            en_add(eF, f, agiant);
+            const double J = d / in.ha;
+            en_add(eJ, J, agiant);
+            if (first) {
+                fa0 = f;
+                Ja0 = J;
+            }
+        }
+        if (in.B) {
+            const double u = in.xb * t;
+            const double f = u - pv;
+            const double uh = in.xhb * t;
+            const double wa = uh - pv;
+            const double d = wa - f;
+            const double J = d / in.hb;
+            double Jn = J / in.ajb;
+            if (first) Jn = Jn + 1.0;
+            const double pr = Jn * f;
+            sum = sum + pr;
+        }
+    }
+
+    __device__ __forceinline__ void fence() {}
+    __device__ __forceinline__ void load_T(int) {}
+
+    __device__ void operator()(int b0, const fv4 (&v)[4])
+    {
+        for (int c = 0; c < 4; ++c) {
+            const int i = b0 + 4 * c;
+            sample(T64[i], (double)v[c].x, i == 0);
+            sample(T64[i + 1], (double)v[c].y, false);
+            sample(T64[i + 2], (double)v[c].z, false);
+            sample(T64[i + 3], (double)v[c].w, false);
+        }
+    }
+};
+
+template <bool DA, bool DB>
+__device__ __forceinline__ void fast_sweep(const DmaTiles &d, int ldD, const PassIn &in,
+                                           const double *__restrict__ T64, double agiant, PassOut &out)
+{
+    FastBody<DA, DB> body(in, T64);
+    sweep_dma(d, ldD, body);
+    const uint32_t hr1 = (uint32_t)((unsigned long long)__double_as_longlong(kRdwarf) >> 32) + 1u;
+    const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant) >> 32);
+    out.f0 = body.fa0;
+    out.J0 = body.Ja0;
+    out.sum = body.sum;
+    out.fnorm = fa_fin(body.fF);
+    out.acnorm = fa_fin(body.fJ);
+    out.bad = DA && in.A && !(fa_ok(body.fF, hr1, hg) && fa_ok(body.fJ, hr1, hg));
 }
 
 // ---- split lmdif: state machine (k_fit_state) <-> data sweeps (k_fit_pass) ----
@@ -735,11 +831,12 @@ __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
 }
 
 // list == nullptr: profiles [0, P) in order (first round); else list[0..nlist).
+// One wave per block (the LDS buffers are private to the wave: no barriers).
 __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, const double *__restrict__ T64,
                                                  long P, int nbin, int ldD, const int32_t *__restrict__ list,
                                                  int nlist, FitStateArrays S)
 {
-    __shared__ float tile[FIT_TB][65];
+    __shared__ __attribute__((aligned(16))) char lbuf[2 * FIT_BUF];
     const int lane = threadIdx.x;
     const long slot = (long)blockIdx.x * 64 + lane;
     const long nact = list ? (long)nlist : P;
@@ -749,17 +846,21 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     const bool reqA = (st == ST_A0) || (st == ST_A2);
     const bool reqB = (st == ST_B);
     if (!__any(reqA || reqB)) return;
-    // row pointers of the tile's 64 profiles (row 0 for empty slots: D's padding keeps it valid)
-    const float *rows[8];
+    DmaTiles dt;
+    dt.lds = lbuf;
     {
-        const int r0 = lane >> 3, c4 = (lane & 7) * 4;
+        const int c = (lane & 3) ^ ((lane >> 4) & 3);
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const long sl = (long)blockIdx.x * 64 + m * 8 + r0;
-            long kr = 0;
+        for (int m = 0; m < 4; ++m) {
+            const long sl = (long)blockIdx.x * 64 + m * 16 + (lane >> 2);
+            long kr = 0;   // empty slots read row 0 (valid: D is padded)
             if (sl < nact) kr = list ? (long)list[sl] : sl;
-            rows[m] = D + (size_t)kr * ldD + c4;
+            dt.src[m] = D + (size_t)kr * ldD + 4 * c;
         }
+        const uint32_t base = lds_u32(lbuf) + 16u * (uint32_t)(64 * (lane >> 4) + 4 * (lane & 15));
+        const int g = (lane >> 2) & 3;
+#pragma unroll
+        for (int c2 = 0; c2 < 4; ++c2) dt.rd[c2] = base + 16u * (uint32_t)(c2 ^ g);
     }
     const double agiant = kRgiant / (double)nbin;
     const double eps = sqrt(DBL_EPSILON);
@@ -784,17 +885,28 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     PassOut o;
     o.bad = false;
     o.fnorm = o.acnorm = o.f0 = o.J0 = o.sum = 0.0;
-    if (__any(fastA || fastB))
-        fit_sweep<false>(tile, rows, T64, ldD, lane, in, __any(fastA), __any(fastB), agiant, o);
+    const bool anyA = __any(fastA), anyB = __any(fastB);
+    if (anyA && anyB)
+        fast_sweep<true, true>(dt, ldD, in, T64, agiant, o);
+    else if (anyA)
+        fast_sweep<true, false>(dt, ldD, in, T64, agiant, o);
+    else if (anyB)
+        fast_sweep<false, true>(dt, ldD, in, T64, agiant, o);
     const bool exA = reqA && (!fastA || o.bad);
     const bool exB = reqB && !fastB;
     if (__any(exA || exB)) {
         PassIn ie = in;
         ie.A = exA;
         ie.B = exB;
-        PassOut oe;
-        fit_sweep<true>(tile, rows, T64, ldD, lane, ie, __any(exA), __any(exB), agiant, oe);
-        if (exA || exB) o = oe;
+        ExactBody body(ie, T64, agiant);
+        sweep_dma(dt, ldD, body);
+        if (exA || exB) {
+            o.f0 = body.fa0;
+            o.J0 = body.Ja0;
+            o.sum = body.sum;
+            o.fnorm = en_fin(body.eF);
+            o.acnorm = en_fin(body.eJ);
+        }
     }
     if (reqA) {
         S.o_fnorm[k] = o.fnorm;
@@ -933,6 +1045,12 @@ __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_doub
 __device__ __forceinline__ double2 cmul(double2 a, double2 w)
 {
     return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+// fused form for the power-of-two path (the FFT diagnostic is compared within
+// a tolerance, never bit-for-bit: pocketfft's own rounding is not reproduced)
+__device__ __forceinline__ double2 cmul_f(double2 a, double2 w)
+{
+    return make_double2(__builtin_fma(a.x, w.x, -(a.y * w.y)), __builtin_fma(a.x, w.y, a.y * w.x));
 }
 __device__ __forceinline__ double2 mul_mi(double2 a) { return make_double2(a.y, -a.x); }   // * (-i)
 
@@ -1220,12 +1338,15 @@ struct P2 {
     static constexpr int ACT = CH < 64 ? CH : 64;
     static constexpr int XPAD = N + 8 * NL;
     static constexpr int XBYTES = ((XPAD * 4 + 15) / 16) * 16;
-    static constexpr int CBYTES = M * 16;
+    static constexpr int CBYTES = (M + M / 8) * 16;   // complex points at cidx(q)
     static constexpr int WAVE_BYTES = XBYTES > CBYTES ? XBYTES : CBYTES;
     static constexpr int LG = __builtin_ctz(M);
 };
 
 __device__ __forceinline__ int xaddr(int idx) { return idx + 8 * (idx >> 7); }
+// complex work array: one 16-B pad per 8 points, so the radix-R scatter of the
+// first stage (lane stride R points) spreads over all 32 banks
+__device__ __forceinline__ int cidx(int q) { return q + (q >> 3); }
 
 template <typename T>
 __device__ __forceinline__ T shfl_xor_t(T v, int m) { return __shfl_xor(v, m); }
@@ -1269,7 +1390,7 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, bool first,
                     v[u][r] = valid ? make_double2((double)xv.x - mu, (double)xv.y - mu)
                                     : make_double2((double)xv.x, (double)xv.y);
                 } else {
-                    v[u][r] = C[q];
+                    v[u][r] = C[cidx(q)];
                 }
             }
         }
@@ -1285,21 +1406,21 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, bool first,
                 double2 wp = w1;
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
-                    v[u][r] = cmul(v[u][r], wp);
-                    if (r + 1 < R) wp = cmul(wp, w1);
+                    v[u][r] = cmul_f(v[u][r], wp);
+                    if (r + 1 < R) wp = cmul_f(wp, w1);
                 }
             }
             dft_small<R>(v[u]);
             const int idx = (b - k) * R + k;
 #pragma unroll
-            for (int r = 0; r < R; ++r) C[idx + r * Ns] = v[u][r];
+            for (int r = 0; r < R; ++r) C[cidx(idx + r * Ns)] = v[u][r];
         }
     }
     wave_sync();
 }
 
 template <int N>
-__global__ __launch_bounds__(256) void k_diag_p2(
+__global__ __launch_bounds__(512) void k_diag_p2(
     const float *__restrict__ D, const double *__restrict__ T64g, const double *__restrict__ amp,
     const int32_t *__restrict__ info, const float *__restrict__ w0, const int32_t *__restrict__ shift,
     const double2 *__restrict__ tw_g, int nsub, int nchan, int ldD, int pr_on, double pr_factor,
@@ -1309,14 +1430,13 @@ __global__ __launch_bounds__(256) void k_diag_p2(
     using C = P2<N>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2 *tw = (double2 *)smem;                     // N/2
-    double *T = (double *)(smem + (size_t)C::M * 16);  // N
+    const double *T = T64g;                            // L1/L2-resident, read coalesced
     const int wpb = blockDim.x >> 6;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     for (int q = threadIdx.x; q < C::M; q += blockDim.x) tw[q] = tw_g[q];
-    for (int q = threadIdx.x; q < N; q += blockDim.x) T[q] = T64g[q];
     __syncthreads();
-    unsigned char *wb = smem + (size_t)C::M * 16 + (size_t)N * 8 + (size_t)wave * C::WAVE_BYTES;
+    unsigned char *wb = smem + (size_t)C::M * 16 + (size_t)wave * C::WAVE_BYTES;
     float *X = (float *)wb;
     double2 *Cb = (double2 *)wb;   // aliases X after the first FFT stage has read it
     const unsigned P = (unsigned)nsub * (unsigned)nchan;
@@ -1428,8 +1548,8 @@ __global__ __launch_bounds__(256) void k_diag_p2(
             double best2 = 0.0;
             int nanf = 0;
             for (int kk = lane; kk <= C::M; kk += 64) {
-                const double2 zk = Cb[kk == C::M ? 0 : kk];
-                const double2 zm = Cb[kk == 0 ? 0 : C::M - kk];
+                const double2 zk = Cb[cidx(kk == C::M ? 0 : kk)];
+                const double2 zm = Cb[cidx(kk == 0 ? 0 : C::M - kk)];
                 const double er = 0.5 * (zk.x + zm.x), ei = 0.5 * (zk.y - zm.y);
                 const double orr = 0.5 * (zk.y + zm.y), oi = -0.5 * (zk.x - zm.x);
                 double wr = -1.0, wi = 0.0;
@@ -1438,9 +1558,9 @@ __global__ __launch_bounds__(256) void k_diag_p2(
                     wr = wv.x;
                     wi = wv.y;
                 }
-                const double re = er + (orr * wr - oi * wi);
-                const double im = ei + (orr * wi + oi * wr);
-                const double a2 = re * re + im * im;
+                const double re = er + __builtin_fma(orr, wr, -(oi * wi));
+                const double im = ei + __builtin_fma(orr, wi, oi * wr);
+                const double a2 = __builtin_fma(re, re, im * im);
                 nanf |= isnan(a2);
                 best2 = fmax(best2, a2);
             }
@@ -1816,8 +1936,8 @@ hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const 
 {
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
-        const size_t fixed = (size_t)(NN / 2) * 16 + (size_t)NN * 8;                               \
-        int wpb = 4;                                                                               \
+        const size_t fixed = (size_t)(NN / 2) * 16;                                                \
+        int wpb = 8;                                                                               \
         while (wpb > 1 && fixed + wpb * (size_t)P2<NN>::WAVE_BYTES > 150 * 1024) --wpb;            \
         const size_t shm = fixed + wpb * (size_t)P2<NN>::WAVE_BYTES;                               \
         const size_t P = (size_t)nsub * nchan;                                                     \
