@@ -164,10 +164,9 @@ def main():
     import torch.distributed as dist
 
     from iterative_cleaner_amd import _native
+    from iterative_cleaner_amd.dist import max_over_ranks, rank_world
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = rank_world()
     if world != a.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
     torch.cuda.set_device(local)
@@ -201,11 +200,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(t1 - t0, device=dev)
     ktimes = sess.kernel_times()
     stats = sess.run_stats()
     n_iter = out["n_iter"]

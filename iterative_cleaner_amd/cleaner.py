@@ -81,8 +81,13 @@ def _output_name(ar, args):
 
 
 def main(args):
+    """CLI driver (iterative_cleaner.py:59-62).  Under torchrun each rank cleans
+    its round-robin share of the archive list on its own GPU (batch mode,
+    SURVEY.md §8(e): no collective)."""
+    from .dist import rank_world, shard
+    rank, world, _ = rank_world()
     backend = archive_backend()
-    for arch in args.archive:
+    for arch in shard(args.archive, rank, world):
         ar = backend.Archive_load(arch)
         o_name = _output_name(ar, args)
         ar = clean(ar, args, arch)
