@@ -96,6 +96,8 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, stats, steps):
     }
     if name == "k_fit_pass":
         return 4 * nbin * stats["fit_profile_sweeps"] * steps
+    if name == "k_fit_tail":
+        return 4 * nbin * stats["fit_tail_sweeps"] * steps
     if name in per_launch:
         return per_launch[name] * launches
     return None
@@ -246,7 +248,9 @@ def main():
                                    " exact leastsq fit" % (a.workload, nsub, nchan, nbin),
                        "profiles_per_archive": P, "loops": loops[-1], "iterations": n_iter,
                        "fit_rounds": stats["fit_rounds"],
-                       "fit_sweeps_per_profile": round(stats["fit_profile_sweeps"] / P / max(1, n_iter), 2),
+                       "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"])
+                                                       / P / max(1, n_iter), 2),
+                       "fit_tail_sweeps": stats["fit_tail_sweeps"] // max(1, n_iter),
                        "parallelism": "replicas" if world > 1 else "single",
                        "loop_hbm_gbs": round(loop_gbs, 1),
                        "loop_hbm_frac": round(loop_gbs / HBM_PEAK_GBS, 4)},

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define IC_ABI_VERSION 1
+#define IC_ABI_VERSION 2
 
 #define IC_OK 0
 #define IC_EINVAL -1   /* bad argument / shape                         */
@@ -112,8 +112,15 @@ typedef struct {
     int32_t iterations;          /* cleaning loops executed                        */
     int32_t fit_rounds;          /* k_fit_pass launches, summed over iterations    */
     int64_t fit_profile_sweeps;  /* profiles swept by k_fit_pass, summed (x nbin x 4 B = fit bytes) */
+    int64_t fit_tail_sweeps;     /* profile sweeps done by k_fit_tail (the last few thousand profiles) */
 } ic_run_stats;
 int ic_get_run_stats(void *session, ic_run_stats *out);
+
+/* Scheduling knob of the exact fit: when at most `threshold` profiles still
+ * need data sweeps, k_fit_tail finishes them in one launch (one wave per
+ * profile) instead of further sweep/state rounds.  Results are identical either
+ * way (both paths are bit-exact).  0 = never; default 8192. */
+int ic_set_fit_tail(void *session, int64_t threshold);
 
 const char *ic_last_error(void);
 

@@ -12,13 +12,13 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libicgpu.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # symbols exported by libicgpu.so, as declared in include/iterative_cleaner.h
 EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session_destroy",
            "ic_upload", "ic_upload_device", "ic_run", "ic_get_residual", "ic_get_template",
            "ic_get_fit", "ic_get_diagnostics", "ic_get_kernel_times", "ic_kernel_name",
-           "ic_set_timing", "ic_get_run_stats", "ic_last_error")
+           "ic_set_timing", "ic_get_run_stats", "ic_set_fit_tail", "ic_last_error")
 
 
 class NativeError(RuntimeError):
@@ -35,7 +35,7 @@ class Params(C.Structure):
 
 class RunStats(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("fit_rounds", C.c_int32),
-                ("fit_profile_sweeps", C.c_int64)]
+                ("fit_profile_sweeps", C.c_int64), ("fit_tail_sweeps", C.c_int64)]
 
 
 class KernelTime(C.Structure):
@@ -76,6 +76,7 @@ def load_library(path: str = LIB_PATH):
     lib.ic_get_kernel_times.argtypes = [vp, C.POINTER(KernelTime), C.c_int]
     lib.ic_set_timing.argtypes = [vp, C.c_int]
     lib.ic_get_run_stats.argtypes = [vp, C.POINTER(RunStats)]
+    lib.ic_set_fit_tail.argtypes = [vp, C.c_int64]
     if lib.ic_abi_version() != ABI_VERSION:
         raise NativeError("libicgpu ABI %d != expected %d" % (lib.ic_abi_version(), ABI_VERSION))
     _lib = lib
@@ -204,11 +205,16 @@ class GpuSession:
     def set_timing(self, on: bool):
         self._check(self.lib.ic_set_timing(self.h, 1 if on else 0), "ic_set_timing")
 
+    def set_fit_tail(self, threshold: int):
+        """Profiles left at which k_fit_tail takes over the fit (0 = never)."""
+        self._check(self.lib.ic_set_fit_tail(self.h, int(threshold)), "ic_set_fit_tail")
+
     def run_stats(self):
         st = RunStats()
         self._check(self.lib.ic_get_run_stats(self.h, C.byref(st)), "ic_get_run_stats")
         return dict(iterations=st.iterations, fit_rounds=st.fit_rounds,
-                    fit_profile_sweeps=int(st.fit_profile_sweeps))
+                    fit_profile_sweeps=int(st.fit_profile_sweeps),
+                    fit_tail_sweeps=int(st.fit_tail_sweeps))
 
     def kernel_times(self):
         buf = (KernelTime * 32)()

@@ -36,6 +36,7 @@ enum KernelId {
     K_LINESTATS,
     K_COMBINE,
     K_RESIDUAL,
+    K_FIT_TAIL,
     K_COUNT
 };
 
@@ -72,10 +73,16 @@ hipError_t launch_fscrunch(hipStream_t st, const double *part, const double *wpa
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
                            double *T64);
 hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
+// list == nullptr: all P profiles; else list[0 .. *nlist) with *nlist <= bound
+// (the host sizes grids from a count it already knows: counts only shrink).
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           const int32_t *list, int nlist, const FitStateArrays &S);
-hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list, int nlist,
-                            double *amp, int32_t *info, int32_t *next_list, int32_t *next_n);
+                           const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S);
+hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
+                            const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
+                            int32_t *next_n);
+hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
+                           const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
+                           double *amp, int32_t *info, unsigned long long *sweeps);
 hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const double *amp,
                        const int32_t *info, const float *w0, const int32_t *shift, const double2 *tw,
                        const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,

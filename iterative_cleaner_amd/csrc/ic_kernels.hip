@@ -834,12 +834,13 @@ __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
 // One wave per block (the LDS buffers are private to the wave: no barriers).
 __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, const double *__restrict__ T64,
                                                  long P, int nbin, int ldD, const int32_t *__restrict__ list,
-                                                 int nlist, FitStateArrays S)
+                                                 const int32_t *__restrict__ nlist, FitStateArrays S)
 {
     __shared__ __attribute__((aligned(16))) char lbuf[2 * FIT_BUF];
     const int lane = threadIdx.x;
     const long slot = (long)blockIdx.x * 64 + lane;
-    const long nact = list ? (long)nlist : P;
+    const long nact = list ? (long)*nlist : P;   // the grid is only an upper bound
+    if ((long)blockIdx.x * 64 >= nact) return;
     const bool in_range = slot < nact;
     const long k = in_range ? (list ? (long)list[slot] : slot) : 0;
     const int st = in_range ? S.mode[k] : ST_DONE;
@@ -922,12 +923,13 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 // Survivors (profiles still needing a sweep) are appended to next_list;
 // *next_n counts them (order within the list is irrelevant: profiles are independent).
 __global__ __launch_bounds__(256) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
-                                                   int nlist, double *__restrict__ amp_o,
+                                                   const int32_t *__restrict__ nlist, double *__restrict__ amp_o,
                                                    int32_t *__restrict__ info_o, int32_t *__restrict__ next_list,
                                                    int32_t *__restrict__ next_n)
 {
     const long slot = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long nact = list ? (long)nlist : P;
+    const long nact = list ? (long)*nlist : P;
+    if ((long)blockIdx.x * blockDim.x >= nact) return;
     int still = 0;
     long k = 0;
     if (slot < nact) {
@@ -977,6 +979,169 @@ __global__ __launch_bounds__(256) void k_fit_state(FitStateArrays S, long P, con
             next_list[base + rank] = (int32_t)k;
         }
     }
+}
+
+// ---- tail: the last few thousand profiles, one wave each, to completion ----
+// Rounds over a small active list are latency-bound (a lone wave sweeping 64
+// profiles).  Here one wave owns ONE profile: lanes compute the per-sample
+// terms of a chunk in parallel (exact divisions), then every lane runs the
+// sequential MINPACK accumulation over the chunk in LDS (same values in all
+// lanes: uniform control flow), and the lmdif state machine runs in registers
+// between sweeps — no host round trips, no state traffic.  All arithmetic is
+// the exact path (true divisions, branchy enorm), so it matches k_fit_pass
+// bit for bit whatever the lane's range.
+#define TAIL_CH 256
+#define TAIL_WAVES 4
+
+__device__ __forceinline__ void tail_sweep_a(const float *__restrict__ p, const double *__restrict__ T64, int nbin,
+                                             double xa, double agiant, double (*buf)[TAIL_CH], int lane,
+                                             double &fnorm, double &acnorm, double &f0, double &J0)
+{
+    const double eps = sqrt(DBL_EPSILON);
+    double h = eps * fabs(xa);
+    if (h == 0.0) h = eps;
+    const double xh = xa + h;
+    Enorm eF, eJ;
+    en_zero(eF);
+    en_zero(eJ);
+    for (int c0 = 0; c0 < nbin; c0 += TAIL_CH) {
+        const int n = min(TAIL_CH, nbin - c0);
+        bool okF = true, okJ = true;   // every component 0 or inside (RDWARF, agiant)
+        for (int q = lane; q < n; q += 64) {
+            const double t = T64[c0 + q];
+            const double pv = (double)p[c0 + q];
+            const double u = xa * t;
+            const double f = u - pv;
+            const double uh = xh * t;
+            const double wa = uh - pv;
+            const double d = wa - f;
+            const double J = d / h;
+            buf[0][q] = f;
+            buf[1][q] = J;
+            const double af = fabs(f), aJ = fabs(J);
+            okF = okF && (af == 0.0 || (af > kRdwarf && af < agiant));
+            okJ = okJ && (aJ == 0.0 || (aJ > kRdwarf && aJ < agiant));
+            buf[2][q] = af * af;
+            buf[3][q] = aJ * aJ;
+        }
+        okF = __all(okF);
+        okJ = __all(okJ);
+        wave_sync();
+        if (c0 == 0) {
+            f0 = buf[0][0];
+            J0 = buf[1][0];
+        }
+        // in range, en_add is exactly s2 += x*x, in order (the squares were
+        // formed above, off the dependency chain)
+        if (okF && okJ) {   // the usual case: both chains interleaved
+            double sF = eF.s2, sJ = eJ.s2;
+            for (int q = 0; q < n; ++q) {
+                sF = sF + buf[2][q];
+                sJ = sJ + buf[3][q];
+            }
+            eF.s2 = sF;
+            eJ.s2 = sJ;
+        } else {
+            if (okF) {
+                for (int q = 0; q < n; ++q) eF.s2 = eF.s2 + buf[2][q];
+            } else {
+                for (int q = 0; q < n; ++q) en_add(eF, buf[0][q], agiant);
+            }
+            if (okJ) {
+                for (int q = 0; q < n; ++q) eJ.s2 = eJ.s2 + buf[3][q];
+            } else {
+                for (int q = 0; q < n; ++q) en_add(eJ, buf[1][q], agiant);
+            }
+        }
+        wave_sync();
+    }
+    fnorm = en_fin(eF);
+    acnorm = en_fin(eJ);
+}
+
+__device__ __forceinline__ double tail_sweep_b(const float *__restrict__ p, const double *__restrict__ T64, int nbin,
+                                               double x, double aj, double (*buf)[TAIL_CH], int lane)
+{
+    const double eps = sqrt(DBL_EPSILON);
+    double h = eps * fabs(x);
+    if (h == 0.0) h = eps;
+    const double xh = x + h;
+    double sum = 0.0;
+    for (int c0 = 0; c0 < nbin; c0 += TAIL_CH) {
+        const int n = min(TAIL_CH, nbin - c0);
+        for (int q = lane; q < n; q += 64) {
+            const double t = T64[c0 + q];
+            const double pv = (double)p[c0 + q];
+            const double u = x * t;
+            const double f = u - pv;
+            const double uh = xh * t;
+            const double wa = uh - pv;
+            const double d = wa - f;
+            const double J = d / h;
+            double Jn = J / aj;
+            if (c0 + q == 0) Jn = Jn + 1.0;
+            buf[0][q] = Jn * f;
+        }
+        wave_sync();
+        for (int q = 0; q < n; ++q) sum = sum + buf[0][q];
+        wave_sync();
+    }
+    return sum;
+}
+
+__global__ __launch_bounds__(64 * TAIL_WAVES) void k_fit_tail(const float *__restrict__ D,
+                                                              const double *__restrict__ T64, long P, int nbin,
+                                                              int ldD, const int32_t *__restrict__ list,
+                                                              const int32_t *__restrict__ nlist, FitStateArrays S,
+                                                              double *__restrict__ amp_o,
+                                                              int32_t *__restrict__ info_o,
+                                                              unsigned long long *__restrict__ sweeps)
+{
+    __shared__ double sbuf[TAIL_WAVES][4][TAIL_CH];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double(*buf)[TAIL_CH] = sbuf[wave];
+    const long nact = list ? (long)*nlist : P;
+    const double agiant = kRgiant / (double)nbin;
+    unsigned long long nsw = 0;
+    for (long slot = (long)blockIdx.x * TAIL_WAVES + wave; slot < nact; slot += (long)gridDim.x * TAIL_WAVES) {
+        const long k = list ? (long)list[slot] : slot;
+        int st = S.mode[k];
+        if (st == ST_DONE) continue;
+        LmState L;
+        lm_load(L, S, k);
+        double xa = S.xa[k];
+        const float *p = D + (size_t)k * ldD;
+        while (st != ST_DONE) {
+            ++nsw;
+            if (st == ST_B) {
+                const double sum = tail_sweep_b(p, T64, nbin, L.x, L.aj, buf, lane);
+                st = lm_after_b(L, sum);
+            } else {
+                double fnorm, acnorm, f0 = 0.0, J0 = 0.0;
+                tail_sweep_a(p, T64, nbin, xa, agiant, buf, lane, fnorm, acnorm, f0, J0);
+                if (st == ST_A0) {
+                    L.fnorm = fnorm;
+                    L.nfev = 1;
+                    L.acnorm = acnorm;
+                    L.f0 = f0;
+                    L.J0 = J0;
+                    st = lm_outer(L);
+                } else {
+                    L.acn2 = acnorm;
+                    L.f02 = f0;
+                    L.J02 = J0;
+                    st = lm_after_a2(L, fnorm);
+                }
+            }
+            if (st == ST_A2) xa = L.x2;
+        }
+        if (lane == 0) {
+            S.mode[k] = ST_DONE;
+            amp_o[k] = L.x;
+            info_o[k] = L.info;
+        }
+    }
+    if (lane == 0 && nsw) atomicAdd(sweeps, nsw);
 }
 
 // ============================================================ diagnostics
@@ -1792,10 +1957,15 @@ __global__ __launch_bounds__(256) void k_combine(
     double *__restrict__ test, float *__restrict__ W, float *__restrict__ hist, int iter,
     int32_t *__restrict__ counters)
 {
+    // grid-stride; the convergence counters are reduced per block (one atomic
+    // per counter per block: same-address atomics serialise at the memory side)
+    __shared__ int red[2][4];
+    __shared__ unsigned long long dred[4];
     const size_t P = (size_t)nsub * nchan;
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     int changed = 0, zero = 0;
-    if (k < P) {
+    unsigned long long diff = 0ull;   // bit h: W != hist[h] somewhere (h < 64)
+    const int hmax = iter < 64 ? iter : 64;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < P; k += (size_t)gridDim.x * blockDim.x) {
         const int s = (int)(k / nchan), c = (int)(k % nchan);
         const bool v = valid[k] != 0;
         double S[4];
@@ -1825,23 +1995,38 @@ __global__ __launch_bounds__(256) void k_combine(
         const float wn = (t >= 1.0) ? 0.0f : w0[k];
         W[k] = wn;
         hist[(size_t)iter * P + k] = wn;
-        changed = !(wn == hist[(size_t)(iter - 1) * P + k]);
-        zero = (wn == 0.0f);
+        changed += !(wn == hist[(size_t)(iter - 1) * P + k]);
+        zero += (wn == 0.0f);
+        // history equality (iterative_cleaner.py:135-136)
+        for (int h = 0; h < hmax; ++h)
+            if (!(wn == hist[(size_t)h * P + k])) diff |= 1ull << h;
+        for (int h = 64; h < iter; ++h)
+            if (!(wn == hist[(size_t)h * P + k])) atomicOr(&counters[2 + h], 1);
     }
-    // wave reduce then one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
         changed += __shfl_xor(changed, off);
         zero += __shfl_xor(zero, off);
+        diff |= __shfl_xor(diff, off);
     }
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        if (changed) atomicAdd(&counters[0], changed);
-        if (zero) atomicAdd(&counters[1], zero);
+        red[0][wave] = changed;
+        red[1][wave] = zero;
+        dred[wave] = diff;
     }
-    // history equality (iterative_cleaner.py:135-136): counters[2+h] |= any(W != hist[h])
-    for (int h = 0; h < iter; ++h) {
-        int d = 0;
-        if (k < P) d = !(W[k] == hist[(size_t)h * P + k]);
-        if (__any(d) && (threadIdx.x & 63) == 0) atomicOr(&counters[2 + h], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ch = 0, ze = 0;
+        unsigned long long df = 0ull;
+        for (int w = 0; w < nw; ++w) {
+            ch += red[0][w];
+            ze += red[1][w];
+            df |= dred[w];
+        }
+        if (ch) atomicAdd(&counters[0], ch);
+        if (ze) atomicAdd(&counters[1], ze);
+        for (int h = 0; h < hmax; ++h)
+            if ((df >> h) & 1ull) atomicOr(&counters[2 + h], 1);
     }
 }
 
@@ -1910,21 +2095,35 @@ hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P)
 }
 
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           const int32_t *list, int nlist, const FitStateArrays &S)
+                           const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S)
 {
-    const long n = list ? (long)nlist : P;
-    if (n == 0) return hipSuccess;
+    const long n = list ? bound : P;
+    if (n <= 0) return hipSuccess;
+    if (ldD % (2 * FIT_TB) != 0) return hipErrorInvalidValue;   // sweep_dma needs an even tile count
     hipLaunchKernelGGL(k_fit_pass, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, list, nlist, S);
     return hipGetLastError();
 }
 
-hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list, int nlist,
-                            double *amp, int32_t *info, int32_t *next_list, int32_t *next_n)
+hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
+                            const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
+                            int32_t *next_n)
 {
-    const long n = list ? (long)nlist : P;
-    if (n == 0) return hipSuccess;
+    const long n = list ? bound : P;
+    if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, 256)), dim3(256), 0, st, S, P, list, nlist, amp, info,
                        next_list, next_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
+                           const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
+                           double *amp, int32_t *info, unsigned long long *sweeps)
+{
+    const long n = list ? bound : P;
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<long>(cdiv(n, TAIL_WAVES), 65536);
+    hipLaunchKernelGGL(k_fit_tail, dim3(grid), dim3(64 * TAIL_WAVES), 0, st, D, T64, P, nbin, ldD, list, nlist,
+                       S, amp, info, sweeps);
     return hipGetLastError();
 }
 
@@ -1988,7 +2187,8 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
                           int32_t *counters)
 {
     const size_t P = (size_t)nsub * nchan;
-    hipLaunchKernelGGL(k_combine, dim3(cdiv(P, 256)), dim3(256), 0, st, nsub, nchan, valid, w0, std_d,
+    const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 256), 1024);
+    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(256), 0, st, nsub, nchan, valid, w0, std_d,
                        mean_d, ptp_d, fft_d, col_med, col_mad, row_med, row_mad, chanthresh, subintthresh,
                        test, W, hist, iter, counters);
     return hipGetLastError();

@@ -40,9 +40,13 @@ int fail(int code, const char *fmt, ...)
                         __LINE__);                                                                \
     } while (0)
 
-const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",   "k_base",      "k_fitcube",
-                                     "k_fscrunch",      "k_tscrunch", "k_fit_pass",  "k_fit_state",
-                                     "k_diag",          "k_linestats", "k_combine",  "k_residual"};
+const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",     "k_fitcube",
+                                     "k_fscrunch",      "k_tscrunch",  "k_fit_pass", "k_fit_state",
+                                     "k_diag",          "k_linestats", "k_combine",  "k_residual",
+                                     "k_fit_tail"};
+
+constexpr int kMaxRounds = 1024;      // lmdif rounds per fit (maxfev = 400 bounds it far below)
+constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
 
 struct Timed {
     int kid;
@@ -69,8 +73,12 @@ struct Session {
     PwPlan *plan = nullptr;
     FitStateArrays fs{};
     int32_t *lists = nullptr;   // two active-profile lists of P entries
+    int32_t *rcount = nullptr;  // per-round survivor counts [kMaxRounds] (+ tail sweep counter)
+    int32_t *h_rcount = nullptr;  // pinned host mirror
+    hipEvent_t rev[2] = {nullptr, nullptr};
     void *fs_block = nullptr;   // one allocation backing fs
     int fit_rounds = 0;
+    long tail_threshold = kTailProfiles;
     ic_run_stats stats{};
     // timing
     bool timing = false;
@@ -161,9 +169,12 @@ void free_all(Session *s)
     void *bufs[] = {s->raw,  s->D,     s->w0,   s->W,   s->base, s->base0, s->F,   s->wf,
                     s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
-                    s->lstat, s->tw,   s->plan, s->fs_block, s->lists};
+                    s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    if (s->h_rcount) (void)hipHostFree(s->h_rcount);
+    for (auto &e : s->rev)
+        if (e) (void)hipEventDestroy(e);
     for (auto &e : s->events) {
         (void)hipEventDestroy(e.a);
         (void)hipEventDestroy(e.b);
@@ -216,34 +227,65 @@ int iteration_template(Session *s)
     return 0;
 }
 
-// exact scipy leastsq for every profile (ic.py:266-272): sweep/state rounds over a
-// compacted list of the profiles that still need a data sweep.
+// exact scipy leastsq for every profile (ic.py:266-272).
+// Rounds of k_fit_pass + k_fit_state over a compacted list of the profiles
+// that still need a data sweep.  Each round's survivor count lands in
+// rcount[r] on the device; kernels read their list length from there, so the
+// host only needs an UPPER bound to size grids (counts never grow) and reads
+// the counts one round behind: the stream always has the next round queued.
+// Once the bound drops to tail_threshold (default kTailProfiles; 0 = never),
+// k_fit_tail finishes the rest in one launch (one wave per profile).
 int run_fit(Session *s)
 {
     const long P = (long)s->P;
     const int nbin = s->p.nbin;
     CK(launch_fit_init(s->stream, s->fs, P));
-    const int32_t *cur = nullptr;       // first round: all profiles
-    int32_t ncur = (int32_t)P;
+    CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * (kMaxRounds + 2), s->stream));
+    unsigned long long *tail_sweeps = (unsigned long long *)(s->rcount + kMaxRounds);
     int32_t *bufs[2] = {s->lists, s->lists + P};
-    int which = 0;
-    int round = 0;
-    int64_t swept = 0;
-    for (; round < 1000 && ncur > 0; ++round) {
-        swept += ncur;
-        LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, cur, ncur, s->fs));
-        CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t), s->stream));
-        int32_t *next = bufs[which];
-        LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, ncur, s->amp, s->info, next, s->counters));
-        CK(hipMemcpyAsync(&ncur, s->counters, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
-        CK(hipStreamSynchronize(s->stream));
+    const int32_t *cur = nullptr, *cin = nullptr;   // round 0: all profiles
+    long bound = P;                                 // >= the active count of the next round
+    int rounds = 0;
+    bool tail = false;
+    for (int r = 0;; ++r) {
+        if (r >= kMaxRounds) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", r);
+        if (bound <= s->tail_threshold) {
+            LAUNCH(s, K_FIT_TAIL, launch_fit_tail(s->stream, s->D, s->T64, P, nbin, s->ldD, cur, cin, bound,
+                                                  s->fs, s->amp, s->info, tail_sweeps));
+            tail = true;
+            break;
+        }
+        int32_t *next = bufs[r & 1];
+        LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, cur, cin, bound, s->fs));
+        LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
+                                                s->rcount + r));
+        CK(hipMemcpyAsync(s->h_rcount + r, s->rcount + r, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+        CK(hipEventRecord(s->rev[r & 1], s->stream));
+        ++rounds;
         cur = next;
-        which ^= 1;
+        cin = s->rcount + r;
+        if (r >= 1) {
+            // count after round r-1 (= input of round r) bounds the count after round r
+            CK(hipEventSynchronize(s->rev[(r - 1) & 1]));
+            const long c = s->h_rcount[r - 1];
+            if (c == 0) break;   // round r had nothing to do
+            bound = c;
+        }
     }
-    if (ncur != 0) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", round);
-    s->fit_rounds = round;
-    s->stats.fit_rounds += round;
+    CK(hipStreamSynchronize(s->stream));
+    int64_t swept = rounds > 0 ? P : 0;   // round 0 input
+    for (int r = 0; r + 1 < rounds; ++r) swept += s->h_rcount[r];
+    int effective = rounds;
+    if (!tail) {
+        // trailing rounds that had an empty input list
+        while (effective > 1 && s->h_rcount[effective - 2] == 0) --effective;
+    }
+    unsigned long long tsw = 0;
+    CK(hipMemcpy(&tsw, tail_sweeps, sizeof tsw, hipMemcpyDeviceToHost));
+    s->fit_rounds = effective;
+    s->stats.fit_rounds += effective;
     s->stats.fit_profile_sweeps += swept;
+    s->stats.fit_tail_sweeps += (int64_t)tsw;
     return 0;
 }
 
@@ -343,7 +385,13 @@ int ic_session_create(const ic_params *params, int device, void **out)
     AL(s->tw, (size_t)nbin);
     AL(s->plan, 1);
     AL(s->lists, 2 * P);
+    AL(s->rcount, (size_t)kMaxRounds + 2);
 #undef AL
+    if (hipHostMalloc((void **)&s->h_rcount, sizeof(int32_t) * kMaxRounds, hipHostMallocDefault) != hipSuccess)
+        return bail(fail(IC_ENOMEM, "hipHostMalloc(round counts) failed"));
+    for (auto &e : s->rev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+            return bail(fail(IC_EHIP, "hipEventCreate failed"));
     {
         // fit state: 23 double arrays + 5 int arrays, each padded to 256 B
         const size_t dstride = ((P * 8 + 255) / 256) * 256, istride = ((P * 4 + 255) / 256) * 256;
@@ -527,6 +575,15 @@ int ic_get_residual(void *session, float *out)
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(R);
     if (e != hipSuccess) return fail(IC_EHIP, "residual: %s", hipGetErrorString(e));
+    return IC_OK;
+}
+
+int ic_set_fit_tail(void *session, int64_t threshold)
+{
+    Session *s = (Session *)session;
+    if (!s) return fail(IC_EINVAL, "null session");
+    if (threshold < 0) return fail(IC_EINVAL, "negative tail threshold");
+    s->tail_threshold = (long)threshold;
     return IC_OK;
 }
 

@@ -16,11 +16,18 @@ FFT_RTOL = 1e-9
 TEST_ATOL = 1e-9
 
 
-def _session(shape, args, duty=0.15):
+# exact-fit schedules: sweep/state rounds only, k_fit_tail only, and the default mix
+FIT_MODES = {"rounds": 0, "tail": 1 << 40, "default": None}
+
+
+def _session(shape, args, duty=0.15, fit_mode="default"):
     from iterative_cleaner_amd import _native
     nsub, nchan, nbin = shape
-    return _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"],
-                              args["subintthresh"], args["pulse_region"], duty, device=0)
+    s = _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"],
+                           args["subintthresh"], args["pulse_region"], duty, device=0)
+    if FIT_MODES[fit_mode] is not None:
+        s.set_fit_tail(FIT_MODES[fit_mode])
+    return s
 
 
 def _close_fft(a, b):
@@ -39,11 +46,12 @@ def _close_test(a, b):
     return bool(ok.all())
 
 
+@pytest.mark.parametrize("fit_mode", sorted(FIT_MODES))
 @pytest.mark.parametrize("path", clean_fixtures(), ids=lambda p: os.path.basename(p)[6:-4])
-def test_loop_matches_reference(path):
+def test_loop_matches_reference(path, fit_mode):
     z, meta, raw, w0, shift, args = load_clean_case(path)
     nit = int(z["n_iter"])
-    with _session(raw.shape, args) as s:
+    with _session(raw.shape, args, fit_mode=fit_mode) as s:
         s.upload(raw, w0, shift)
         out = s.run()
         T = s.template()
@@ -104,8 +112,9 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("fit_mode", ["rounds", "tail"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "%dx%dx%d" % c[:3])
-def test_loop_matches_c_oracle(case, oracle_lib):
+def test_loop_matches_c_oracle(case, fit_mode, oracle_lib):
     from iterative_cleaner_amd import synth
     nsub, nchan, nbin, seed, rfi, extra = case
     data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
@@ -115,12 +124,17 @@ def test_loop_matches_c_oracle(case, oracle_lib):
     pr = None if args["pulse_region"] == [0, 0, 1] else args["pulse_region"]
     ref = oracle_lib.clean_loop(raw, w0, shift, args["chanthresh"], args["subintthresh"],
                                 args["max_iter"], pr, want_residual=True, want_details=True)
-    with _session(raw.shape, args) as s:
+    with _session(raw.shape, args, fit_mode=fit_mode) as s:
         s.upload(raw, w0, shift)
         out = s.run()
         amp, info = s.fit()
         sd, mn, pt, ff = s.diagnostics()
         R = s.residual()
+        st = s.run_stats()
+    if fit_mode == "rounds":
+        assert st["fit_tail_sweeps"] == 0
+    else:
+        assert st["fit_profile_sweeps"] == 0 and st["fit_tail_sweeps"] > 0
     assert out["loops"] == ref["loops"]
     assert bits_equal(out["weights"], ref["weights"])
     assert np.array_equal(out["changed"], ref["changed"][:out["n_iter"]])
@@ -131,7 +145,8 @@ def test_loop_matches_c_oracle(case, oracle_lib):
     assert bits_equal(R, ref["residual"])
 
 
-def test_edge_profiles_match_c_oracle(oracle_lib):
+@pytest.mark.parametrize("fit_mode", ["rounds", "tail"])
+def test_edge_profiles_match_c_oracle(fit_mode, oracle_lib):
     """Dead (all-zero) channels with weight 1, zero profiles, a NaN-free
     constant channel, fractional weights (K2, K7, K10)."""
     from iterative_cleaner_amd import synth
@@ -145,7 +160,7 @@ def test_edge_profiles_match_c_oracle(oracle_lib):
     w0[2, 9] = 0.0
     ref = oracle_lib.clean_loop(raw, w0, shift, want_details=True)
     args = dict(max_iter=5, chanthresh=5, subintthresh=5, pulse_region=[0, 0, 1])
-    with _session(raw.shape, args) as s:
+    with _session(raw.shape, args, fit_mode=fit_mode) as s:
         s.upload(raw, w0, shift)
         out = s.run()
         amp, info = s.fit()
