@@ -144,42 +144,54 @@ __global__ __launch_bounds__(256) void k_window(const double *__restrict__ part,
 // One wave per 64 profiles; window chunks of 64 positions are loaded coalesced
 // (one profile row per load instruction) into a transposed LDS tile, then each
 // lane adds its own profile's column in order.
+// Per-profile baseline level: f32(sum_seq f64(x_j) / width) over the subint's
+// window, in the dedispersed frame (Appendix C stand-in; oracle orc_baseline).
+// One wave per profile.  The sequential f64 sum of f32 values is computed in
+// parallel when that is provably exact: every x_j is an integer multiple of
+// 2^(emin-150) and |sum| < width * 2^(emax-126), so when
+// ceil(log2 width) + emax - emin + 24 <= 53 every partial sum, in any order,
+// is representable and the result equals the sequential one bit for bit.
+// Otherwise (rare: values spanning > 2^21, or Inf/NaN) the wave walks the
+// window in order.
 __global__ __launch_bounds__(256) void k_base(const float *__restrict__ raw, const int32_t *__restrict__ shift,
                                               const int32_t *__restrict__ win, int nsub, int nchan,
                                               int nbin, int width, float *__restrict__ base)
 {
-    __shared__ float buf[4][64][65];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const size_t P = (size_t)nsub * nchan;
-    const size_t k0 = ((size_t)blockIdx.x * 4 + wave) * 64;
-    if (k0 >= P) return;
-    const size_t k = k0 + lane;
-    const bool live = k < P;
-    int q0 = 0;
-    if (live) {
-        q0 = win[k / nchan] + shift[k % nchan];
+    const long P = (long)nsub * nchan;
+    const int lgw = 32 - __clz(max(width - 1, 1));   // ceil(log2(width)), >= 1
+    for (long k = (long)blockIdx.x * 4 + wave; k < P; k += (long)gridDim.x * 4) {
+        int q0 = win[k / nchan] + shift[k % nchan];
         if (q0 >= nbin) q0 -= nbin;
-    }
-    float(*t)[65] = buf[wave];
-    double acc = 0.0;
-    for (int c0 = 0; c0 < width; c0 += 64) {
-        wave_sync();
-        for (int r = 0; r < 64; ++r) {
-            const size_t kr = k0 + r;
-            const int qr = __shfl(q0, r);
-            float v = 0.0f;
-            if (kr < P && c0 + lane < width) {
-                int q = qr + c0 + lane;
-                q %= nbin;
-                v = raw[kr * nbin + q];
+        const float *row = raw + (size_t)k * nbin;
+        double acc = 0.0;
+        int emax = 0, emin = 255;
+        for (int j = lane; j < width; j += 64) {
+            int q = q0 + j;
+            if (q >= nbin) q -= nbin;
+            const float x = row[q];
+            acc = acc + (double)x;
+            const int be = max((int)((__float_as_uint(x) >> 23) & 0xffu), 1);
+            if (x != 0.0f) {
+                emax = max(emax, be);
+                emin = min(emin, be);
             }
-            t[lane][r] = v;
         }
-        wave_sync();
-        const int cn = min(64, width - c0);
-        for (int q = 0; q < cn; ++q) acc = acc + (double)t[q][lane];
+        for (int off = 32; off > 0; off >>= 1) {
+            acc = acc + __shfl_xor(acc, off);
+            emax = max(emax, __shfl_xor(emax, off));
+            emin = min(emin, __shfl_xor(emin, off));
+        }
+        if (emax != 0 && lgw + emax - emin + 24 > 53) {
+            acc = 0.0;   // in order (uniform: every lane walks the same values)
+            for (int j = 0; j < width; ++j) {
+                int q = q0 + j;
+                if (q >= nbin) q -= nbin;
+                acc = acc + (double)row[q];
+            }
+        }
+        if (lane == 0) base[k] = (float)(acc / (double)width);
     }
-    if (live) base[k] = (float)(acc / (double)width);
 }
 
 // D[k][i] = f32(ded[k][i] - base0[k])  (fit cube, dedispersed frame); one row per wave step
@@ -2058,8 +2070,8 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
                        int nsub, int nchan, int nbin, int width, float *base)
 {
     const size_t P = (size_t)nsub * nchan;
-    hipLaunchKernelGGL(k_base, dim3(cdiv(P, 256)), dim3(256), 0, st, raw, shift, win, nsub, nchan, nbin,
-                       width, base);
+    const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
+    hipLaunchKernelGGL(k_base, dim3(grid), dim3(256), 0, st, raw, shift, win, nsub, nchan, nbin, width, base);
     return hipGetLastError();
 }
 

@@ -209,18 +209,23 @@ int prepare(Session *s)
     return 0;
 }
 
-int iteration_template(Session *s)
+int iteration_template(Session *s, int iter)
 {
     const int nsub = s->p.nsub, nchan = s->p.nchan, nbin = s->p.nbin;
-    // remove_baseline with the current weights (template stage)
-    LAUNCH(s, K_CHAN_PARTIALS,
-           launch_chan_partials(s->stream, s->raw, s->W, s->shift, nullptr, nsub, nchan, nbin, s->part,
-                                nullptr));
-    LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win));
-    LAUNCH(s, K_BASE, launch_base(s->stream, s->raw, s->shift, s->win, nsub, nchan, nbin, s->width, s->base));
+    // remove_baseline with the current weights (template stage).  In the first
+    // iteration W == w0, so the baseline is exactly prepare()'s base0.
+    const float *base = s->base0;
+    if (iter > 1) {
+        LAUNCH(s, K_CHAN_PARTIALS,
+               launch_chan_partials(s->stream, s->raw, s->W, s->shift, nullptr, nsub, nchan, nbin, s->part,
+                                    nullptr));
+        LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win));
+        LAUNCH(s, K_BASE, launch_base(s->stream, s->raw, s->shift, s->win, nsub, nchan, nbin, s->width, s->base));
+        base = s->base;
+    }
     // dedisperse + fscrunch + tscrunch
     LAUNCH(s, K_CHAN_PARTIALS,
-           launch_chan_partials(s->stream, s->raw, s->W, s->shift, s->base, nsub, nchan, nbin, s->part,
+           launch_chan_partials(s->stream, s->raw, s->W, s->shift, base, nsub, nchan, nbin, s->part,
                                 s->wpart));
     LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->part, s->wpart, nsub, s->nsb, nbin, s->F, s->wf));
     LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64));
@@ -517,7 +522,7 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
     while (x < p.max_iter) {
         x += 1;
         ++n_iter;
-        if (int rc = iteration_template(s)) return rc;
+        if (int rc = iteration_template(s, n_iter)) return rc;
         if (int rc = run_fit(s)) return rc;
         LAUNCH(s, K_DIAG,
                launch_diag(s->stream, s->D, s->T64, s->amp, s->info, s->w0, s->shift, s->tw, s->plan, nsub,
