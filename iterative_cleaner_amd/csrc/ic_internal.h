@@ -83,9 +83,10 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
                            double *amp, int32_t *info, unsigned long long *sweeps);
+// tw: exp(-2 pi i q/nbin), q < nbin; tw_p2 (power-of-two nbin only): see p2_twiddles()
 hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const double *amp,
                        const int32_t *info, const float *w0, const int32_t *shift, const double2 *tw,
-                       const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
+                       const double2 *tw_p2, const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
                        int pr_start, int pr_end, double *std_o, double *mean_o, float *ptp_o,
                        double *fft_o);
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a);

@@ -42,6 +42,70 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- cross-lane trees on DPP + readlane (VALU latency, no LDS crossbar) ----
+// Level m of an xor-butterfly pairs lane groups [0,m) and [m,2m).  Within a
+// row of 16 that is quad_perm (m = 1, 2), row_half_mirror (m = 4) and
+// row_mirror (m = 8): after level m every lane of a group of m holds the same
+// value, so a mirror delivers the partner group's value.  The last two levels
+// combine lanes 0, 16, 32, 48 read into scalars, in tree order.  The result is
+// wave-uniform.  (IEEE add/max/min are commutative: a lane adding its partner's
+// value gets the same bits as the partner adding its own.)
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ float lane_read(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ int lane_read(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double lane_read(double v, int l)
+{
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+// tree over lanes [0, ACT) (ACT a power of two <= 64), uniform result
+template <int ACT, typename T, typename Op>
+__device__ __forceinline__ T wave_tree(T v, Op op)
+{
+    if (ACT >= 2) v = op(v, dpp<kDppXor1>(v));
+    if (ACT >= 4) v = op(v, dpp<kDppXor2>(v));
+    if (ACT >= 8) v = op(v, dpp<kDppHalfMirror>(v));
+    if (ACT >= 16) v = op(v, dpp<kDppMirror>(v));
+    if (ACT == 64) return op(op(lane_read(v, 0), lane_read(v, 16)), op(lane_read(v, 32), lane_read(v, 48)));
+    if (ACT == 32) return op(lane_read(v, 0), lane_read(v, 16));
+    return lane_read(v, 0);
+}
+
+struct OpAdd {
+    template <typename T>
+    __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
+};
+struct OpMaxF {
+    __device__ __forceinline__ float operator()(float a, float b) const { return fmaxf(a, b); }
+    __device__ __forceinline__ double operator()(double a, double b) const { return fmax(a, b); }
+};
+struct OpMinF {
+    __device__ __forceinline__ float operator()(float a, float b) const { return fminf(a, b); }
+};
+struct OpOr {
+    __device__ __forceinline__ int operator()(int a, int b) const { return a | b; }
+};
+
+
 // ============================================================ template stage
 
 // part[s][sb][i] = sum_{c in sb, ascending} W[s,c] * x[s,c,i]   (f64, from 0.0)
@@ -1402,11 +1466,9 @@ __global__ __launch_bounds__(256) void k_diag(
                 mx = fmaxf(mx, v);
                 mn = fminf(mn, v);
             }
-            for (int off = 32; off > 0; off >>= 1) {
-                mx = fmaxf(mx, __shfl_xor(mx, off));
-                mn = fminf(mn, __shfl_xor(mn, off));
-                nan |= __shfl_xor(nan, off);
-            }
+            mx = wave_tree<64>(mx, OpMaxF());
+            mn = wave_tree<64>(mn, OpMinF());
+            nan = wave_tree<64>(nan, OpOr());
             ptp = nan ? NAN : (mx - mn);
         }
         // fftmax: max_k |rfft(v)_k|, v = f64(X) - mean (valid) or f64(X) (invalid)
@@ -1515,41 +1577,39 @@ struct P2 {
     static constexpr int ACT = CH < 64 ? CH : 64;
     static constexpr int XPAD = N + 8 * NL;
     static constexpr int XBYTES = ((XPAD * 4 + 15) / 16) * 16;
-    static constexpr int CBYTES = (M + M / 8) * 16;   // complex points at cidx(q)
+    static constexpr int CBYTES = M * 16;   // complex points at cidx(q)
     static constexpr int WAVE_BYTES = XBYTES > CBYTES ? XBYTES : CBYTES;
     static constexpr int LG = __builtin_ctz(M);
+    static constexpr int TW = 2 * M;   // twiddle entries: M post-processing + <= M stage tables
 };
 
 __device__ __forceinline__ int xaddr(int idx) { return idx + 8 * (idx >> 7); }
-// complex work array: one 16-B pad per 8 points, so the radix-R scatter of the
-// first stage (lane stride R points) spreads over all 32 banks
-__device__ __forceinline__ int cidx(int q) { return q + (q >> 3); }
+// complex work array slot of point q: XOR swizzle of the low 3 bits with bits
+// 3-5.  Conflict-free for every access of the kernel: the radix-8 scatters
+// (ds_write_b128, 8-lane groups over 32 banks: low bits (b&7)^r or r^(b&7)) and
+// the contiguous / reversed gathers (ds_read_b128, 16-lane groups over 64 banks).
+__device__ __forceinline__ int cidx(int q) { return q ^ ((q >> 3) & 7); }
 
-template <typename T>
-__device__ __forceinline__ T shfl_xor_t(T v, int m) { return __shfl_xor(v, m); }
-
-// xor-butterfly combine over lanes [0, act): levels 1,2,4,... < act
 template <typename T, int ACT>
 __device__ __forceinline__ T tree_lanes(T v)
 {
-#pragma unroll
-    for (int m = 1; m < ACT; m <<= 1) v = v + shfl_xor_t(v, m);
-    return v;
+    return wave_tree<ACT>(v, OpAdd());
 }
 
 template <typename T, int CPL>
 __device__ __forceinline__ T tree_slots(const T (&v)[CPL])
 {
-    if (CPL == 1) return v[0];
-    if (CPL == 2) return v[0] + v[1];
-    if (CPL == 4) return (v[0] + v[1]) + (v[2] + v[3]);
-    // CPL == 8
-    return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    if constexpr (CPL == 1) return v[0];
+    else if constexpr (CPL == 2) return v[0] + v[1];
+    else if constexpr (CPL == 4) return (v[0] + v[1]) + (v[2] + v[3]);
+    else return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));   // CPL == 8
 }
 
+// stw: this stage's twiddles w^(r k), w = exp(-2 pi i/(R Ns)), as [k][r-1]
+// (host-built in long double; no recurrences)
 template <int R, int BPL, int M, int N>
 __device__ __forceinline__ void p2_stage(double2 *C, const float *X, bool first, bool valid, double mu,
-                                         int Ns, const double2 *tw, int lane)
+                                         int Ns, const double2 *stw, int lane)
 {
     constexpr int NB = M / R;
     double2 v[BPL][R];
@@ -1579,13 +1639,9 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, bool first,
         if (b < NB) {
             const int k = kk[u];
             if (Ns > 1) {
-                const double2 w1 = tw[k * (N / (R * Ns))];
-                double2 wp = w1;
+                const double2 *t = stw + k * (R - 1);
 #pragma unroll
-                for (int r = 1; r < R; ++r) {
-                    v[u][r] = cmul_f(v[u][r], wp);
-                    if (r + 1 < R) wp = cmul_f(wp, w1);
-                }
+                for (int r = 1; r < R; ++r) v[u][r] = cmul_f(v[u][r], t[r - 1]);
             }
             dft_small<R>(v[u]);
             const int idx = (b - k) * R + k;
@@ -1606,20 +1662,36 @@ __global__ __launch_bounds__(512) void k_diag_p2(
 {
     using C = P2<N>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double2 *tw = (double2 *)smem;                     // N/2
-    const double *T = T64g;                            // L1/L2-resident, read coalesced
+    double2 *tw = (double2 *)smem;   // [M] post-processing twiddles, then the stage tables
+    const double *T = T64g;          // L1/L2-resident, read coalesced
     const int wpb = blockDim.x >> 6;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    for (int q = threadIdx.x; q < C::M; q += blockDim.x) tw[q] = tw_g[q];
+    for (int q = threadIdx.x; q < C::TW; q += blockDim.x) tw[q] = tw_g[q];
     __syncthreads();
-    unsigned char *wb = smem + (size_t)C::M * 16 + (size_t)wave * C::WAVE_BYTES;
+    unsigned char *wb = smem + (size_t)C::TW * 16 + (size_t)wave * C::WAVE_BYTES;
     float *X = (float *)wb;
     double2 *Cb = (double2 *)wb;   // aliases X after the first FFT stage has read it
     const unsigned P = (unsigned)nsub * (unsigned)nchan;
     const unsigned stride = gridDim.x * wpb;
-
-    for (unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + wave); k < P; k += stride) {
+    // the template stays in registers (N <= 1024), and each wave loads the
+    // next profile's row while it works on the current one: every global load
+    // of the loop is issued ahead of its use (software pipelining)
+    constexpr int NPL = N / 64;
+    constexpr bool TREG = N <= 1024;
+    constexpr bool PREFETCH = N <= 1024;
+    double tv[TREG ? NPL : 1];
+    if (TREG) {
+#pragma unroll
+        for (int u = 0; u < NPL; ++u) tv[u] = T[lane + 64 * u];
+    }
+    float pv[NPL];
+    unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + wave);
+    if (PREFETCH && k < P) {
+#pragma unroll
+        for (int u = 0; u < NPL; ++u) pv[u] = D[(size_t)k * ldD + lane + 64 * u];
+    }
+    for (; k < P; k += stride) {
         const unsigned c = k % (unsigned)nchan;
         const double x = amp[k];
         const int stt = info[k];
@@ -1627,20 +1699,27 @@ __global__ __launch_bounds__(512) void k_diag_p2(
         const float w = w0[k];
         const bool valid = (w != 0.0f);
         const int sh = shift[c];
-        const float *p = D + (size_t)k * ldD;
+        if (!PREFETCH) {
+#pragma unroll
+            for (int u = 0; u < NPL; ++u) pv[u] = D[(size_t)k * ldD + lane + 64 * u];
+        }
         wave_sync();
         // residual -> X (dispersed frame, padded addresses)
-#pragma unroll 4
-        for (int i = lane; i < N; i += 64) {
-            float R = 0.0f;
-            if (ok) {
-                const double u = x * T[i];
-                double e = u - (double)p[i];
-                if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
-                R = (float)e;
-            }
+#pragma unroll
+        for (int u = 0; u < NPL; ++u) {
+            const int i = lane + 64 * u;
+            const double t = TREG ? tv[u] : T[i];
+            const double uu = x * t;
+            double e = uu - (double)pv[u];
+            if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
+            const float R = ok ? (float)e : 0.0f;
             const int j = (i + sh) & (N - 1);
             X[xaddr(j)] = R * w;
+        }
+        if (PREFETCH && k + stride < P) {
+            const float *pn = D + (size_t)(k + stride) * ldD;
+#pragma unroll
+            for (int u = 0; u < NPL; ++u) pv[u] = pn[lane + 64 * u];
         }
         wave_sync();
         double mean = 0.0, sd = 0.0, fftv = 0.0;
@@ -1665,7 +1744,7 @@ __global__ __launch_bounds__(512) void k_diag_p2(
                 for (int q = 1; q < C::CL; ++q) r = r + v[sl][q];
                 fs[sl] = tree_lanes<float, C::ACT>(r);
             }
-            const float s32 = 0.0f + __shfl(tree_slots<float, C::CPL>(fs), 0);
+            const float s32 = 0.0f + tree_slots<float, C::CPL>(fs);
             mean = (double)s32 / (double)N;
             // var: f64 pairwise sum of (f64(X) - mean)^2
             double ds[C::CPL];
@@ -1681,7 +1760,7 @@ __global__ __launch_bounds__(512) void k_diag_p2(
                 }
                 ds[sl] = tree_lanes<double, C::ACT>(r);
             }
-            const double ss = 0.0 + __shfl(tree_slots<double, C::CPL>(ds), 0);
+            const double ss = 0.0 + tree_slots<double, C::CPL>(ds);
             sd = sqrt(ss / (double)N);
             // ptp (NaN-propagating)
             float mx = -INFINITY, mn = INFINITY;
@@ -1697,38 +1776,41 @@ __global__ __launch_bounds__(512) void k_diag_p2(
                         mn = fminf(mn, t);
                     }
             }
-            for (int off = 32; off > 0; off >>= 1) {
-                mx = fmaxf(mx, __shfl_xor(mx, off));
-                mn = fminf(mn, __shfl_xor(mn, off));
-                nan |= __shfl_xor(nan, off);
-            }
+            mx = wave_tree<64>(mx, OpMaxF());
+            mn = wave_tree<64>(mn, OpMinF());
+            nan = wave_tree<64>(nan, OpOr());
             ptp = nan ? NAN : (mx - mn);
             // rFFT of f64(X) - mean: N/2-point complex Stockham, in place
             {
-                int done = 0, Ns = 1;
+                int done = 0, Ns = 1, off = C::M;
                 bool first = true;
                 while (done < C::LG) {
                     const int rem = C::LG - done;
                     if (rem >= 3) {
-                        p2_stage<8, (C::M / 8 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw, lane);
+                        p2_stage<8, (C::M / 8 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw + off, lane);
+                        if (Ns > 1) off += Ns * 7;
                         Ns <<= 3; done += 3;
                     } else if (rem == 2) {
-                        p2_stage<4, (C::M / 4 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw, lane);
+                        p2_stage<4, (C::M / 4 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw + off, lane);
+                        if (Ns > 1) off += Ns * 3;
                         Ns <<= 2; done += 2;
                     } else {
-                        p2_stage<2, (C::M / 2 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw, lane);
+                        p2_stage<2, (C::M / 2 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw + off, lane);
+                        if (Ns > 1) off += Ns;
                         Ns <<= 1; done += 1;
                     }
                     first = false;
                 }
             }
+            // X_k = E_k + w^k O_k, computed as 2 X_k (the 1/2 factors are exact
+            // powers of two, applied once to the maximum)
             double best2 = 0.0;
             int nanf = 0;
             for (int kk = lane; kk <= C::M; kk += 64) {
                 const double2 zk = Cb[cidx(kk == C::M ? 0 : kk)];
                 const double2 zm = Cb[cidx(kk == 0 ? 0 : C::M - kk)];
-                const double er = 0.5 * (zk.x + zm.x), ei = 0.5 * (zk.y - zm.y);
-                const double orr = 0.5 * (zk.y + zm.y), oi = -0.5 * (zk.x - zm.x);
+                const double er = zk.x + zm.x, ei = zk.y - zm.y;
+                const double orr = zk.y + zm.y, oi = zm.x - zk.x;
                 double wr = -1.0, wi = 0.0;
                 if (kk < C::M) {
                     const double2 wv = tw[kk];
@@ -1741,16 +1823,14 @@ __global__ __launch_bounds__(512) void k_diag_p2(
                 nanf |= isnan(a2);
                 best2 = fmax(best2, a2);
             }
-            for (int off = 32; off > 0; off >>= 1) {
-                best2 = fmax(best2, __shfl_xor(best2, off));
-                nanf |= __shfl_xor(nanf, off);
-            }
-            fftv = nanf ? NAN : sqrt(best2);
+            best2 = wave_tree<64>(best2, OpMaxF());
+            nanf = wave_tree<64>(nanf, OpOr());
+            fftv = nanf ? NAN : 0.5 * sqrt(best2);
         } else {
             // invalid: rfft of f64(X) = +-0 -> 0, unless R was non-finite (X NaN)
             int nanx = 0;
             for (int i = lane; i < N; i += 64) nanx |= isnan(X[xaddr(i)]);
-            for (int off = 32; off > 0; off >>= 1) nanx |= __shfl_xor(nanx, off);
+            nanx = wave_tree<64>(nanx, OpOr());
             fftv = nanx ? NAN : 0.0;
         }
         if (lane == 0) {
@@ -2141,20 +2221,20 @@ hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, lo
 
 hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const double *amp,
                        const int32_t *info, const float *w0, const int32_t *shift, const double2 *tw,
-                       const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
+                       const double2 *tw_p2, const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
                        int pr_start, int pr_end, double *std_o, double *mean_o, float *ptp_o,
                        double *fft_o)
 {
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
-        const size_t fixed = (size_t)(NN / 2) * 16;                                                \
+        const size_t fixed = (size_t)P2<NN>::TW * 16;                                               \
         int wpb = 8;                                                                               \
         while (wpb > 1 && fixed + wpb * (size_t)P2<NN>::WAVE_BYTES > 150 * 1024) --wpb;            \
         const size_t shm = fixed + wpb * (size_t)P2<NN>::WAVE_BYTES;                               \
         const size_t P = (size_t)nsub * nchan;                                                     \
         const unsigned grid = (unsigned)std::min<size_t>((P + wpb - 1) / wpb, 4096);               \
         hipLaunchKernelGGL(k_diag_p2<NN>, dim3(grid), dim3(64 * wpb), shm, st, D, T64, amp, info, w0, \
-                           shift, tw, nsub, nchan, ldD, pr_on, pr_factor, pr_start, pr_end, std_o,  \
+                           shift, tw_p2, nsub, nchan, ldD, pr_on, pr_factor, pr_start, pr_end, std_o, \
                            mean_o, ptp_o, fft_o);                                                  \
         return hipGetLastError();                                                                  \
     }

@@ -69,7 +69,7 @@ struct Session {
     int32_t *shift = nullptr, *win = nullptr, *info = nullptr, *counters = nullptr;
     double *part = nullptr, *wpart = nullptr, *T64 = nullptr, *amp = nullptr, *std_ = nullptr,
            *mean = nullptr, *fft = nullptr, *test = nullptr, *lstat = nullptr;
-    double2 *tw = nullptr;
+    double2 *tw = nullptr, *tw_p2 = nullptr;
     PwPlan *plan = nullptr;
     FitStateArrays fs{};
     int32_t *lists = nullptr;   // two active-profile lists of P entries
@@ -148,6 +148,35 @@ int make_plan(int n, PwPlan *pl)
         }                                                                      \
     } while (0)
 
+// Twiddles of k_diag_p2 for nbin = N = 2^k: [M = N/2] exp(-2 pi i q/N) for the
+// real-FFT post-processing, then for every Stockham stage after the first (radix
+// R = 8 while >= 3 levels remain, then 4 or 2; Ns = product of earlier radices)
+// the table w^(r k), w = exp(-2 pi i/(R Ns)), k < Ns, r = 1..R-1, as [k][r-1].
+// Total <= N entries.
+std::vector<double2> p2_twiddles(int N)
+{
+    std::vector<double2> t;
+    if (N < 4 || (N & (N - 1))) return t;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    auto w = [&](long double num, long double den) {
+        const long double a = -2.0L * pi * num / den;
+        return make_double2((double)cosl(a), (double)sinl(a));
+    };
+    const int M = N / 2;
+    for (int q = 0; q < M; ++q) t.push_back(w(q, N));
+    int lg = 0;
+    while ((1 << lg) < M) ++lg;
+    for (int done = 0, Ns = 1; done < lg;) {
+        const int rem = lg - done, R = rem >= 3 ? 8 : (rem == 2 ? 4 : 2);
+        if (Ns > 1)
+            for (int k = 0; k < Ns; ++k)
+                for (int r = 1; r < R; ++r) t.push_back(w((long double)r * k, (long double)R * Ns));
+        Ns *= R;
+        done += R == 8 ? 3 : (R == 4 ? 2 : 1);
+    }
+    return t;
+}
+
 int collect_timing(Session *s)
 {
     if (!s->timing) return 0;
@@ -169,7 +198,7 @@ void free_all(Session *s)
     void *bufs[] = {s->raw,  s->D,     s->w0,   s->W,   s->base, s->base0, s->F,   s->wf,
                     s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
-                    s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount};
+                    s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (s->h_rcount) (void)hipHostFree(s->h_rcount);
@@ -388,6 +417,7 @@ int ic_session_create(const ic_params *params, int device, void **out)
     AL(s->lstat, (size_t)16 * (nchan + nsub));
     AL(s->counters, (size_t)(p.max_iter + 4));
     AL(s->tw, (size_t)nbin);
+    AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     AL(s->lists, 2 * P);
     AL(s->rcount, (size_t)kMaxRounds + 2);
@@ -417,9 +447,12 @@ int ic_session_create(const ic_params *params, int device, void **out)
         const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)q / (long double)nbin;
         tw[q] = make_double2((double)cosl(ang), (double)sinl(ang));
     }
+    const std::vector<double2> tw2 = p2_twiddles(nbin);
     PwPlan plan;
     if (make_plan(nbin, &plan) != 0) return bail(fail(IC_EINVAL, "pairwise plan too large for nbin=%d", nbin));
     if (hipMemcpy(s->tw, tw.data(), sizeof(double2) * nbin, hipMemcpyHostToDevice) != hipSuccess ||
+        (!tw2.empty() &&
+         hipMemcpy(s->tw_p2, tw2.data(), sizeof(double2) * tw2.size(), hipMemcpyHostToDevice) != hipSuccess) ||
         hipMemcpy(s->plan, &plan, sizeof plan, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(IC_EHIP, "upload of constants failed"));
     *out = s;
@@ -525,7 +558,7 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
         if (int rc = iteration_template(s, n_iter)) return rc;
         if (int rc = run_fit(s)) return rc;
         LAUNCH(s, K_DIAG,
-               launch_diag(s->stream, s->D, s->T64, s->amp, s->info, s->w0, s->shift, s->tw, s->plan, nsub,
+               launch_diag(s->stream, s->D, s->T64, s->amp, s->info, s->w0, s->shift, s->tw, s->tw_p2, s->plan, nsub,
                            nchan, nbin, s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, s->std_, s->mean, s->ptp,
                            s->fft));
         LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, la));
