@@ -111,6 +111,7 @@ struct OpOr {
 // part[s][sb][i] = sum_{c in sb, ascending} W[s,c] * x[s,c,i]   (f64, from 0.0)
 // x = ded (base == nullptr) or f32(ded - base[s,c]);  wpart[s][sb] = sum W.
 // One lane per bin; lanes of a wave read 64 consecutive (rotated) bins.
+template <bool BASE>
 __global__ __launch_bounds__(256) void k_chan_partials(
     const float *__restrict__ raw, const float *__restrict__ W, const int32_t *__restrict__ shift,
     const float *__restrict__ base, int nsub, int nchan, int nbin, int nsb,
@@ -124,15 +125,35 @@ __global__ __launch_bounds__(256) void k_chan_partials(
     if (i < nbin) {
         double acc = 0.0;
         const size_t krow = (size_t)s * nchan;
-#pragma unroll 4
-        for (int c = c0; c < c1; ++c) {
+        // batches of 16 channels: all 16 row loads are issued before the
+        // (sequential, canonical-order) accumulation consumes them
+        constexpr int B = 16;
+        int c = c0;
+        for (; c + B <= c1; c += B) {
+            float xv[B], wv[B], bv[B];
+#pragma unroll
+            for (int q = 0; q < B; ++q) {
+                int j = i + shift[c + q];
+                if (j >= nbin) j -= nbin;
+                xv[q] = raw[(krow + c + q) * nbin + j];
+                wv[q] = W[krow + c + q];
+                bv[q] = BASE ? base[krow + c + q] : 0.0f;
+            }
+#pragma unroll
+            for (int q = 0; q < B; ++q) {
+                float x = xv[q];
+                if (BASE) x = x - bv[q];
+                const double t = (double)wv[q] * (double)x;
+                acc = acc + t;
+            }
+        }
+        for (; c < c1; ++c) {
             const size_t k = krow + c;
-            const double w = (double)W[k];
             int j = i + shift[c];
             if (j >= nbin) j -= nbin;
             float x = raw[k * nbin + j];
-            if (base) x = x - base[k];
-            const double t = w * (double)x;
+            if (BASE) x = x - base[k];
+            const double t = (double)W[k] * (double)x;
             acc = acc + t;
         }
         part[((size_t)s * nsb + sb) * nbin + i] = acc;
@@ -1605,27 +1626,27 @@ __device__ __forceinline__ T tree_slots(const T (&v)[CPL])
     else return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));   // CPL == 8
 }
 
-// stw: this stage's twiddles w^(r k), w = exp(-2 pi i/(R Ns)), as [k][r-1]
-// (host-built in long double; no recurrences)
-template <int R, int BPL, int M, int N>
-__device__ __forceinline__ void p2_stage(double2 *C, const float *X, bool first, bool valid, double mu,
-                                         int Ns, const double2 *stw, int lane)
+// One radix-R Stockham stage (compile-time R, NS = product of earlier radices),
+// in place: every input of the stage is in registers before it writes.
+// stw: this stage's twiddles w^(r k), w = exp(-2 pi i/(R NS)), as [k][r-1]
+// (host-built in long double; no recurrences).  FIRST: the input is the real
+// signal X (f32, padded addresses) minus mu, read as complex pairs.
+template <int R, int NS, bool FIRST, int M>
+__device__ __forceinline__ void p2_stage(double2 *C, const float *X, double mu, const double2 *stw, int lane)
 {
     constexpr int NB = M / R;
+    constexpr int BPL = (NB + 63) / 64;
     double2 v[BPL][R];
-    int kk[BPL];
 #pragma unroll
     for (int u = 0; u < BPL; ++u) {
         const int b = lane + 64 * u;
-        kk[u] = b & (Ns - 1);
-        if (b < NB) {
+        if (NB % 64 == 0 || b < NB) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int q = b + r * NB;
-                if (first) {
+                if (FIRST) {
                     const float2 xv = *(const float2 *)(X + xaddr(2 * q));
-                    v[u][r] = valid ? make_double2((double)xv.x - mu, (double)xv.y - mu)
-                                    : make_double2((double)xv.x, (double)xv.y);
+                    v[u][r] = make_double2((double)xv.x - mu, (double)xv.y - mu);
                 } else {
                     v[u][r] = C[cidx(q)];
                 }
@@ -1636,9 +1657,9 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, bool first,
 #pragma unroll
     for (int u = 0; u < BPL; ++u) {
         const int b = lane + 64 * u;
-        if (b < NB) {
-            const int k = kk[u];
-            if (Ns > 1) {
+        if (NB % 64 == 0 || b < NB) {
+            const int k = b & (NS - 1);
+            if (NS > 1) {
                 const double2 *t = stw + k * (R - 1);
 #pragma unroll
                 for (int r = 1; r < R; ++r) v[u][r] = cmul_f(v[u][r], t[r - 1]);
@@ -1646,10 +1667,24 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, bool first,
             dft_small<R>(v[u]);
             const int idx = (b - k) * R + k;
 #pragma unroll
-            for (int r = 0; r < R; ++r) C[cidx(idx + r * Ns)] = v[u][r];
+            for (int r = 0; r < R; ++r) C[cidx(idx + r * NS)] = v[u][r];
         }
     }
     wave_sync();
+}
+
+// the whole N/2-point FFT as a compile-time chain of stages (radix 8 while >= 3
+// levels remain, then 4 or 2); OFF = offset of the next stage table in tw
+template <int M, int LG, int DONE, int NS, int OFF>
+__device__ __forceinline__ void p2_fft(double2 *C, const float *X, double mu, const double2 *tw, int lane)
+{
+    if constexpr (DONE < LG) {
+        constexpr int REM = LG - DONE;
+        constexpr int R = REM >= 3 ? 8 : (REM == 2 ? 4 : 2);
+        constexpr int LR = R == 8 ? 3 : (R == 4 ? 2 : 1);
+        p2_stage<R, NS, DONE == 0, M>(C, X, mu, tw + OFF, lane);
+        p2_fft<M, LG, DONE + LR, NS * R, (NS > 1 ? OFF + NS * (R - 1) : OFF)>(C, X, mu, tw, lane);
+    }
 }
 
 template <int N>
@@ -1781,27 +1816,7 @@ __global__ __launch_bounds__(512) void k_diag_p2(
             nan = wave_tree<64>(nan, OpOr());
             ptp = nan ? NAN : (mx - mn);
             // rFFT of f64(X) - mean: N/2-point complex Stockham, in place
-            {
-                int done = 0, Ns = 1, off = C::M;
-                bool first = true;
-                while (done < C::LG) {
-                    const int rem = C::LG - done;
-                    if (rem >= 3) {
-                        p2_stage<8, (C::M / 8 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw + off, lane);
-                        if (Ns > 1) off += Ns * 7;
-                        Ns <<= 3; done += 3;
-                    } else if (rem == 2) {
-                        p2_stage<4, (C::M / 4 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw + off, lane);
-                        if (Ns > 1) off += Ns * 3;
-                        Ns <<= 2; done += 2;
-                    } else {
-                        p2_stage<2, (C::M / 2 + 63) / 64, C::M, N>(Cb, X, first, true, mean, Ns, tw + off, lane);
-                        if (Ns > 1) off += Ns;
-                        Ns <<= 1; done += 1;
-                    }
-                    first = false;
-                }
-            }
+            p2_fft<C::M, C::LG, 0, 1, C::M>(Cb, X, mean, tw, lane);
             // X_k = E_k + w^k O_k, computed as 2 X_k (the 1/2 factors are exact
             // powers of two, applied once to the maximum)
             double best2 = 0.0;
@@ -2133,8 +2148,12 @@ hipError_t launch_chan_partials(hipStream_t st, const float *raw, const float *W
     const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
     dim3 grid(cdiv(nbin, bs), nsb, nsub);
-    hipLaunchKernelGGL(k_chan_partials, grid, dim3(bs), 0, st, raw, W, shift, base, nsub, nchan, nbin,
-                       nsb, part, wpart);
+    if (base)
+        hipLaunchKernelGGL(k_chan_partials<true>, grid, dim3(bs), 0, st, raw, W, shift, base, nsub, nchan, nbin,
+                           nsb, part, wpart);
+    else
+        hipLaunchKernelGGL(k_chan_partials<false>, grid, dim3(bs), 0, st, raw, W, shift, base, nsub, nchan, nbin,
+                           nsb, part, wpart);
     return hipGetLastError();
 }
 
