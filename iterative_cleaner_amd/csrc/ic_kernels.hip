@@ -1722,39 +1722,67 @@ __global__ __launch_bounds__(512) void k_diag_p2(
     }
     float pv[NPL];
     unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + wave);
-    if (PREFETCH && k < P) {
+    // per-profile scalars, loaded one profile ahead as well
+    double nx = 0.0;
+    int nst = 0, nsh = 0;
+    float nw = 0.0f;
+    if (k < P) {
+        if (PREFETCH) {
 #pragma unroll
-        for (int u = 0; u < NPL; ++u) pv[u] = D[(size_t)k * ldD + lane + 64 * u];
+            for (int u = 0; u < NPL; ++u) pv[u] = D[(size_t)k * ldD + lane + 64 * u];
+        }
+        nx = amp[k];
+        nst = info[k];
+        nw = w0[k];
+        nsh = shift[k % (unsigned)nchan];
     }
     for (; k < P; k += stride) {
-        const unsigned c = k % (unsigned)nchan;
-        const double x = amp[k];
-        const int stt = info[k];
-        const bool ok = stt >= 1 && stt <= 4;
-        const float w = w0[k];
+        const double x = nx;
+        const bool ok = nst >= 1 && nst <= 4;
+        const float w = nw;
         const bool valid = (w != 0.0f);
-        const int sh = shift[c];
+        const int sh = nsh;
         if (!PREFETCH) {
 #pragma unroll
             for (int u = 0; u < NPL; ++u) pv[u] = D[(size_t)k * ldD + lane + 64 * u];
         }
         wave_sync();
         // residual -> X (dispersed frame, padded addresses)
+        if (pr_on) {
 #pragma unroll
-        for (int u = 0; u < NPL; ++u) {
-            const int i = lane + 64 * u;
-            const double t = TREG ? tv[u] : T[i];
-            const double uu = x * t;
-            double e = uu - (double)pv[u];
-            if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
-            const float R = ok ? (float)e : 0.0f;
-            const int j = (i + sh) & (N - 1);
-            X[xaddr(j)] = R * w;
+            for (int u = 0; u < NPL; ++u) {
+                const int i = lane + 64 * u;
+                const double t = TREG ? tv[u] : T[i];
+                const double uu = x * t;
+                double e = uu - (double)pv[u];
+                if (i >= pr_start && i < pr_end) e = e * pr_factor;
+                const float R = ok ? (float)e : 0.0f;
+                const int j = (i + sh) & (N - 1);
+                X[xaddr(j)] = R * w;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < NPL; ++u) {
+                const int i = lane + 64 * u;
+                const double t = TREG ? tv[u] : T[i];
+                const double uu = x * t;
+                const double e = uu - (double)pv[u];
+                const float R = ok ? (float)e : 0.0f;
+                const int j = (i + sh) & (N - 1);
+                X[xaddr(j)] = R * w;
+            }
         }
-        if (PREFETCH && k + stride < P) {
-            const float *pn = D + (size_t)(k + stride) * ldD;
+        if (k + stride < P) {
+            const unsigned kn = k + stride;
+            if (PREFETCH) {
+                const float *pn = D + (size_t)kn * ldD;
 #pragma unroll
-            for (int u = 0; u < NPL; ++u) pv[u] = pn[lane + 64 * u];
+                for (int u = 0; u < NPL; ++u) pv[u] = pn[lane + 64 * u];
+            }
+            nx = amp[kn];
+            nst = info[kn];
+            nw = w0[kn];
+            nsh = shift[kn % (unsigned)nchan];
         }
         wave_sync();
         double mean = 0.0, sd = 0.0, fftv = 0.0;
@@ -1819,24 +1847,30 @@ __global__ __launch_bounds__(512) void k_diag_p2(
             p2_fft<C::M, C::LG, 0, 1, C::M>(Cb, X, mean, tw, lane);
             // X_k = E_k + w^k O_k, computed as 2 X_k (the 1/2 factors are exact
             // powers of two, applied once to the maximum)
+            // k = 0 .. M-1 on all lanes; the Nyquist term k = M (w = -1, Z_M = Z_0)
+            // reduces to (Re 2Z_0 - Im 2Z_0)^2 and is added by lane 0 from k = 0
             double best2 = 0.0;
             int nanf = 0;
-            for (int kk = lane; kk <= C::M; kk += 64) {
-                const double2 zk = Cb[cidx(kk == C::M ? 0 : kk)];
+#pragma unroll 2
+            for (int j = 0; j < (C::M + 63) / 64; ++j) {
+                const int kk = lane + 64 * j;
+                if (C::M % 64 != 0 && kk >= C::M) continue;   // M = 32 (N = 64)
+                const double2 zk = Cb[cidx(kk)];
                 const double2 zm = Cb[cidx(kk == 0 ? 0 : C::M - kk)];
                 const double er = zk.x + zm.x, ei = zk.y - zm.y;
                 const double orr = zk.y + zm.y, oi = zm.x - zk.x;
-                double wr = -1.0, wi = 0.0;
-                if (kk < C::M) {
-                    const double2 wv = tw[kk];
-                    wr = wv.x;
-                    wi = wv.y;
-                }
-                const double re = er + __builtin_fma(orr, wr, -(oi * wi));
-                const double im = ei + __builtin_fma(orr, wi, oi * wr);
+                const double2 wv = tw[kk];
+                const double re = er + __builtin_fma(orr, wv.x, -(oi * wv.y));
+                const double im = ei + __builtin_fma(orr, wv.y, oi * wv.x);
                 const double a2 = __builtin_fma(re, re, im * im);
                 nanf |= isnan(a2);
                 best2 = fmax(best2, a2);
+                if (j == 0 && lane == 0) {
+                    const double rn = er - orr;
+                    const double an = rn * rn;
+                    nanf |= isnan(an);
+                    best2 = fmax(best2, an);
+                }
             }
             best2 = wave_tree<64>(best2, OpMaxF());
             nanf = wave_tree<64>(nanf, OpOr());
