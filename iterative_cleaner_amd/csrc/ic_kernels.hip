@@ -1932,113 +1932,178 @@ __device__ __forceinline__ double unkey64(unsigned long long k)
     return __longlong_as_double((long long)b);
 }
 
-__device__ void bitonic_sort(unsigned long long *a, int N)
+// ---- per-line median / MAD: one wave per line, radix select ------------------
+// Lines: columns (length nsub) of each diagnostic, or rows (length nchan);
+// diag 0 std, 1 mean, 2 ptp (f32 arithmetic), 3 fft (plain: every entry valid).
+// The valid values of the line go to wave-private LDS as order-preserving
+// 64-bit keys (key64), compacted with a ballot.  Order statistics come from a
+// most-significant-digit radix select: 8-bit digits from the highest bit where min and max differ,
+// a 256-bin LDS histogram per digit, the target bin found by a DPP prefix scan.
+// numpy.ma median arithmetic: odd -> 0+mid, even -> ((0+lo)+hi)/2 in the
+// dtype; any NaN -> NaN.
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 {
-    for (int kk = 2; kk <= N; kk <<= 1) {
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < N; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const bool up = (i & kk) == 0;
-                    const unsigned long long x = a[i], y = a[ixj];
-                    if ((x > y) == up) {
-                        a[i] = y;
-                        a[ixj] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = o < v ? o : v;
     }
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
+{
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v)
+{
+    return wave_tree<64>(v, OpAdd());
 }
 
-// median of the cnt smallest keys (sorted ascending), numpy arithmetic in dtype
-__device__ double sorted_median(const unsigned long long *a, int cnt, bool f32)
+// inclusive prefix sum over the 64 lanes (DPP row shifts + row broadcasts)
+__device__ __forceinline__ int wave_incl_scan(int v)
 {
-    const int idx = cnt / 2;
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// r-th smallest (0-based) of keys[0, n): uniform result
+__device__ unsigned long long wave_select(const unsigned long long *keys, int n, int r, unsigned *hist, int lane)
+{
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int j = lane; j < n; j += 64) {
+        const unsigned long long k = keys[j];
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+    lo = wave_min_u64(lo);
+    hi = wave_max_u64(hi);
+    if (lo == hi) return lo;
+    const int top = 63 - __clzll((long long)(lo ^ hi));
+    int shift = (top / 8) * 8;
+    unsigned long long prefix = shift + 8 >= 64 ? 0ull : (lo & (~0ull << (shift + 8)));
+    for (; shift >= 0; shift -= 8) {
+        const unsigned long long hmask = shift + 8 >= 64 ? 0ull : (~0ull << (shift + 8));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hist[lane * 4 + q] = 0u;
+        wave_sync();
+        for (int j = lane; j < n; j += 64) {
+            const unsigned long long k = keys[j];
+            if ((k & hmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+        wave_sync();
+        const uint4 c4 = *(const uint4 *)&hist[lane * 4];
+        const int sl = (int)(c4.x + c4.y + c4.z + c4.w);
+        const int incl = wave_incl_scan(sl);
+        const unsigned long long over = __ballot(incl > r);
+        const int L = __ffsll((long long)over) - 1;   // lane holding the target bin
+        int below = __shfl(incl - sl, L);
+        const uint4 cl = *(const uint4 *)&hist[L * 4];
+        int bin = L * 4;
+        if (r - below >= (int)cl.x) {
+            below += cl.x;
+            ++bin;
+            if (r - below >= (int)cl.y) {
+                below += cl.y;
+                ++bin;
+                if (r - below >= (int)cl.z) {
+                    below += cl.z;
+                    ++bin;
+                }
+            }
+        }
+        r -= below;
+        prefix |= (unsigned long long)bin << shift;
+        wave_sync();
+    }
+    return prefix;
+}
+
+// median of keys[0, n) (n > 0, no NaN), dtype arithmetic
+__device__ double wave_median(const unsigned long long *keys, int n, bool f32, unsigned *hist, int lane)
+{
+    const int idx = n / 2;
+    if (n % 2) {
+        const double m = unkey64(wave_select(keys, n, idx, hist, lane));
+        return f32 ? (double)(0.0f + (float)m) : 0.0 + m;
+    }
+    const unsigned long long klo = wave_select(keys, n, idx - 1, hist, lane);
+    // hi = rank idx: klo again if it is repeated, else the next larger key
+    int le = 0;
+    unsigned long long nxt = ~0ull;
+    for (int j = lane; j < n; j += 64) {
+        const unsigned long long k = keys[j];
+        le += k <= klo;
+        if (k > klo && k < nxt) nxt = k;
+    }
+    le = wave_sum_i(le);
+    nxt = wave_min_u64(nxt);
+    const unsigned long long khi = le > idx ? klo : nxt;
+    const double lo = unkey64(klo), hi = unkey64(khi);
     if (f32) {
-        const float hi = (float)unkey64(a[idx]);
-        if (cnt % 2) return (double)(0.0f + hi);
-        const float lo = (float)unkey64(a[idx - 1]);
-        const float t = (0.0f + lo) + hi;
+        const float t = (0.0f + (float)lo) + (float)hi;
         return (double)(t / 2.0f);
     }
-    const double hi = unkey64(a[idx]);
-    if (cnt % 2) return 0.0 + hi;
-    const double lo = unkey64(a[idx - 1]);
     const double t = (0.0 + lo) + hi;
     return t / 2.0;
 }
 
-// One block per line: lines [0, 4*nchan) are columns (diag = line / nchan),
-// lines [4*nchan, 4*nchan + 4*nsub) rows.  diag 0 std, 1 mean, 2 ptp (f32), 3 fft (plain).
-__global__ __launch_bounds__(256) void k_linestats(LineStatsArgs a)
+__global__ __launch_bounds__(256) void k_linestats(LineStatsArgs a, int rows, int len, int wpb, int per_wave)
 {
-    extern __shared__ unsigned long long keys[];
-    __shared__ int cnt_s, nan_s;
-    const int line = blockIdx.x;
-    const bool col = line < 4 * a.nchan;
-    const int diag = col ? line / a.nchan : (line - 4 * a.nchan) / a.nsub;
-    const int idx = col ? line % a.nchan : (line - 4 * a.nchan) % a.nsub;
-    const int len = col ? a.nsub : a.nchan;
-    const bool f32 = diag == 2;
-    const bool plain = diag == 3;
-    int Npad = 1;
-    while (Npad < len) Npad <<= 1;
-    auto at = [&](int q, bool &v) -> double {
-        const size_t kk = col ? (size_t)q * a.nchan + idx : (size_t)idx * a.nchan + q;
-        v = plain ? true : (a.valid[kk] != 0);
-        if (diag == 0) return a.std_d[kk];
-        if (diag == 1) return a.mean_d[kk];
-        if (diag == 2) return (double)a.ptp_d[kk];
-        return a.fft_d[kk];
-    };
-    // pass 1: valid values
-    if (threadIdx.x == 0) { cnt_s = 0; nan_s = 0; }
-    __syncthreads();
-    for (int q = threadIdx.x; q < Npad; q += blockDim.x) keys[q] = ~0ull;
-    __syncthreads();
-    for (int q = threadIdx.x; q < len; q += blockDim.x) {
-        bool v;
-        const double d = at(q, v);
-        if (v) {
-            const int pos = atomicAdd(&cnt_s, 1);
-            keys[pos] = key64(d);
-            if (isnan(d)) atomicOr(&nan_s, 1);
+    extern __shared__ __attribute__((aligned(16))) unsigned char lsm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int line = blockIdx.x * wpb + wave;
+    const int nl = 4 * (rows ? a.nsub : a.nchan);
+    if (line >= nl || wave >= wpb) return;
+    unsigned *hist = (unsigned *)(lsm + (size_t)wave * per_wave);
+    unsigned long long *keys = (unsigned long long *)(lsm + (size_t)wave * per_wave + 1024);
+    const int nline = rows ? a.nsub : a.nchan;
+    const int diag = line / nline, idx = line % nline;
+    const bool f32 = diag == 2, plain = diag == 3;
+    // gather the valid values (ballot compaction keeps no particular order: the
+    // selection does not need one)
+    int cnt = 0, nan = 0;
+    for (int q0 = 0; q0 < len; q0 += 64) {
+        const int q = q0 + lane;
+        double d = 0.0;
+        bool v = false;
+        if (q < len) {
+            const size_t kk = rows ? (size_t)idx * a.nchan + q : (size_t)q * a.nchan + idx;
+            v = plain ? true : (a.valid[kk] != 0);
+            d = diag == 0 ? a.std_d[kk] : diag == 1 ? a.mean_d[kk] : diag == 2 ? (double)a.ptp_d[kk] : a.fft_d[kk];
         }
+        const unsigned long long m = __ballot(v);
+        if (v) keys[cnt + __popcll(m & ((1ull << lane) - 1ull))] = key64(d);
+        nan |= v && isnan(d);
+        cnt += __popcll(m);
     }
-    __syncthreads();
-    const int cnt = cnt_s;
+    nan = __any(nan);
+    wave_sync();
     double med = NAN, mad = NAN;
-    if (cnt > 0 && !nan_s) {
-        bitonic_sort(keys, Npad);
-        med = sorted_median(keys, cnt, f32);
-        __syncthreads();
-        // pass 2: |d - med| over valid entries (in dtype)
-        if (threadIdx.x == 0) { cnt_s = 0; nan_s = 0; }
-        __syncthreads();
-        for (int q = threadIdx.x; q < Npad; q += blockDim.x) keys[q] = ~0ull;
-        __syncthreads();
-        for (int q = threadIdx.x; q < len; q += blockDim.x) {
-            bool v;
-            const double d = at(q, v);
-            if (v) {
-                double r;
-                if (f32) r = (double)fabsf((float)d - (float)med);
-                else r = fabs(d - med);
-                const int pos = atomicAdd(&cnt_s, 1);
-                keys[pos] = key64(r);
-                if (isnan(r)) atomicOr(&nan_s, 1);
-            }
+    if (cnt > 0 && !nan) {
+        med = wave_median(keys, cnt, f32, hist, lane);
+        // |d - med| in the dtype, in place
+        int rnan = 0;
+        for (int j = lane; j < cnt; j += 64) {
+            const double d = unkey64(keys[j]);
+            const double r = f32 ? (double)fabsf((float)d - (float)med) : fabs(d - med);
+            rnan |= isnan(r);
+            keys[j] = key64(r);
         }
-        __syncthreads();
-        if (!nan_s) {
-            bitonic_sort(keys, Npad);
-            mad = sorted_median(keys, cnt, f32);
-        }
+        rnan = __any(rnan);
+        wave_sync();
+        if (!rnan) mad = wave_median(keys, cnt, f32, hist, lane);
     }
-    if (threadIdx.x == 0) {
-        if (col) {
+    if (lane == 0) {
+        if (!rows) {
             a.col_med[diag * a.nchan + idx] = med;
             a.col_mad[diag * a.nchan + idx] = mad;
         } else {
@@ -2308,20 +2373,25 @@ hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const 
     return hipGetLastError();
 }
 
-static int next_pow2(int v)
-{
-    int p = 1;
-    while (p < v) p <<= 1;
-    return p;
-}
 
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a)
 {
-    const int Npad = next_pow2(a.nsub > a.nchan ? a.nsub : a.nchan);
-    const size_t shm = (size_t)Npad * 8;
-    const unsigned lines = 4u * (unsigned)(a.nchan + a.nsub);
-    hipLaunchKernelGGL(k_linestats, dim3(lines), dim3(256), shm, st, a);
-    return hipGetLastError();
+    // columns (length nsub), then rows (length nchan); wave-private LDS:
+    // 256-bin histogram + the line's keys
+    for (int rows = 0; rows < 2; ++rows) {
+        const int len = rows ? a.nchan : a.nsub;
+        const int per_wave = 1024 + ((len * 8 + 15) / 16) * 16;
+        int wpb = 4;
+        while (wpb > 1 && (size_t)wpb * per_wave > 64 * 1024) --wpb;
+        const size_t shm = (size_t)wpb * per_wave;
+        if (shm > 160 * 1024) return hipErrorInvalidValue;
+        const int lines = 4 * (rows ? a.nsub : a.nchan);
+        hipLaunchKernelGGL(k_linestats, dim3(cdiv(lines, wpb)), dim3(64 * wpb), shm, st, a, rows, len, wpb,
+                           per_wave);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const float *w0,
