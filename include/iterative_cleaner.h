@@ -113,6 +113,8 @@ typedef struct {
     int32_t fit_rounds;          /* k_fit_pass launches, summed over iterations    */
     int64_t fit_profile_sweeps;  /* profiles swept by k_fit_pass, summed (x nbin x 4 B = fit bytes) */
     int64_t fit_tail_sweeps;     /* profile sweeps done by k_fit_tail (the last few thousand profiles) */
+    int32_t window_moves;        /* subint baseline windows that moved between iterations */
+    int32_t reserved;
 } ic_run_stats;
 int ic_get_run_stats(void *session, ic_run_stats *out);
 

@@ -35,7 +35,8 @@ class Params(C.Structure):
 
 class RunStats(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("fit_rounds", C.c_int32),
-                ("fit_profile_sweeps", C.c_int64), ("fit_tail_sweeps", C.c_int64)]
+                ("fit_profile_sweeps", C.c_int64), ("fit_tail_sweeps", C.c_int64),
+                ("window_moves", C.c_int32), ("reserved", C.c_int32)]
 
 
 class KernelTime(C.Structure):
@@ -214,7 +215,8 @@ class GpuSession:
         self._check(self.lib.ic_get_run_stats(self.h, C.byref(st)), "ic_get_run_stats")
         return dict(iterations=st.iterations, fit_rounds=st.fit_rounds,
                     fit_profile_sweeps=int(st.fit_profile_sweeps),
-                    fit_tail_sweeps=int(st.fit_tail_sweeps))
+                    fit_tail_sweeps=int(st.fit_tail_sweeps),
+                    window_moves=int(st.window_moves))
 
     def kernel_times(self):
         buf = (KernelTime * 32)()

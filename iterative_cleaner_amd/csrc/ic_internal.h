@@ -59,13 +59,17 @@ struct LineStatsArgs {
 };
 
 // ---- launch wrappers (ic_kernels.hip); all asynchronous on `st` ----
-hipError_t launch_chan_partials(hipStream_t st, const float *raw, const float *W, const int32_t *shift,
-                                const float *base, int nsub, int nchan, int nbin, double *part,
-                                double *wpart);
+// mode 0: part = sum W*ded; 1: part2 = sum W*f32(ded-base) + wpart; 2: both.
+// flags: only subints with flags[s] != 0 (nullptr: all)
+hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, const float *W, const int32_t *shift,
+                                const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
+                                double *part, double *part2, double *wpart);
+// flags != nullptr: flags[s] = window of subint s moved (win updated in place)
 hipError_t launch_window(hipStream_t st, const double *part, int nsub, int nsb, int nbin, int width,
-                         int32_t *win);
+                         int32_t *win, int32_t *flags);
+// flags != nullptr: only subints with flags[s] != 0
 hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, const int32_t *win,
-                       int nsub, int nchan, int nbin, int width, float *base);
+                       const int32_t *flags, int nsub, int nchan, int nbin, int width, float *base);
 hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
                           int nsub, int nchan, int nbin, int ldD, float *D);
 hipError_t launch_fscrunch(hipStream_t st, const double *part, const double *wpart, int nsub, int nsb,

@@ -111,19 +111,26 @@ struct OpOr {
 // part[s][sb][i] = sum_{c in sb, ascending} W[s,c] * x[s,c,i]   (f64, from 0.0)
 // x = ded (base == nullptr) or f32(ded - base[s,c]);  wpart[s][sb] = sum W.
 // One lane per bin; lanes of a wave read 64 consecutive (rotated) bins.
-template <bool BASE>
+// Canonical-order channel partial sums over one super-block, lane per bin:
+//   MODE 0: part  = sum_c W*ded                     (baseline window total)
+//   MODE 1: part2 = sum_c W*f32(ded - base), wpart  (fscrunch)
+//   MODE 2: both, in one read of the cube (base = the previous iteration's)
+// flags != nullptr: only subints with flags[s] != 0 (a moved window) run.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_chan_partials(
     const float *__restrict__ raw, const float *__restrict__ W, const int32_t *__restrict__ shift,
-    const float *__restrict__ base, int nsub, int nchan, int nbin, int nsb,
-    double *__restrict__ part, double *__restrict__ wpart)
+    const float *__restrict__ base, const int32_t *__restrict__ flags, int nsub, int nchan, int nbin, int nsb,
+    double *__restrict__ part, double *__restrict__ part2, double *__restrict__ wpart)
 {
+    constexpr bool A = MODE != 1, F = MODE != 0;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int sb = blockIdx.y;
     const int s = blockIdx.z;
+    if (flags && flags[s] == 0) return;
     const int c0 = sb * kSuperBlock;
     const int c1 = min(c0 + kSuperBlock, nchan);
     if (i < nbin) {
-        double acc = 0.0;
+        double acc = 0.0, acc2 = 0.0;
         const size_t krow = (size_t)s * nchan;
         // batches of 16 channels: all 16 row loads are issued before the
         // (sequential, canonical-order) accumulation consumes them
@@ -137,28 +144,28 @@ __global__ __launch_bounds__(256) void k_chan_partials(
                 if (j >= nbin) j -= nbin;
                 xv[q] = raw[(krow + c + q) * nbin + j];
                 wv[q] = W[krow + c + q];
-                bv[q] = BASE ? base[krow + c + q] : 0.0f;
+                bv[q] = F ? base[krow + c + q] : 0.0f;
             }
 #pragma unroll
             for (int q = 0; q < B; ++q) {
-                float x = xv[q];
-                if (BASE) x = x - bv[q];
-                const double t = (double)wv[q] * (double)x;
-                acc = acc + t;
+                const double w = (double)wv[q];
+                if (A) acc = acc + w * (double)xv[q];
+                if (F) acc2 = acc2 + w * (double)(xv[q] - bv[q]);
             }
         }
         for (; c < c1; ++c) {
             const size_t k = krow + c;
             int j = i + shift[c];
             if (j >= nbin) j -= nbin;
-            float x = raw[k * nbin + j];
-            if (BASE) x = x - base[k];
-            const double t = (double)W[k] * (double)x;
-            acc = acc + t;
+            const float x = raw[k * nbin + j];
+            const double w = (double)W[k];
+            if (A) acc = acc + w * (double)x;
+            if (F) acc2 = acc2 + w * (double)(x - base[k]);
         }
-        part[((size_t)s * nsb + sb) * nbin + i] = acc;
+        if (A) part[((size_t)s * nsb + sb) * nbin + i] = acc;
+        if (F) part2[((size_t)s * nsb + sb) * nbin + i] = acc2;
     }
-    if (wpart && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (F && blockIdx.x == 0 && threadIdx.x == 0) {
         double a = 0.0;
         for (int c = c0; c < c1; ++c) a = a + (double)W[(size_t)s * nchan + c];
         wpart[(size_t)s * nsb + sb] = a;
@@ -180,8 +187,9 @@ __device__ __forceinline__ bool argmin_better(double va, int ia, double vb, int 
 
 // One block per subint: tot[i] = sum_sb part; m[j] = sum_{k<width} tot[(j+k)%n];
 // win[s] = first argmin.
+// flags != nullptr: flags[s] = (window moved), win[s] updated in place
 __global__ __launch_bounds__(256) void k_window(const double *__restrict__ part, int nsb, int nbin,
-                                                int width, int32_t *__restrict__ win)
+                                                int width, int32_t *__restrict__ win, int32_t *__restrict__ flags)
 {
     extern __shared__ double sh[];
     double *tot = sh;                       // nbin
@@ -222,7 +230,14 @@ __global__ __launch_bounds__(256) void k_window(const double *__restrict__ part,
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) win[s] = bi[0];
+    if (threadIdx.x == 0) {
+        if (flags) {
+            const int moved = win[s] != bi[0];
+            flags[s] = moved;
+            if (moved) atomicAdd(&flags[gridDim.x], 1);   // flags[nsub]: moves counter
+        }
+        win[s] = bi[0];
+    }
 }
 
 // base[k] = f32( (sum_{t<width} f64(ded[(win+t)%n])) / width ), sequential in t.
@@ -239,13 +254,14 @@ __global__ __launch_bounds__(256) void k_window(const double *__restrict__ part,
 // Otherwise (rare: values spanning > 2^21, or Inf/NaN) the wave walks the
 // window in order.
 __global__ __launch_bounds__(256) void k_base(const float *__restrict__ raw, const int32_t *__restrict__ shift,
-                                              const int32_t *__restrict__ win, int nsub, int nchan,
-                                              int nbin, int width, float *__restrict__ base)
+                                              const int32_t *__restrict__ win, const int32_t *__restrict__ flags,
+                                              int nsub, int nchan, int nbin, int width, float *__restrict__ base)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long P = (long)nsub * nchan;
     const int lgw = 32 - __clz(max(width - 1, 1));   // ceil(log2(width)), >= 1
     for (long k = (long)blockIdx.x * 4 + wave; k < P; k += (long)gridDim.x * 4) {
+        if (flags && flags[k / nchan] == 0) continue;   // window unchanged: base unchanged
         int q0 = win[k / nchan] + shift[k % nchan];
         if (q0 >= nbin) q0 -= nbin;
         const float *row = raw + (size_t)k * nbin;
@@ -2240,36 +2256,39 @@ __global__ __launch_bounds__(256) void k_combine(
 
 static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
-hipError_t launch_chan_partials(hipStream_t st, const float *raw, const float *W, const int32_t *shift,
-                                const float *base, int nsub, int nchan, int nbin, double *part,
-                                double *wpart)
+hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, const float *W, const int32_t *shift,
+                                const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
+                                double *part, double *part2, double *wpart)
 {
     const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
     dim3 grid(cdiv(nbin, bs), nsb, nsub);
-    if (base)
-        hipLaunchKernelGGL(k_chan_partials<true>, grid, dim3(bs), 0, st, raw, W, shift, base, nsub, nchan, nbin,
-                           nsb, part, wpart);
+    if (mode == 0)
+        hipLaunchKernelGGL(k_chan_partials<0>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin,
+                           nsb, part, part2, wpart);
+    else if (mode == 1)
+        hipLaunchKernelGGL(k_chan_partials<1>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin,
+                           nsb, part, part2, wpart);
     else
-        hipLaunchKernelGGL(k_chan_partials<false>, grid, dim3(bs), 0, st, raw, W, shift, base, nsub, nchan, nbin,
-                           nsb, part, wpart);
+        hipLaunchKernelGGL(k_chan_partials<2>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin,
+                           nsb, part, part2, wpart);
     return hipGetLastError();
 }
 
 hipError_t launch_window(hipStream_t st, const double *part, int nsub, int nsb, int nbin, int width,
-                         int32_t *win)
+                         int32_t *win, int32_t *flags)
 {
     const size_t shm = (size_t)nbin * 8 + 256 * 8 + 256 * 4;
-    hipLaunchKernelGGL(k_window, dim3(nsub), dim3(256), shm, st, part, nsb, nbin, width, win);
+    hipLaunchKernelGGL(k_window, dim3(nsub), dim3(256), shm, st, part, nsb, nbin, width, win, flags);
     return hipGetLastError();
 }
 
-hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, const int32_t *win,
+hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, const int32_t *win, const int32_t *flags,
                        int nsub, int nchan, int nbin, int width, float *base)
 {
     const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
-    hipLaunchKernelGGL(k_base, dim3(grid), dim3(256), 0, st, raw, shift, win, nsub, nchan, nbin, width, base);
+    hipLaunchKernelGGL(k_base, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
     return hipGetLastError();
 }
 

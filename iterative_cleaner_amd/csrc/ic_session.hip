@@ -66,8 +66,8 @@ struct Session {
     float *raw = nullptr, *D = nullptr, *w0 = nullptr, *W = nullptr, *base = nullptr, *base0 = nullptr;
     float *F = nullptr, *wf = nullptr, *T = nullptr, *ptp = nullptr, *hist = nullptr;
     uint8_t *valid = nullptr;
-    int32_t *shift = nullptr, *win = nullptr, *info = nullptr, *counters = nullptr;
-    double *part = nullptr, *wpart = nullptr, *T64 = nullptr, *amp = nullptr, *std_ = nullptr,
+    int32_t *shift = nullptr, *win = nullptr, *wflag = nullptr, *info = nullptr, *counters = nullptr;
+    double *part = nullptr, *part2 = nullptr, *wpart = nullptr, *T64 = nullptr, *amp = nullptr, *std_ = nullptr,
            *mean = nullptr, *fft = nullptr, *test = nullptr, *lstat = nullptr;
     double2 *tw = nullptr, *tw_p2 = nullptr;
     PwPlan *plan = nullptr;
@@ -198,7 +198,8 @@ void free_all(Session *s)
     void *bufs[] = {s->raw,  s->D,     s->w0,   s->W,   s->base, s->base0, s->F,   s->wf,
                     s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
-                    s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2};
+                    s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
+                    s->wflag};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (s->h_rcount) (void)hipHostFree(s->h_rcount);
@@ -222,7 +223,9 @@ __global__ void k_valid(const float *w0, uint8_t *valid, float *W, float *hist0,
     }
 }
 
-// fit-cube preparation (iterative_cleaner.py:96-100): baseline with w0, dedisperse
+// fit-cube preparation (iterative_cleaner.py:96-100): baseline with w0, dedisperse.
+// The w0 baseline (window + per-profile levels) is also the template stage's
+// baseline of the first iteration (W == w0).
 int prepare(Session *s)
 {
     const int nsub = s->p.nsub, nchan = s->p.nchan, nbin = s->p.nbin;
@@ -230,33 +233,44 @@ int prepare(Session *s)
                        s->valid, s->W, s->hist, s->P);
     CK(hipGetLastError());
     LAUNCH(s, K_CHAN_PARTIALS,
-           launch_chan_partials(s->stream, s->raw, s->w0, s->shift, nullptr, nsub, nchan, nbin, s->part,
-                                nullptr));
-    LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win));
-    LAUNCH(s, K_BASE, launch_base(s->stream, s->raw, s->shift, s->win, nsub, nchan, nbin, s->width, s->base0));
+           launch_chan_partials(s->stream, 0, s->raw, s->w0, s->shift, nullptr, nullptr, nsub, nchan, nbin, s->part,
+                                nullptr, nullptr));
+    LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win, nullptr));
+    LAUNCH(s, K_BASE,
+           launch_base(s->stream, s->raw, s->shift, s->win, nullptr, nsub, nchan, nbin, s->width, s->base0));
     LAUNCH(s, K_FITCUBE, launch_fitcube(s->stream, s->raw, s->shift, s->base0, nsub, nchan, nbin, s->ldD, s->D));
+    CK(hipMemcpyAsync(s->base, s->base0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
+    CK(hipMemsetAsync(s->wflag + nsub, 0, sizeof(int32_t), s->stream));
     return 0;
 }
 
+// Template of iteration `iter` (iterative_cleaner.py:88-94): remove_baseline
+// with the current weights W, dedisperse, fscrunch, tscrunch.  The baseline
+// level of a profile depends on W only through its subint's window (the window
+// position is the argmin over the W-weighted total; the level is the raw
+// window mean), so s->base/s->win carry over between iterations: one read of
+// the cube computes the W-weighted total AND the fscrunch partials with the
+// carried baseline; subints whose window moved get their levels and partials
+// recomputed (flagged launches that are empty when nothing moved).
 int iteration_template(Session *s, int iter)
 {
     const int nsub = s->p.nsub, nchan = s->p.nchan, nbin = s->p.nbin;
-    // remove_baseline with the current weights (template stage).  In the first
-    // iteration W == w0, so the baseline is exactly prepare()'s base0.
-    const float *base = s->base0;
-    if (iter > 1) {
+    if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s
         LAUNCH(s, K_CHAN_PARTIALS,
-               launch_chan_partials(s->stream, s->raw, s->W, s->shift, nullptr, nsub, nchan, nbin, s->part,
-                                    nullptr));
-        LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win));
-        LAUNCH(s, K_BASE, launch_base(s->stream, s->raw, s->shift, s->win, nsub, nchan, nbin, s->width, s->base));
-        base = s->base;
+               launch_chan_partials(s->stream, 1, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
+                                    nullptr, s->part2, s->wpart));
+    } else {
+        LAUNCH(s, K_CHAN_PARTIALS,
+               launch_chan_partials(s->stream, 2, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
+                                    s->part, s->part2, s->wpart));
+        LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win, s->wflag));
+        LAUNCH(s, K_BASE,
+               launch_base(s->stream, s->raw, s->shift, s->win, s->wflag, nsub, nchan, nbin, s->width, s->base));
+        LAUNCH(s, K_CHAN_PARTIALS,
+               launch_chan_partials(s->stream, 1, s->raw, s->W, s->shift, s->base, s->wflag, nsub, nchan, nbin,
+                                    nullptr, s->part2, s->wpart));
     }
-    // dedisperse + fscrunch + tscrunch
-    LAUNCH(s, K_CHAN_PARTIALS,
-           launch_chan_partials(s->stream, s->raw, s->W, s->shift, base, nsub, nchan, nbin, s->part,
-                                s->wpart));
-    LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->part, s->wpart, nsub, s->nsb, nbin, s->F, s->wf));
+    LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->part2, s->wpart, nsub, s->nsb, nbin, s->F, s->wf));
     LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64));
     return 0;
 }
@@ -398,7 +412,9 @@ int ic_session_create(const ic_params *params, int device, void **out)
     AL(s->valid, P);
     AL(s->shift, (size_t)nchan);
     AL(s->win, (size_t)nsub);
+    AL(s->wflag, (size_t)nsub + 1);   // + window-moves counter
     AL(s->part, (size_t)nsub * s->nsb * nbin);
+    AL(s->part2, (size_t)nsub * s->nsb * nbin);
     AL(s->wpart, (size_t)nsub * s->nsb);
     AL(s->F, (size_t)nsub * nbin);
     AL(s->wf, (size_t)nsub);
@@ -586,6 +602,11 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
     if (weights_out)
         CK(hipMemcpyAsync(weights_out, s->W, sizeof(float) * s->P, hipMemcpyDeviceToHost, s->stream));
     CK(hipStreamSynchronize(s->stream));
+    {
+        int32_t moves = 0;
+        CK(hipMemcpy(&moves, s->wflag + nsub, sizeof moves, hipMemcpyDeviceToHost));
+        s->stats.window_moves = moves;
+    }
     if (int rc = collect_timing(s)) return rc;
     if (loops_out) *loops_out = loops;
     if (n_iter_out) *n_iter_out = n_iter;
