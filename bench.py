@@ -112,7 +112,7 @@ def pmc_traffic(workload, kernel):
     sys.path.insert(0, os.path.join(REPO, "tools"))
     from pmc_traffic import source_sha
     sha = source_sha()
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")), reverse=True):
         with open(path) as f:
             rec = json.load(f)
         if rec.get("workload") == workload and rec.get("source_sha") == sha and kernel in rec["kernels"]:
