@@ -7,10 +7,15 @@ max_iter) over one synthetic archive already resident in HBM.  Default
 workload: configs[1] of BASELINE.json, a LOFAR HBA-like archive
 360 subint x 3200 chan x 1024 bin, default thresholds, max_iter 5.
 
-Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): this workload
-is "replicas only" (SURVEY.md §8(e)): every rank cleans its own archive, no
-collective on the data path; value = all ranks' profiles / max-over-ranks
-time (weak scaling).
+Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): the default
+workload at N > 1 is configs[2], the large archive C3 = 1024 x 8192 x 1024,
+channel-sharded across the N ranks: each rank cleans its
+channel slice in a libicgpu shard session that exchanges template roots,
+diagnostics rows, row statistics and convergence counters over RCCL/xGMI
+(torch.distributed "nccl" through dist.TorchComm); value = C3 profiles x
+steps / max-over-ranks time (strong scaling: total work fixed).
+``--workload C3`` at N = 1 is the unsharded 1-GPU reference point of that
+curve; ``--workload C2`` at N > 1 runs independent replicas (weak scaling).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
 ``roofline`` for the dominant kernel (HIP events on the session stream) and
@@ -37,9 +42,11 @@ WORKLOADS = {
     # name: (nsub, nchan, nbin, seed, rfi_frac)
     "C1": (64, 256, 256, 0, 0.05),
     "C2": (360, 3200, 1024, 1, 0.05),
+    "C3": (1024, 8192, 1024, 2, 0.05),
     "C4": (128, 1024, 512, 1000, 0.05),
     "C5": (256, 1024, 4096, 5, 0.30),
 }
+BLOCKWISE = {"C3"}   # generated per 256-channel block: any channel shard builds its slice alone
 
 
 def make_cube_device(nsub, nchan, nbin, seed, rfi, device):
@@ -75,6 +82,47 @@ def make_cube_device(nsub, nchan, nbin, seed, rfi, device):
     n_dead = int(round(0.02 * nchan))
     if n_dead:
         w0[:, torch.randperm(nchan, generator=g, device=device)[:n_dead]] = 0.0
+    return cube.contiguous(), w0.contiguous(), shift.contiguous()
+
+
+def make_block_cube_device(nsub, nchan, nbin, seed, rfi, c0, c1, device):
+    """Channels [c0, c1) of a SURVEY.md §8(d) synthetic archive whose every
+    256-channel block has its own generator (seed, block): the cube is the same
+    whichever way it is sharded.  Impulsive-RFI subints are drawn once per
+    archive.  Returns (cube [nsub][c1-c0][nbin], w0, shift) on `device`."""
+    import torch
+    f32, f64 = torch.float32, torch.float64
+    phase = (torch.arange(nbin, device=device, dtype=f64) + 0.5) / nbin
+    pulse = torch.exp(-0.5 * ((phase - 0.3) / 0.02) ** 2)
+    g0 = torch.Generator(device=device)
+    g0.manual_seed(seed * 1000003 + 999983)
+    n_imp = int(round(rfi * nsub))
+    imp = torch.randperm(nsub, generator=g0, device=device)[:n_imp]
+    cube = torch.empty((nsub, c1 - c0, nbin), device=device, dtype=f32)
+    w0 = torch.ones((nsub, c1 - c0), device=device, dtype=f32)
+    shift = (torch.arange(c0, c1, device=device) % 7).to(torch.int32)
+    for b0 in range(c0 - c0 % 256, c1, 256):
+        lo, hi = max(b0, c0), min(b0 + 256, nchan, c1)
+        nb = min(b0 + 256, nchan) - b0
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 1000003 + b0 // 256)
+        sh = (torch.arange(b0, b0 + nb, device=device) % 7).long()
+        idx = (torch.arange(nbin, device=device)[None, :] - sh[:, None]) % nbin
+        u = torch.rand((2, nsub, nb), generator=g, device=device, dtype=f64)
+        gain = (0.5 * (-torch.log1p(-u[0]) - torch.log1p(-u[1]))).to(f32)
+        blk = torch.randn((nsub, nb, nbin), generator=g, device=device, dtype=f32)
+        blk += gain[:, :, None] * pulse[idx].to(f32)[None]
+        nbm = torch.rand(nb, generator=g, device=device) < rfi
+        nu = 1.0 + 19.0 * torch.rand(nb, generator=g, device=device, dtype=f64)
+        amp = 5.0 * torch.randn((nsub, nb), generator=g, device=device, dtype=f64)
+        wave = torch.sin(2.0 * math.pi * nu[:, None] * phase[None, :])
+        blk += torch.where(nbm[None, :, None], amp[:, :, None] * wave[None], 0.0).to(f32)
+        if n_imp:
+            hits = torch.rand((n_imp, nb, nbin), generator=g, device=device) < 0.01
+            blk[imp] += hits.to(f32) * 20.0
+        dead = torch.rand(nb, generator=g, device=device) < 0.02
+        cube[:, lo - c0:hi - c0] = blk[:, lo - b0:hi - b0]
+        w0[:, lo - c0:hi - c0] = torch.where(dead[lo - b0:hi - b0], 0.0, 1.0)[None].to(f32)
     return cube.contiguous(), w0.contiguous(), shift.contiguous()
 
 
@@ -156,31 +204,52 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="default: C2 on one GPU, C3 channel-sharded on several")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=30.0)
     ap.add_argument("--kernel-report", action="store_true", help="print per-kernel times to stderr")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the channel-shard session even on one GPU (one-rank RCCL group)")
     a = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
     from iterative_cleaner_amd import _native
-    from iterative_cleaner_amd.dist import max_over_ranks, rank_world
+    from iterative_cleaner_amd.dist import TorchComm, max_over_ranks, rank_world
 
     rank, world, local = rank_world()
     if world != a.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
+    workload = a.workload or ("C2" if world == 1 else "C3")
+    sharded = (world > 1 and workload in BLOCKWISE) or a.sharded
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    elif sharded:
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
 
-    nsub, nchan, nbin, seed, rfi = WORKLOADS[a.workload]
-    cube, w0, shift = make_cube_device(nsub, nchan, nbin, seed + 7919 * rank, rfi, dev)
+    nsub, nchan, nbin, seed, rfi = WORKLOADS[workload]
+    P_total = nsub * nchan
+    if sharded:
+        chans, _ = _native.shard_layout(nsub, nchan, world)
+        c0, c1 = chans[rank]
+        cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, c0, c1, dev)
+        comm = TorchComm(dev)
+        sess = _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm, max_iter=5, device=local)
+        per_rank_P = nsub * (c1 - c0)
+    else:
+        if workload in BLOCKWISE:
+            cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, 0, nchan, dev)
+        else:
+            cube, w0, shift = make_cube_device(nsub, nchan, nbin, seed + 7919 * rank, rfi, dev)
+        sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local)
+        per_rank_P = P_total
+        if world > 1:
+            P_total = P_total * world          # replicas: every rank cleans its own archive
     torch.cuda.synchronize()
-    P = nsub * nchan
-    sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local)
     sess.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
     del cube
     torch.cuda.empty_cache()
@@ -209,13 +278,15 @@ def main():
     sess.close()
 
     if rank == 0:
+        lnchan = sess.shape[1]                 # this rank's channels (kernel byte counts)
         ms_step = 1000.0 * elapsed / a.steps
-        value = a.steps * P * world / elapsed
-        total_k = sum(v["ms"] for v in ktimes.values())
-        dom = max(ktimes, key=lambda k: ktimes[k]["ms"])
-        dk = ktimes[dom]
+        value = a.steps * P_total / elapsed
+        kernels = {k: v for k, v in ktimes.items() if k.startswith("k_")}
+        total_k = sum(v["ms"] for v in kernels.values())
+        dom = max(kernels, key=lambda k: kernels[k]["ms"])
+        dk = kernels[dom]
         avg_s = dk["ms"] / 1000.0 / max(1, dk["launches"])
-        total_bytes = algorithmic_bytes(dom, nsub, nchan, nbin, dk["launches"], stats, a.steps)
+        total_bytes = algorithmic_bytes(dom, nsub, lnchan, nbin, dk["launches"], stats, a.steps)
         bytes_launch = total_bytes / max(1, dk["launches"]) if total_bytes else None
         achieved = bytes_launch / avg_s / 1e9 if bytes_launch else None
         roof = {"bound": "hbm", "kernel": dom,
@@ -229,33 +300,41 @@ def main():
         for kname, kv in ktimes.items():
             if kv["launches"] == 0:
                 continue
-            tb = algorithmic_bytes(kname, nsub, nchan, nbin, kv["launches"], stats, a.steps)
+            tb = algorithmic_bytes(kname, nsub, lnchan, nbin, kv["launches"], stats, a.steps)
             per_kernel[kname] = {"ms_per_step": round(kv["ms"] / a.steps, 3),
                                  "launches_per_step": kv["launches"] // a.steps,
                                  "gbs": round(tb / (kv["ms"] / 1000.0) / 1e9, 1) if tb else None}
-        traffic, src = pmc_traffic(a.workload, dom)
+        traffic, src = pmc_traffic(workload if not sharded else "%s/%d" % (workload, world), dom)
         roof["traffic"] = traffic
         roof["traffic_source"] = src if traffic else "no PMC summary for these HIP sources"
         roof["per_kernel"] = per_kernel
-        iter_bytes = 8 * P * nbin + 64 * P    # SURVEY §8(d) B_iter
+        iter_bytes = 8 * per_rank_P * nbin + 64 * per_rank_P    # SURVEY §8(d) B_iter, one GPU's share
         loop_gbs = iter_bytes * n_iter / (elapsed / a.steps) / 1e9
+        if sharded:
+            parallelism = "channel-sharded x%d (RCCL: 2 all-gathers, 1 all-to-all, 1 all-gather, " \
+                          "1 all-reduce per iteration)" % world
+        else:
+            parallelism = "replicas" if world > 1 else "single"
         rec = {
             "metric": "profiles cleaned/sec (whole node)", "value": round(value, 1),
             "unit": "profiles/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": "%s %dx%dx%d (nsub x nchan x nbin), max_iter 5, thresholds 5/5,"
-                                   " exact leastsq fit" % (a.workload, nsub, nchan, nbin),
-                       "profiles_per_archive": P, "loops": loops[-1], "iterations": n_iter,
+                                   " exact leastsq fit" % (workload, nsub, nchan, nbin),
+                       "profiles_per_archive": nsub * nchan, "loops": loops[-1], "iterations": n_iter,
                        "fit_rounds": stats["fit_rounds"],
                        "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"])
-                                                       / P / max(1, n_iter), 2),
+                                                       / per_rank_P / max(1, n_iter), 2),
                        "fit_tail_sweeps": stats["fit_tail_sweeps"] // max(1, n_iter),
-                       "parallelism": "replicas" if world > 1 else "single",
-                       "loop_hbm_gbs": round(loop_gbs, 1),
+                       "parallelism": parallelism,
+                       "loop_hbm_gbs_per_gpu": round(loop_gbs, 1),
                        "loop_hbm_frac": round(loop_gbs / HBM_PEAK_GBS, 4)},
             "roofline": roof,
         }
+        if "exchange" in ktimes and ktimes["exchange"]["launches"]:
+            rec["config"]["exchange_ms_per_step"] = round(ktimes["exchange"]["ms"] / a.steps, 3)
         if world == 1 and not a.no_cpu_baseline:
             try:
                 rec["cpu_baseline"] = cpu_baseline(nchan, nbin, seed, rfi, a.cpu_budget)
@@ -266,7 +345,7 @@ def main():
                 print("%-16s %9.3f ms  %4d launches  %.3f ms/launch" %
                       (k, v["ms"], v["launches"], v["ms"] / max(1, v["launches"])), file=sys.stderr)
         print(json.dumps(rec))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

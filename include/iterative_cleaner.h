@@ -27,19 +27,21 @@
 #ifndef ITERATIVE_CLEANER_H
 #define ITERATIVE_CLEANER_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define IC_ABI_VERSION 2
+#define IC_ABI_VERSION 3
 
 #define IC_OK 0
 #define IC_EINVAL -1   /* bad argument / shape                         */
 #define IC_EHIP -2     /* HIP runtime error                            */
 #define IC_ENOMEM -3   /* device or host allocation failed             */
 #define IC_ESTATE -4   /* call out of order (e.g. run before upload)   */
+#define IC_ECOMM -5    /* a shard exchange failed (or a peer aborted)  */
 
 /* Loop parameters: args Namespace of iterative_cleaner.py:16-42. */
 typedef struct {
@@ -125,6 +127,62 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
 int ic_set_fit_tail(void *session, int64_t threshold);
 
 const char *ic_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Channel-sharded cleaning of ONE archive across `world` shards (config C3,
+ * SURVEY.md §8(e)).  The reference cleans an archive in one process
+ * (iterative_cleaner.py:83-146); these entry points split the same loop by
+ * channel blocks.  Rank r owns the channels of one node of the canonical
+ * super-block tree (archive.py sb_tree / shards.py channel_shards) and the
+ * subint rows [r*nsub/world, (r+1)*nsub/world) of the row medians.  Per
+ * iteration a shard exchanges: the template's per-subint channel-sum roots
+ * (two all-gathers of nsub*nbin f64), its diagnostics rows with the row owners
+ * (one all-to-all), the row medians/MADs (one all-gather of 8*rows doubles) and
+ * the convergence counters (one all-reduce).  Results are bit-identical to an
+ * unsharded session.  world must be a power of two <= the number of 256-channel
+ * super-blocks.
+ *
+ * A shard session takes the GLOBAL shape in ic_params; ic_upload /
+ * ic_upload_device take the shard's channel slice: cube [nsub][nchan_loc][nbin],
+ * w0 [nsub][nchan_loc], shift [nchan_loc]; per-profile outputs of ic_run and
+ * the ic_get_* calls are the shard's [nsub][nchan_loc] slice, while loops,
+ * changed and nzero are global.  Every shard of a group must call ic_run
+ * together (collectives inside).
+ * ------------------------------------------------------------------------ */
+
+/* Channel ranges [chan_ranges[2r], chan_ranges[2r+1]) and row ranges of every
+ * rank (arrays of 2*world int32). */
+int ic_shard_layout(int nsub, int nchan, int world, int32_t *chan_ranges, int32_t *row_ranges);
+
+/* Host-provided transport (one process per GPU; e.g. torch.distributed over
+ * RCCL/xGMI).  All exchange buffers are obtained through alloc() so that the
+ * host owns them.  Collectives are issued in stream order on `stream` (the
+ * session's hipStream_t) and return 0 on success.
+ *   allgather:  recv[r*bytes .. (r+1)*bytes) = rank r's send, every r
+ *   alltoallv:  send = blocks for ranks 0..world-1 (send_bytes[r] each, back to
+ *               back); recv = blocks from ranks 0..world-1 (recv_bytes[r])
+ *   allreduce_sum_i32: in place */
+typedef struct {
+    void *ctx;
+    int (*alloc)(void *ctx, size_t bytes, void **dev_ptr);
+    int (*release)(void *ctx, void *dev_ptr);
+    int (*allgather)(void *ctx, const void *send, void *recv, size_t bytes, void *stream);
+    int (*alltoallv)(void *ctx, const void *send, const size_t *send_bytes, void *recv,
+                     const size_t *recv_bytes, void *stream);
+    int (*allreduce_sum_i32)(void *ctx, int32_t *buf, size_t n, void *stream);
+} ic_comm_ops;
+
+/* Shard `rank` of `world` on HIP device `device`, exchanging through `ops`
+ * (copied; ops->ctx must outlive the session). */
+int ic_session_create_shard(const ic_params *params, int device, int rank, int world, const ic_comm_ops *ops,
+                            void **session);
+
+/* In-process shard group: `world` shards driven by `world` host threads of one
+ * process (one or several devices), exchanging by device-to-device / peer
+ * copies.  Destroy the group after all its sessions. */
+int ic_group_create(int world, void **group);
+void ic_group_destroy(void *group);
+int ic_session_create_grouped(const ic_params *params, int device, void *group, int rank, void **session);
 
 #ifdef __cplusplus
 }

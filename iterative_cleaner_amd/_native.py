@@ -12,13 +12,15 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libicgpu.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # symbols exported by libicgpu.so, as declared in include/iterative_cleaner.h
 EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session_destroy",
            "ic_upload", "ic_upload_device", "ic_run", "ic_get_residual", "ic_get_template",
            "ic_get_fit", "ic_get_diagnostics", "ic_get_kernel_times", "ic_kernel_name",
-           "ic_set_timing", "ic_get_run_stats", "ic_set_fit_tail", "ic_last_error")
+           "ic_set_timing", "ic_get_run_stats", "ic_set_fit_tail", "ic_last_error",
+           "ic_shard_layout", "ic_session_create_shard", "ic_group_create", "ic_group_destroy",
+           "ic_session_create_grouped")
 
 
 class NativeError(RuntimeError):
@@ -43,7 +45,40 @@ class KernelTime(C.Structure):
     _fields_ = [("kernel", C.c_int32), ("launches", C.c_int32), ("ms", C.c_double)]
 
 
+# ic_comm_ops callbacks (include/iterative_cleaner.h)
+ALLOC_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p))
+RELEASE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t), C.c_void_p,
+                           C.POINTER(C.c_size_t), C.c_void_p)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
+class CommOps(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("alloc", ALLOC_FN), ("release", RELEASE_FN),
+                ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN),
+                ("allreduce_sum_i32", ALLREDUCE_FN)]
+
+
 _lib = None
+
+
+def _init_torch_hip():
+    """torch-ROCm bundles its own HIP runtime (torch/lib/libamdhip64.so) next to
+    the one libicgpu.so links (/opt/rocm/lib/libamdhip64.so.7); both share the
+    process's GPU address space, which is what lets torch tensors be passed to
+    the C-ABI by pointer.  torch's runtime only finds the GPUs when it
+    initialises first, so when torch is installed it is initialised before
+    libicgpu is loaded (torch owns exchange buffers and streams in sharded and
+    benchmark runs)."""
+    try:
+        import torch
+    except ImportError:  # pragma: no cover - torch is part of the image
+        return
+    try:
+        torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        pass
 
 
 def load_library(path: str = LIB_PATH):
@@ -54,6 +89,7 @@ def load_library(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise NativeError("libicgpu.so not built at %s (run __graft_entry__.build() or make -C "
                           "iterative_cleaner_amd/csrc)" % path)
+    _init_torch_hip()
     try:
         lib = C.CDLL(path)
     except OSError as e:  # pragma: no cover - environment dependent
@@ -78,6 +114,13 @@ def load_library(path: str = LIB_PATH):
     lib.ic_set_timing.argtypes = [vp, C.c_int]
     lib.ic_get_run_stats.argtypes = [vp, C.POINTER(RunStats)]
     lib.ic_set_fit_tail.argtypes = [vp, C.c_int64]
+    lib.ic_shard_layout.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
+    lib.ic_session_create_shard.argtypes = [C.POINTER(Params), C.c_int, C.c_int, C.c_int,
+                                            C.POINTER(CommOps), C.POINTER(vp)]
+    lib.ic_group_create.argtypes = [C.c_int, C.POINTER(vp)]
+    lib.ic_group_destroy.argtypes = [vp]
+    lib.ic_group_destroy.restype = None
+    lib.ic_session_create_grouped.argtypes = [C.POINTER(Params), C.c_int, vp, C.c_int, C.POINTER(vp)]
     if lib.ic_abi_version() != ABI_VERSION:
         raise NativeError("libicgpu ABI %d != expected %d" % (lib.ic_abi_version(), ABI_VERSION))
     _lib = lib
@@ -120,10 +163,15 @@ class GpuSession:
         self.params = Params(int(nsub), int(nchan), int(nbin), int(max_iter), float(chanthresh),
                              float(subintthresh), on, fac, a, b, float(baseline_duty), 0)
         h = C.c_void_p()
-        rc = self.lib.ic_session_create(C.byref(self.params), int(device), C.byref(h))
+        rc = self._create(int(device), h)
         if rc != 0:
-            raise NativeError("ic_session_create: %s (rc=%d)" % (_err(self.lib), rc))
+            raise NativeError("%s: %s (rc=%d)" % (self._create_name, _err(self.lib), rc))
         self.h = h
+
+    _create_name = "ic_session_create"
+
+    def _create(self, device, h):
+        return self.lib.ic_session_create(C.byref(self.params), device, C.byref(h))
 
     # context manager -----------------------------------------------------
     def close(self):
@@ -226,3 +274,80 @@ class GpuSession:
             name = self.lib.ic_kernel_name(buf[q].kernel).decode()
             out[name] = dict(ms=buf[q].ms, launches=buf[q].launches)
         return out
+
+
+# ---------------------------------------------------------------- channel shards
+
+def shard_layout(nsub, nchan, world):
+    """([(c0, c1)] per rank, [(s0, s1)] per rank) from ic_shard_layout (C++),
+    the rule of iterative_cleaner_amd/shards.py."""
+    lib = load_library()
+    cr = np.zeros(2 * world, np.int32)
+    rr = np.zeros(2 * world, np.int32)
+    rc = lib.ic_shard_layout(int(nsub), int(nchan), int(world), _ptr(cr), _ptr(rr))
+    if rc != 0:
+        raise NativeError("ic_shard_layout: %s (rc=%d)" % (_err(lib), rc))
+    return ([(int(cr[2 * r]), int(cr[2 * r + 1])) for r in range(world)],
+            [(int(rr[2 * r]), int(rr[2 * r + 1])) for r in range(world)])
+
+
+class ShardGroup:
+    """In-process shard group (ic_group_create): `world` shard sessions driven
+    by `world` host threads of this process, exchanging by device copies."""
+
+    def __init__(self, world):
+        self.lib = load_library()
+        self.world = int(world)
+        h = C.c_void_p()
+        if self.lib.ic_group_create(self.world, C.byref(h)) != 0:
+            raise NativeError("ic_group_create: %s" % _err(self.lib))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ic_group_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
+class ShardSession(GpuSession):
+    """Channel shard `rank` of `world` of one archive (global shape in the
+    arguments; uploads and per-profile outputs are the shard's channel slice).
+    Exchanges go through `group` (a ShardGroup: in-process) or `comm` (an
+    object with ``ops()`` returning a CommOps, e.g. dist.TorchComm)."""
+
+    _create_name = "ic_session_create_shard"
+
+    def __init__(self, nsub, nchan, nbin, rank, world, group=None, comm=None, **kw):
+        if (group is None) == (comm is None):
+            raise ValueError("ShardSession needs exactly one of group / comm")
+        self.rank, self.world = int(rank), int(world)
+        self.group, self.comm = group, comm
+        chans, rows = shard_layout(nsub, nchan, world)
+        self.chan_range = chans[self.rank]
+        self.row_range = rows[self.rank]
+        self.global_shape = (int(nsub), int(nchan), int(nbin))
+        super().__init__(nsub, nchan, nbin, **kw)
+        c0, c1 = self.chan_range
+        self.shape = (int(nsub), c1 - c0, int(nbin))
+
+    def _create(self, device, h):
+        if self.group is not None:
+            self._create_name = "ic_session_create_grouped"
+            return self.lib.ic_session_create_grouped(C.byref(self.params), device, self.group.h,
+                                                      self.rank, C.byref(h))
+        self._ops = self.comm.ops()
+        return self.lib.ic_session_create_shard(C.byref(self.params), device, self.rank,
+                                                self.world, C.byref(self._ops), C.byref(h))
+
+    def _check(self, rc, what):
+        if rc < 0 and self.comm is not None and getattr(self.comm, "error", None):
+            raise NativeError("%s: %s (rc=%d); transport: %s"
+                              % (what, _err(self.lib), rc, self.comm.error))
+        return super()._check(rc, what)

@@ -14,8 +14,11 @@ order so that the HIP kernels can reproduce it bit-for-bit:
   ``dm_shift[c]`` bins, ``ded[i] = raw[(i + shift) % nbin]``;
 * channel sums (baseline total, fscrunch) use the CANONICAL CHANNEL ORDER
   (:func:`chan_sum`): f64, sequential inside super-blocks of ``SUPER_BLOCK``
-  channels, partials added sequentially.  Shards that own whole super-blocks
-  therefore reproduce single-device bits;
+  channels; the super-block partials are combined by the halving tree of
+  :func:`sb_tree`.  A shard that owns one node of that tree (2^d shards own
+  the 2^d nodes at depth d) computes its subtree alone, and the top d levels
+  combine the shard roots, so channel-sharded runs reproduce single-device
+  bits;
 * ``remove_baseline``: per subint (psrchive Integration::remove_baseline),
   the off-pulse window of width ``int(duty*nbin)`` is the first argmin of
   the circular window sums of the weighted, dedispersed total profile; each
@@ -33,25 +36,40 @@ import numpy as np
 SUPER_BLOCK = 256          # channels per canonical-order super-block
 BASELINE_DUTY = 0.15       # psrchive BaselineWindow default duty cycle
 
-__all__ = ["Archive", "Archive_load", "Profile", "Integration", "chan_sum",
+__all__ = ["Archive", "Archive_load", "Profile", "Integration", "chan_sum", "sb_tree",
            "baseline_width", "window_argmin", "SUPER_BLOCK", "BASELINE_DUTY"]
+
+
+def sb_tree(parts):
+    """Canonical combine of super-block partials ``parts[0..n)`` (n >= 1):
+    tree(lo, hi) = parts[lo] if hi - lo == 1 else tree(lo, mid) + tree(mid, hi),
+    mid = lo + (hi - lo) // 2."""
+    def tree(lo, hi):
+        if hi - lo == 1:
+            return parts[lo]
+        mid = lo + (hi - lo) // 2
+        return tree(lo, mid) + tree(mid, hi)
+    return tree(0, len(parts))
 
 
 def chan_sum(terms: np.ndarray, axis: int) -> np.ndarray:
     """Canonical channel reduction of f64 ``terms`` along ``axis``.
 
-    result = 0.0; for each super-block b: part = 0.0; part += t[c] for c in b
-    (ascending); result += part.  Zero-size → 0.0.
+    For each super-block b of SUPER_BLOCK channels: part_b = 0.0; part_b += t[c]
+    for c in b (ascending).  result = sb_tree(part_0 .. part_{nsb-1}).
+    Zero-size → 0.0.
     """
     t = np.moveaxis(np.asarray(terms, dtype=np.float64), axis, 0)
     nchan = t.shape[0]
-    total = np.zeros(t.shape[1:], dtype=np.float64)
+    if nchan == 0:
+        return np.zeros(t.shape[1:], dtype=np.float64)
+    parts = []
     for b0 in range(0, nchan, SUPER_BLOCK):
         part = np.zeros(t.shape[1:], dtype=np.float64)
         for c in range(b0, min(b0 + SUPER_BLOCK, nchan)):
             part = part + t[c]
-        total = total + part
-    return total
+        parts.append(part)
+    return sb_tree(parts)
 
 
 def baseline_width(nbin: int, duty: float = BASELINE_DUTY) -> int:

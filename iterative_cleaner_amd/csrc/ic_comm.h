@@ -1,0 +1,48 @@
+// ic_comm.h — shard exchange transports of libicgpu.so (not part of the C-ABI).
+//
+// A channel-sharded session (ic_session.hip) exchanges four things per
+// cleaning iteration (DESIGN.md "Channel-sharded large archive"): per-subint
+// channel-sum roots (all-gather), diagnostics rows to their row owners
+// (all-to-all), row medians/MADs (all-gather) and convergence counters
+// (all-reduce).  Every exchange is issued in stream order on the session's
+// stream; no host synchronisation is implied.
+//
+// Transports:
+//   CallbackComm — the host's ic_comm_ops (one process per GPU; the Python
+//                  host binds torch.distributed, i.e. RCCL over xGMI).
+//   LocalComm    — shards of one process (threads), device-to-device / peer
+//                  copies ordered by HIP events and a host barrier.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/iterative_cleaner.h"
+
+namespace icgpu {
+
+class Comm {
+public:
+    int rank = 0, world = 1;
+    virtual ~Comm() = default;
+    // device exchange buffer (host-owned for CallbackComm)
+    virtual int alloc(void **p, size_t bytes) = 0;
+    virtual void release(void *p) = 0;
+    virtual int allgather(const void *send, void *recv, size_t bytes, hipStream_t st) = 0;
+    virtual int alltoallv(const void *send, const size_t *send_bytes, void *recv, const size_t *recv_bytes,
+                          hipStream_t st) = 0;
+    virtual int allreduce_sum_i32(int32_t *buf, size_t n, hipStream_t st) = 0;
+    // a failing shard tells its peers (LocalComm: wakes their barriers)
+    virtual void abort() {}
+};
+
+Comm *make_callback_comm(const ic_comm_ops &ops, int rank, int world);
+
+struct LocalGroup;
+LocalGroup *local_group_create(int world);
+void local_group_destroy(LocalGroup *g);
+int local_group_world(const LocalGroup *g);
+// nullptr + message in *err when the rank is taken / out of range
+Comm *make_local_comm(LocalGroup *g, int rank, int device, const char **err);
+
+}  // namespace icgpu

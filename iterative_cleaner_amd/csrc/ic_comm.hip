@@ -1,0 +1,247 @@
+// ic_comm.hip — shard exchange transports (see ic_comm.h).
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <vector>
+
+#include "ic_comm.h"
+#include "ic_internal.h"
+
+namespace icgpu {
+
+// ------------------------------------------------------------ host callbacks
+
+class CallbackComm final : public Comm {
+public:
+    explicit CallbackComm(const ic_comm_ops &o) : ops(o) {}
+    int alloc(void **p, size_t bytes) override { return ops.alloc(ops.ctx, bytes, p); }
+    void release(void *p) override
+    {
+        if (p) (void)ops.release(ops.ctx, p);
+    }
+    int allgather(const void *send, void *recv, size_t bytes, hipStream_t st) override
+    {
+        return ops.allgather(ops.ctx, send, recv, bytes, (void *)st);
+    }
+    int alltoallv(const void *send, const size_t *sb, void *recv, const size_t *rb, hipStream_t st) override
+    {
+        return ops.alltoallv(ops.ctx, send, sb, recv, rb, (void *)st);
+    }
+    int allreduce_sum_i32(int32_t *buf, size_t n, hipStream_t st) override
+    {
+        return ops.allreduce_sum_i32(ops.ctx, buf, n, (void *)st);
+    }
+
+private:
+    ic_comm_ops ops;
+};
+
+Comm *make_callback_comm(const ic_comm_ops &ops, int rank, int world)
+{
+    auto *c = new CallbackComm(ops);
+    c->rank = rank;
+    c->world = world;
+    return c;
+}
+
+// ------------------------------------------------------------ in-process group
+
+struct LocalGroup {
+    struct Slot {
+        const void *send = nullptr;
+        const size_t *sb = nullptr;   // nullptr: all-gather (the same `send` for every peer)
+        hipEvent_t ready = nullptr;   // send buffer written (recorded on the owner's stream)
+        hipEvent_t done = nullptr;    // the owner has read every peer's send buffer
+        int device = 0;
+        bool taken = false;
+    };
+    int world = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    unsigned long long gen = 0;
+    bool aborted = false;
+    Slot slot[kMaxShards];
+
+    // all `world` threads meet; -1 if a shard aborted or nobody came for 10 min
+    int barrier()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        if (aborted) return -1;
+        const unsigned long long g0 = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return 0;
+        }
+        const bool ok = cv.wait_for(lk, std::chrono::minutes(10), [&] { return gen != g0 || aborted; });
+        if (gen != g0) return 0;
+        if (!ok) aborted = true;
+        cv.notify_all();
+        return -1;
+    }
+    void abort()
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+LocalGroup *local_group_create(int world)
+{
+    if (world < 1 || world > kMaxShards) return nullptr;
+    auto *g = new LocalGroup();
+    g->world = world;
+    return g;
+}
+
+void local_group_destroy(LocalGroup *g) { delete g; }
+
+int local_group_world(const LocalGroup *g) { return g ? g->world : 0; }
+
+class LocalComm final : public Comm {
+public:
+    LocalComm(LocalGroup *g_, int r, int dev) : g(g_), device(dev)
+    {
+        rank = r;
+        world = g_->world;
+    }
+    ~LocalComm() override
+    {
+        auto &me = g->slot[rank];
+        if (me.ready) (void)hipEventDestroy(me.ready);
+        if (me.done) (void)hipEventDestroy(me.done);
+        if (tmp) (void)hipFree(tmp);
+        std::lock_guard<std::mutex> lk(g->mu);
+        me = LocalGroup::Slot();
+    }
+    int init()
+    {
+        auto &me = g->slot[rank];
+        me.device = device;
+        if (hipEventCreateWithFlags(&me.ready, hipEventDisableTiming) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&me.done, hipEventDisableTiming) != hipSuccess) return -1;
+        return 0;
+    }
+    int alloc(void **p, size_t bytes) override { return hipMalloc(p, bytes ? bytes : 8) == hipSuccess ? 0 : -1; }
+    void release(void *p) override
+    {
+        if (p) (void)hipFree(p);
+    }
+    int allgather(const void *send, void *recv, size_t bytes, hipStream_t st) override
+    {
+        return exchange(send, nullptr, recv, nullptr, bytes, st);
+    }
+    int alltoallv(const void *send, const size_t *sb, void *recv, const size_t *rb, hipStream_t st) override
+    {
+        return exchange(send, sb, recv, rb, 0, st);
+    }
+    int allreduce_sum_i32(int32_t *buf, size_t n, hipStream_t st) override
+    {
+        if (n * world > tmp_n) {
+            if (tmp) (void)hipFree(tmp);
+            tmp = nullptr;
+            tmp_n = 0;
+            if (hipMalloc(&tmp, sizeof(int32_t) * n * world) != hipSuccess) return -1;
+            tmp_n = n * world;
+        }
+        if (int rc = exchange(buf, nullptr, tmp, nullptr, sizeof(int32_t) * n, st)) return rc;
+        return launch_sum_i32(st, tmp, world, (int)n, buf) == hipSuccess ? 0 : -1;
+    }
+    void abort() override { g->abort(); }
+
+private:
+    LocalGroup *g;
+    int device;
+    int32_t *tmp = nullptr;
+    size_t tmp_n = 0;
+    unsigned long long peer_on = 0;   // devices whose peer access this shard enabled
+
+    int copy(void *dst, const void *src, size_t bytes, int src_dev, hipStream_t st)
+    {
+        if (!bytes) return 0;
+        if (src_dev != device && src_dev < 64 && !((peer_on >> src_dev) & 1ull)) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, device, src_dev) == hipSuccess && can)
+                (void)hipDeviceEnablePeerAccess(src_dev, 0);
+            (void)hipGetLastError();   // "already enabled" is fine
+            peer_on |= 1ull << src_dev;
+        }
+        const hipError_t e = src_dev == device
+                                 ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st)
+                                 : hipMemcpyPeerAsync(dst, device, src, src_dev, bytes, st);
+        return e == hipSuccess ? 0 : -1;
+    }
+
+    // sb == nullptr: all-gather of gbytes; else all-to-all with per-peer sizes.
+    // Any failure aborts the group so that no peer waits for this shard.
+    int exchange(const void *send, const size_t *sb, void *recv, const size_t *rb, size_t gbytes, hipStream_t st)
+    {
+        const int rc = exchange_(send, sb, recv, rb, gbytes, st);
+        if (rc) g->abort();
+        return rc;
+    }
+    int exchange_(const void *send, const size_t *sb, void *recv, const size_t *rb, size_t gbytes, hipStream_t st)
+    {
+        auto &me = g->slot[rank];
+        me.send = send;
+        me.sb = sb;
+        if (hipEventRecord(me.ready, st) != hipSuccess) return -1;
+        if (g->barrier()) return -2;
+        size_t doff = 0;
+        for (int p = 0; p < world; ++p) {
+            const auto &ps = g->slot[p];
+            size_t bytes, soff = 0;
+            char *dst;
+            if (!sb) {
+                bytes = gbytes;
+                dst = (char *)recv + (size_t)p * gbytes;
+            } else {
+                if (!ps.sb) return -3;          // peer is in a different collective
+                bytes = ps.sb[rank];
+                for (int q = 0; q < rank; ++q) soff += ps.sb[q];
+                if (bytes != rb[p]) return -3;  // inconsistent block sizes
+                dst = (char *)recv + doff;
+                doff += rb[p];
+            }
+            if (!bytes) continue;
+            if (p != rank && hipStreamWaitEvent(st, ps.ready, 0) != hipSuccess) return -1;
+            if (copy(dst, (const char *)ps.send + soff, bytes, ps.device, st)) return -1;
+        }
+        if (hipEventRecord(me.done, st) != hipSuccess) return -1;
+        if (g->barrier()) return -2;
+        // nobody may overwrite its send buffer before every peer has copied it
+        for (int p = 0; p < world; ++p)
+            if (p != rank && hipStreamWaitEvent(st, g->slot[p].done, 0) != hipSuccess) return -1;
+        return 0;
+    }
+
+    friend Comm *make_local_comm(LocalGroup *, int, int, const char **);
+};
+
+Comm *make_local_comm(LocalGroup *g, int rank, int device, const char **err)
+{
+    if (!g || rank < 0 || rank >= g->world) {
+        *err = "rank out of range for the group";
+        return nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (g->slot[rank].taken) {
+            *err = "rank already has a session in this group";
+            return nullptr;
+        }
+        g->slot[rank].taken = true;
+    }
+    auto *c = new LocalComm(g, rank, device);
+    if (c->init()) {
+        delete c;
+        *err = "hipEventCreate failed";
+        return nullptr;
+    }
+    return c;
+}
+
+}  // namespace icgpu

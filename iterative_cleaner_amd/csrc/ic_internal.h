@@ -10,6 +10,29 @@ constexpr int kSuperBlock = 256;    // canonical channel super-block (archive.py
 constexpr int kMaxLeaves = 256;     // pairwise-sum leaves (nbin <= 32768)
 constexpr int kFitTile = 32;        // bins per k_fit_pass LDS tile (fit cube row padding)
 
+// Canonical combine of super-block partials (archive.py sb_tree): the halving
+// tree over n leaves, evaluated as a post-order stack program: push leaf j,
+// then merge the two top entries merges[j] times.  n <= kMaxSbLeaves (nchan <=
+// 16384); the stack never holds more than 1 + log2(n) <= 7 entries.
+constexpr int kMaxSbLeaves = 64;
+struct SbPlan {
+    int32_t n;
+    uint8_t merges[kMaxSbLeaves];
+};
+
+// Row/column geometry of a channel shard's exchanges (world <= kMaxShards):
+// rank r owns channels [chan0[r], chan0[r+1]) and subint rows [row0[r], row0[r+1]).
+constexpr int kMaxShards = 64;
+struct ShardGeom {
+    int32_t world, rank, nsub, nchan_g;
+    int32_t chan0[kMaxShards + 1];
+    int32_t row0[kMaxShards + 1];
+};
+
+// bytes of one exchange block of n elements of esz bytes (28 = std+mean+fft+ptp),
+// padded so that every block, and the f64 fields inside it, start 8-aligned
+__host__ __device__ inline size_t shard_block_bytes(size_t n, size_t esz) { return ((n * esz + 7) / 8) * 8; }
+
 // numpy pairwise-summation plan for one nbin (numpy loops_utils.h.src order):
 // leaves in address order, then a post-order list of internal adds.
 struct PwPlan {
@@ -37,6 +60,9 @@ enum KernelId {
     K_COMBINE,
     K_RESIDUAL,
     K_FIT_TAIL,
+    K_SB_TREE,
+    K_SHARD_PACK,     // pack / assemble / unpack of shard exchanges
+    K_EXCHANGE,       // the collectives themselves (host transport or peer copies)
     K_COUNT
 };
 
@@ -65,15 +91,36 @@ hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, cons
                                 const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
                                 double *part, double *part2, double *wpart);
 // flags != nullptr: flags[s] = window of subint s moved (win updated in place)
-hipError_t launch_window(hipStream_t st, const double *part, int nsub, int nsb, int nbin, int width,
-                         int32_t *win, int32_t *flags);
+// element (s, leaf, i) of `part` is part[s*ss + leaf*sl + i]; the leaves are
+// combined with `plan` (single device: the nsb super-blocks; sharded: the
+// gathered shard roots)
+hipError_t launch_window(hipStream_t st, const double *part, long ss, long sl, const SbPlan &plan, int nsub,
+                         int nbin, int width, int32_t *win, int32_t *flags);
 // flags != nullptr: only subints with flags[s] != 0
 hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, const int32_t *win,
                        const int32_t *flags, int nsub, int nchan, int nbin, int width, float *base);
 hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
                           int nsub, int nchan, int nbin, int ldD, float *D);
-hipError_t launch_fscrunch(hipStream_t st, const double *part, const double *wpart, int nsub, int nsb,
-                           int nbin, float *F, float *wf);
+// num (s, leaf, i) = part[s*ss + leaf*sl + i], weight (s, leaf) = wpart[s*wss + leaf*wsl]
+hipError_t launch_fscrunch(hipStream_t st, const double *part, long ss, long sl, const double *wpart, long wss,
+                           long wsl, const SbPlan &plan, int nsub, int nbin, float *F, float *wf);
+// shard root of the local super-block partials: out[s][i] = tree(part[s][*][i]),
+// outw[s] = tree(wpart[s][*]) (wpart/outw may be null); flags: only flagged subints
+hipError_t launch_sb_tree(hipStream_t st, const double *part, const double *wpart, const SbPlan &plan, int nsub,
+                          int nbin, const int32_t *flags, double *out, double *outw);
+// diagnostics rows -> per-destination blocks [std|mean|fft (f64)|ptp (f32)] x rows_d x nchan_loc
+// (valid == true: the single u8 field `valid` instead)
+hipError_t launch_pack_rows(hipStream_t st, const ShardGeom &g, int nchan_loc, const double *std_d,
+                            const double *mean_d, const double *fft_d, const float *ptp_d, const uint8_t *valid,
+                            unsigned char *send);
+// per-source blocks -> owned rows [rows_own][nchan_g] of each field
+hipError_t launch_assemble_rows(hipStream_t st, const ShardGeom &g, const unsigned char *recv, double *std_r,
+                                double *mean_r, double *fft_r, float *ptp_r, uint8_t *valid_r);
+// gathered [world][8 * rows_pad] (rank p: med [4][rows_p], mad [4][rows_p]) -> row_med/row_mad [4][nsub]
+hipError_t launch_unpack_rowstats(hipStream_t st, const ShardGeom &g, int rows_pad, const double *recv,
+                                  double *row_med, double *row_mad);
+// buf[i] = sum_r gathered[r][i]
+hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, int n, int32_t *buf);
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
                            double *T64);
 hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
@@ -93,7 +140,8 @@ hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const 
                        const double2 *tw_p2, const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
                        int pr_start, int pr_end, double *std_o, double *mean_o, float *ptp_o,
                        double *fft_o);
-hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a);
+// which: bit 0 = column lines (length nsub), bit 1 = row lines (length nchan)
+hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which = 3);
 hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const float *w0,
                           const double *std_d, const double *mean_d, const float *ptp_d,
                           const double *fft_d, const double *col_med, const double *col_mad,

@@ -14,6 +14,7 @@
 //                    window sums (archive.py window_argmin)
 //   k_base           per-profile window mean -> f32 baseline
 //   k_fscrunch       combine super-block partials -> F[s][i], wf[s]
+//   k_sb_tree        (channel shards) local super-block partials -> shard root
 //   k_tscrunch       weighted mean over subints, *10000 -> T (ic.py:94)
 //   k_fit            exact scipy leastsq(a*T-p, [1.0]) per profile (ic.py:278)
 //   k_diag           residual (ic.py:279-288), f32 store (:272), dededisperse
@@ -172,6 +173,28 @@ __global__ __launch_bounds__(256) void k_chan_partials(
     }
 }
 
+// Canonical super-block combine (archive.py sb_tree) as a post-order stack
+// program (SbPlan): the stack lives in registers (static indices only), top
+// at st[0].
+template <typename Get>
+__device__ __forceinline__ double sb_eval(const SbPlan &pl, Get get)
+{
+    double st[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st[k] = 0.0;
+    for (int j = 0; j < pl.n; ++j) {
+#pragma unroll
+        for (int k = 7; k > 0; --k) st[k] = st[k - 1];
+        st[0] = get(j);
+        for (int m = 0; m < (int)pl.merges[j]; ++m) {
+            st[0] = st[1] + st[0];   // left subtree + right subtree
+#pragma unroll
+            for (int k = 1; k < 7; ++k) st[k] = st[k + 1];
+        }
+    }
+    return st[0];
+}
+
 // numpy argmin combine: first NaN wins; otherwise smaller value, then lower index.
 __device__ __forceinline__ bool argmin_better(double va, int ia, double vb, int ib)
 {
@@ -185,11 +208,12 @@ __device__ __forceinline__ bool argmin_better(double va, int ia, double vb, int 
     return ia < ib;
 }
 
-// One block per subint: tot[i] = sum_sb part; m[j] = sum_{k<width} tot[(j+k)%n];
-// win[s] = first argmin.
+// One block per subint: tot[i] = sb_tree over the leaves of part; m[j] =
+// sum_{k<width} tot[(j+k)%n]; win[s] = first argmin.
 // flags != nullptr: flags[s] = (window moved), win[s] updated in place
-__global__ __launch_bounds__(256) void k_window(const double *__restrict__ part, int nsb, int nbin,
-                                                int width, int32_t *__restrict__ win, int32_t *__restrict__ flags)
+__global__ __launch_bounds__(256) void k_window(const double *__restrict__ part, long ss, long sl, SbPlan plan,
+                                                int nbin, int width, int32_t *__restrict__ win,
+                                                int32_t *__restrict__ flags)
 {
     extern __shared__ double sh[];
     double *tot = sh;                       // nbin
@@ -197,9 +221,8 @@ __global__ __launch_bounds__(256) void k_window(const double *__restrict__ part,
     int *bi = (int *)(bv + 256);            // 256
     const int s = blockIdx.x;
     for (int i = threadIdx.x; i < nbin; i += blockDim.x) {
-        double t = 0.0;
-        for (int sb = 0; sb < nsb; ++sb) t = t + part[((size_t)s * nsb + sb) * nbin + i];
-        tot[i] = t;
+        const double *src = part + (size_t)s * ss + i;
+        tot[i] = sb_eval(plan, [&](int j) { return src[(size_t)j * sl]; });
     }
     __syncthreads();
     double best = 0.0;
@@ -315,21 +338,41 @@ __global__ __launch_bounds__(256) void k_fitcube(const float *__restrict__ raw, 
     }
 }
 
-// F[s][i] = f32(num/wsum) (0 if wsum == 0); wf[s] = f32(wsum)
-__global__ __launch_bounds__(256) void k_fscrunch(const double *__restrict__ part, const double *__restrict__ wpart,
-                                                  int nsb, int nbin, float *__restrict__ F,
-                                                  float *__restrict__ wf)
+// F[s][i] = f32(num/wsum) (0 if wsum == 0); wf[s] = f32(wsum); num and wsum
+// are the canonical trees over the leaves
+__global__ __launch_bounds__(256) void k_fscrunch(const double *__restrict__ part, long ss, long sl,
+                                                  const double *__restrict__ wpart, long wss, long wsl, SbPlan plan,
+                                                  int nbin, float *__restrict__ F, float *__restrict__ wf)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int s = blockIdx.y;
     if (i >= nbin) return;
-    double num = 0.0, wsum = 0.0;
-    for (int sb = 0; sb < nsb; ++sb) {
-        num = num + part[((size_t)s * nsb + sb) * nbin + i];
-        wsum = wsum + wpart[(size_t)s * nsb + sb];
-    }
+    const double *src = part + (size_t)s * ss + i;
+    const double *wsrc = wpart + (size_t)s * wss;
+    const double num = sb_eval(plan, [&](int j) { return src[(size_t)j * sl]; });
+    const double wsum = sb_eval(plan, [&](int j) { return wsrc[(size_t)j * wsl]; });
     F[(size_t)s * nbin + i] = (wsum != 0.0) ? (float)(num / wsum) : 0.0f;
     if (i == 0) wf[s] = (float)wsum;
+}
+
+// Shard root of local super-block partials [s][nsb_loc][nbin] (channel shards):
+// out[s][i] = sb_tree(part[s][*][i]); outw[s] = sb_tree(wpart[s][*]).
+__global__ __launch_bounds__(256) void k_sb_tree(const double *__restrict__ part, const double *__restrict__ wpart,
+                                                 SbPlan plan, int nbin, const int32_t *__restrict__ flags,
+                                                 double *__restrict__ out, double *__restrict__ outw)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = blockIdx.y;
+    if (flags && flags[s] == 0) return;
+    const int n = plan.n;
+    if (i < nbin) {
+        const double *src = part + (size_t)s * n * nbin + i;
+        out[(size_t)s * nbin + i] = sb_eval(plan, [&](int j) { return src[(size_t)j * nbin]; });
+    }
+    if (wpart && i == 0) {
+        const double *w = wpart + (size_t)s * n;
+        outw[s] = sb_eval(plan, [&](int j) { return w[j]; });
+    }
 }
 
 // T[i] = f32( f32(sum_s wf*F / sum_s wf) * 10000 )
@@ -2252,6 +2295,108 @@ __global__ __launch_bounds__(256) void k_combine(
     }
 }
 
+// ============================================================ shard exchanges
+
+// owner rank of subint row s / channel c (world <= 64: linear scan)
+__device__ __forceinline__ int geom_row_owner(const ShardGeom &g, int s)
+{
+    int r = 0;
+    while (r + 1 < g.world && s >= g.row0[r + 1]) ++r;
+    return r;
+}
+__device__ __forceinline__ int geom_chan_owner(const ShardGeom &g, int c)
+{
+    int r = 0;
+    while (r + 1 < g.world && c >= g.chan0[r + 1]) ++r;
+    return r;
+}
+
+// Send blocks to row owners.  Destination d receives, for its rows
+// [row0[d], row0[d+1]) x my nchan_loc channels, the fields back to back:
+// std, mean, fft (f64), ptp (f32)  — or, in valid mode, valid (u8).
+// Blocks are padded to 8 bytes (shard_block_bytes); d's block starts after
+// the blocks of d' < d.
+__global__ __launch_bounds__(256) void k_pack_rows(ShardGeom g, int nchan_loc, const double *__restrict__ std_d,
+                                                   const double *__restrict__ mean_d, const double *__restrict__ fft_d,
+                                                   const float *__restrict__ ptp_d, const uint8_t *__restrict__ valid,
+                                                   unsigned char *__restrict__ send)
+{
+    const size_t P = (size_t)g.nsub * nchan_loc;
+    const size_t esz = valid ? 1 : 28;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < P; k += (size_t)gridDim.x * blockDim.x) {
+        const int s = (int)(k / nchan_loc);
+        const int d = geom_row_owner(g, s);
+        const size_t n_d = (size_t)(g.row0[d + 1] - g.row0[d]) * nchan_loc;   // elements in d's block
+        const size_t e = k - (size_t)g.row0[d] * nchan_loc;                   // element within it
+        size_t off = 0;
+        for (int q = 0; q < d; ++q) off += shard_block_bytes((size_t)(g.row0[q + 1] - g.row0[q]) * nchan_loc, esz);
+        unsigned char *blk = send + off;
+        if (valid) {
+            blk[e] = valid[k];
+        } else {
+            ((double *)blk)[e] = std_d[k];
+            ((double *)blk)[n_d + e] = mean_d[k];
+            ((double *)blk)[2 * n_d + e] = fft_d[k];
+            ((float *)(blk + 24 * n_d))[e] = ptp_d[k];
+        }
+    }
+}
+
+// Owned rows from the per-source blocks (source p sent rows_own x nchan_p
+// elements per field, after the padded blocks of sources p' < p).
+__global__ __launch_bounds__(256) void k_assemble_rows(ShardGeom g, const unsigned char *__restrict__ recv,
+                                                       double *__restrict__ std_r, double *__restrict__ mean_r,
+                                                       double *__restrict__ fft_r, float *__restrict__ ptp_r,
+                                                       uint8_t *__restrict__ valid_r)
+{
+    const int rows = g.row0[g.rank + 1] - g.row0[g.rank];
+    const size_t n = (size_t)rows * g.nchan_g;
+    const size_t esz = valid_r ? 1 : 28;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(k / g.nchan_g), c = (int)(k % g.nchan_g);
+        const int p = geom_chan_owner(g, c);
+        const int np = g.chan0[p + 1] - g.chan0[p];
+        const size_t n_p = (size_t)rows * np;
+        const size_t e = (size_t)r * np + (c - g.chan0[p]);
+        size_t off = 0;
+        for (int q = 0; q < p; ++q) off += shard_block_bytes((size_t)rows * (g.chan0[q + 1] - g.chan0[q]), esz);
+        const unsigned char *blk = recv + off;
+        if (valid_r) {
+            valid_r[k] = blk[e];
+        } else {
+            std_r[k] = ((const double *)blk)[e];
+            mean_r[k] = ((const double *)blk)[n_p + e];
+            fft_r[k] = ((const double *)blk)[2 * n_p + e];
+            ptp_r[k] = ((const float *)(blk + 24 * n_p))[e];
+        }
+    }
+}
+
+// gathered row statistics: rank p's slot (8 * rows_pad doubles) holds med
+// [4][rows_p] then mad [4][rows_p] of its rows_p owned rows
+__global__ __launch_bounds__(256) void k_unpack_rowstats(ShardGeom g, int rows_pad, const double *__restrict__ recv,
+                                                         double *__restrict__ row_med, double *__restrict__ row_mad)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;   // q * nsub + s
+    if (k >= 4 * g.nsub) return;
+    const int q = k / g.nsub, s = k % g.nsub;
+    const int p = geom_row_owner(g, s);
+    const int rows_p = g.row0[p + 1] - g.row0[p];
+    const int r = s - g.row0[p];
+    const double *slot = recv + (size_t)p * 8 * rows_pad;
+    row_med[k] = slot[q * rows_p + r];
+    row_mad[k] = slot[4 * rows_p + q * rows_p + r];
+}
+
+__global__ void k_sum_i32(const int32_t *__restrict__ gathered, int world, int n, int32_t *__restrict__ buf)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t a = 0;
+    for (int r = 0; r < world; ++r) a += gathered[(size_t)r * n + i];
+    buf[i] = a;
+}
+
 // ============================================================ launchers
 
 static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
@@ -2275,11 +2420,12 @@ hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, cons
     return hipGetLastError();
 }
 
-hipError_t launch_window(hipStream_t st, const double *part, int nsub, int nsb, int nbin, int width,
-                         int32_t *win, int32_t *flags)
+hipError_t launch_window(hipStream_t st, const double *part, long ss, long sl, const SbPlan &plan, int nsub,
+                         int nbin, int width, int32_t *win, int32_t *flags)
 {
+    if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
     const size_t shm = (size_t)nbin * 8 + 256 * 8 + 256 * 4;
-    hipLaunchKernelGGL(k_window, dim3(nsub), dim3(256), shm, st, part, nsb, nbin, width, win, flags);
+    hipLaunchKernelGGL(k_window, dim3(nsub), dim3(256), shm, st, part, ss, sl, plan, nbin, width, win, flags);
     return hipGetLastError();
 }
 
@@ -2301,12 +2447,58 @@ hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift
     return hipGetLastError();
 }
 
-hipError_t launch_fscrunch(hipStream_t st, const double *part, const double *wpart, int nsub, int nsb,
-                           int nbin, float *F, float *wf)
+hipError_t launch_fscrunch(hipStream_t st, const double *part, long ss, long sl, const double *wpart, long wss,
+                           long wsl, const SbPlan &plan, int nsub, int nbin, float *F, float *wf)
 {
+    if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
-    hipLaunchKernelGGL(k_fscrunch, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, wpart, nsb, nbin, F,
-                       wf);
+    hipLaunchKernelGGL(k_fscrunch, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, ss, sl, wpart, wss, wsl, plan,
+                       nbin, F, wf);
+    return hipGetLastError();
+}
+
+hipError_t launch_sb_tree(hipStream_t st, const double *part, const double *wpart, const SbPlan &plan, int nsub,
+                          int nbin, const int32_t *flags, double *out, double *outw)
+{
+    if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
+    const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
+    hipLaunchKernelGGL(k_sb_tree, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, wpart, plan, nbin, flags, out,
+                       outw);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_rows(hipStream_t st, const ShardGeom &g, int nchan_loc, const double *std_d,
+                            const double *mean_d, const double *fft_d, const float *ptp_d, const uint8_t *valid,
+                            unsigned char *send)
+{
+    const size_t P = (size_t)g.nsub * nchan_loc;
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack_rows, dim3(std::min<unsigned>(cdiv(P, 256), 4096)), dim3(256), 0, st, g, nchan_loc,
+                       std_d, mean_d, fft_d, ptp_d, valid, send);
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble_rows(hipStream_t st, const ShardGeom &g, const unsigned char *recv, double *std_r,
+                                double *mean_r, double *fft_r, float *ptp_r, uint8_t *valid_r)
+{
+    const size_t n = (size_t)(g.row0[g.rank + 1] - g.row0[g.rank]) * g.nchan_g;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_assemble_rows, dim3(std::min<unsigned>(cdiv(n, 256), 4096)), dim3(256), 0, st, g, recv,
+                       std_r, mean_r, fft_r, ptp_r, valid_r);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_rowstats(hipStream_t st, const ShardGeom &g, int rows_pad, const double *recv,
+                                  double *row_med, double *row_mad)
+{
+    hipLaunchKernelGGL(k_unpack_rowstats, dim3(cdiv(4 * (size_t)g.nsub, 256)), dim3(256), 0, st, g, rows_pad, recv,
+                       row_med, row_mad);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, int n, int32_t *buf)
+{
+    hipLaunchKernelGGL(k_sum_i32, dim3(cdiv(n, 64)), dim3(64), 0, st, gathered, world, n, buf);
     return hipGetLastError();
 }
 
@@ -2393,18 +2585,20 @@ hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const 
 }
 
 
-hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a)
+hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
 {
     // columns (length nsub), then rows (length nchan); wave-private LDS:
     // 256-bin histogram + the line's keys
     for (int rows = 0; rows < 2; ++rows) {
+        if (!((which >> rows) & 1)) continue;
         const int len = rows ? a.nchan : a.nsub;
+        const int lines = 4 * (rows ? a.nsub : a.nchan);
+        if (lines == 0 || len == 0) continue;
         const int per_wave = 1024 + ((len * 8 + 15) / 16) * 16;
         int wpb = 4;
         while (wpb > 1 && (size_t)wpb * per_wave > 64 * 1024) --wpb;
         const size_t shm = (size_t)wpb * per_wave;
         if (shm > 160 * 1024) return hipErrorInvalidValue;
-        const int lines = 4 * (rows ? a.nsub : a.nchan);
         hipLaunchKernelGGL(k_linestats, dim3(cdiv(lines, wpb)), dim3(64 * wpb), shm, st, a, rows, len, wpb,
                            per_wave);
         const hipError_t e = hipGetLastError();

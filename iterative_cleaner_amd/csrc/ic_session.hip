@@ -2,7 +2,9 @@
 // include/iterative_cleaner.h.  Owns device buffers and the HIP stream of a
 // session, prepares the fit cube at the start of every run, and drives the cleaning
 // loop of iterative_cleaner.py:83-146 (one launch sequence per iteration and
-// one small device->host read of the convergence counters).
+// one small device->host read of the convergence counters).  A channel shard
+// (ic_session_create_shard / _grouped) runs the same sequence on its channel
+// slice with four exchanges per iteration through a Comm (ic_comm.h).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdarg.h>
@@ -13,6 +15,7 @@
 #include <vector>
 
 #include "../../include/iterative_cleaner.h"
+#include "ic_comm.h"
 #include "ic_internal.h"
 
 using namespace icgpu;
@@ -43,7 +46,7 @@ int fail(int code, const char *fmt, ...)
 const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",     "k_fitcube",
                                      "k_fscrunch",      "k_tscrunch",  "k_fit_pass", "k_fit_state",
                                      "k_diag",          "k_linestats", "k_combine",  "k_residual",
-                                     "k_fit_tail"};
+                                     "k_fit_tail",      "k_sb_tree",   "k_shard_pack", "exchange"};
 
 constexpr int kMaxRounds = 1024;      // lmdif rounds per fit (maxfev = 400 bounds it far below)
 constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
@@ -62,6 +65,23 @@ struct Session {
     int nsb = 0, width = 0;
     bool uploaded = false, ran = false;
     int last_iter = 0;
+    // channel shard (unsharded: world == 1, comm == nullptr, nchan == p.nchan)
+    int rank = 0, world = 1;
+    Comm *comm = nullptr;
+    int nchan = 0;                  // channels of this session (local slice)
+    int c0 = 0;                     // its first global channel
+    ShardGeom geom{};
+    SbPlan plan_sb{};               // the session's super-blocks
+    SbPlan plan_top{};              // the shard roots (world leaves)
+    int rows_own = 0, rows_pad = 0;
+    double *xw_send = nullptr, *xw_recv = nullptr;          // window-total roots
+    double *xf_send = nullptr, *xf_recv = nullptr;          // fscrunch roots + weight roots
+    unsigned char *xd_send = nullptr, *xd_recv = nullptr;   // diagnostics / valid rows
+    double *xr_send = nullptr, *xr_recv = nullptr;          // row medians / MADs
+    std::vector<size_t> dsb, drb, vsb, vrb;                 // block bytes: diag, valid
+    double *std_r = nullptr, *mean_r = nullptr, *fft_r = nullptr;   // owned rows [rows_own][nchan_g]
+    float *ptp_r = nullptr;
+    uint8_t *valid_r = nullptr;
     // device buffers
     float *raw = nullptr, *D = nullptr, *w0 = nullptr, *W = nullptr, *base = nullptr, *base0 = nullptr;
     float *F = nullptr, *wf = nullptr, *T = nullptr, *ptp = nullptr, *hist = nullptr;
@@ -196,12 +216,24 @@ int collect_timing(Session *s)
 void free_all(Session *s)
 {
     void *bufs[] = {s->raw,  s->D,     s->w0,   s->W,   s->base, s->base0, s->F,   s->wf,
-                    s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->counters,
+                    s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
                     s->wflag};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    void *rbufs[] = {s->std_r, s->mean_r, s->fft_r, s->ptp_r, s->valid_r};
+    for (void *b : rbufs)
+        if (b) (void)hipFree(b);
+    if (s->comm) {
+        void *xbufs[] = {s->xw_send, s->xw_recv, s->xf_send, s->xf_recv, s->xd_send, s->xd_recv, s->xr_send,
+                         s->xr_recv, s->counters};
+        for (void *b : xbufs)
+            if (b) s->comm->release(b);
+        s->counters = nullptr;
+        delete s->comm;
+        s->comm = nullptr;
+    }
     if (s->h_rcount) (void)hipHostFree(s->h_rcount);
     for (auto &e : s->rev)
         if (e) (void)hipEventDestroy(e);
@@ -223,19 +255,130 @@ __global__ void k_valid(const float *w0, uint8_t *valid, float *W, float *hist0,
     }
 }
 
+#define CM(S, call, what)                                                                         \
+    do {                                                                                          \
+        Timed t_{K_EXCHANGE, nullptr, nullptr};                                                   \
+        if ((S)->timing) {                                                                        \
+            CK(hipEventCreate(&t_.a));                                                            \
+            CK(hipEventCreate(&t_.b));                                                            \
+            CK(hipEventRecord(t_.a, (S)->stream));                                                \
+        }                                                                                         \
+        const int rc_ = (call);                                                                   \
+        if ((S)->timing) {                                                                        \
+            CK(hipEventRecord(t_.b, (S)->stream));                                                \
+            (S)->events.push_back(t_);                                                            \
+        }                                                                                         \
+        if (rc_ != 0) {                                                                           \
+            (S)->comm->abort();                                                                   \
+            return fail(IC_ECOMM, "shard %d/%d: %s exchange failed (%d)", (S)->rank, (S)->world,  \
+                        what, rc_);                                                               \
+        }                                                                                         \
+    } while (0)
+
+// Halving-tree plan (archive.py sb_tree) as a post-order stack program.
+void sb_plan_rec(int lo, int hi, uint8_t *merges)
+{
+    if (hi - lo == 1) return;
+    const int mid = lo + (hi - lo) / 2;
+    sb_plan_rec(lo, mid, merges);
+    sb_plan_rec(mid, hi, merges);
+    merges[hi - 1]++;
+}
+
+SbPlan make_sb_plan(int n)
+{
+    SbPlan pl;
+    memset(&pl, 0, sizeof pl);
+    pl.n = n;
+    if (n >= 1 && n <= kMaxSbLeaves) sb_plan_rec(0, n, pl.merges);
+    return pl;
+}
+
+// shards.py channel_shards / row_owners; 0 or an error message
+const char *shard_layout(int nsub, int nchan, int world, int32_t *chan0, int32_t *row0)
+{
+    if (world < 1 || (world & (world - 1))) return "world size must be a power of two";
+    if (world > kMaxShards) return "world size too large";
+    const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
+    if (nsb < world) return "fewer 256-channel super-blocks than shards";
+    int depth = 0;
+    while ((1 << depth) < world) ++depth;
+    for (int r = 0; r < world; ++r) {
+        int lo = 0, hi = nsb;
+        for (int d = depth - 1; d >= 0; --d) {
+            const int mid = lo + (hi - lo) / 2;
+            if ((r >> d) & 1)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        chan0[2 * r] = lo * kSuperBlock;
+        chan0[2 * r + 1] = std::min(hi * kSuperBlock, nchan);
+        row0[2 * r] = (int)((long)r * nsub / world);
+        row0[2 * r + 1] = (int)((long)(r + 1) * nsub / world);
+    }
+    return nullptr;
+}
+
+// Window stage: per-subint window from the W-weighted total of `part`
+// (unsharded: combine the super-blocks; sharded: reduce the local
+// super-blocks to this shard's root, all-gather the roots, combine them).
+int window_stage(Session *s, int32_t *flags)
+{
+    const int nsub = s->p.nsub, nbin = s->p.nbin;
+    if (!s->comm) {
+        LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, (long)s->nsb * nbin, nbin, s->plan_sb, nsub, nbin,
+                                          s->width, s->win, flags));
+        return 0;
+    }
+    LAUNCH(s, K_SB_TREE, launch_sb_tree(s->stream, s->part, nullptr, s->plan_sb, nsub, nbin, nullptr, s->xw_send,
+                                        nullptr));
+    CM(s, s->comm->allgather(s->xw_send, s->xw_recv, sizeof(double) * nsub * nbin, s->stream), "window roots");
+    LAUNCH(s, K_WINDOW, launch_window(s->stream, s->xw_recv, nbin, (long)nsub * nbin, s->plan_top, nsub, nbin,
+                                      s->width, s->win, flags));
+    return 0;
+}
+
+// fscrunch + tscrunch from part2/wpart (same sharding as window_stage)
+int scrunch_stage(Session *s)
+{
+    const int nsub = s->p.nsub, nbin = s->p.nbin;
+    if (!s->comm) {
+        LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->part2, (long)s->nsb * nbin, nbin, s->wpart, s->nsb, 1,
+                                              s->plan_sb, nsub, nbin, s->F, s->wf));
+    } else {
+        const long L = (long)nsub * nbin + nsub;   // one shard's roots: [nsub][nbin] + [nsub]
+        LAUNCH(s, K_SB_TREE, launch_sb_tree(s->stream, s->part2, s->wpart, s->plan_sb, nsub, nbin, nullptr,
+                                            s->xf_send, s->xf_send + (size_t)nsub * nbin));
+        CM(s, s->comm->allgather(s->xf_send, s->xf_recv, sizeof(double) * L, s->stream), "fscrunch roots");
+        LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->xf_recv, nbin, L, s->xf_recv + (size_t)nsub * nbin, 1, L,
+                                              s->plan_top, nsub, nbin, s->F, s->wf));
+    }
+    LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64));
+    return 0;
+}
+
 // fit-cube preparation (iterative_cleaner.py:96-100): baseline with w0, dedisperse.
 // The w0 baseline (window + per-profile levels) is also the template stage's
-// baseline of the first iteration (W == w0).
+// baseline of the first iteration (W == w0).  A shard also hands the validity
+// of its profiles to the row owners (static for the whole run).
 int prepare(Session *s)
 {
-    const int nsub = s->p.nsub, nchan = s->p.nchan, nbin = s->p.nbin;
+    const int nsub = s->p.nsub, nchan = s->nchan, nbin = s->p.nbin;
     hipLaunchKernelGGL(k_valid, dim3((unsigned)((s->P + 255) / 256)), dim3(256), 0, s->stream, s->w0,
                        s->valid, s->W, s->hist, s->P);
     CK(hipGetLastError());
+    if (s->comm) {
+        LAUNCH(s, K_SHARD_PACK,
+               launch_pack_rows(s->stream, s->geom, nchan, nullptr, nullptr, nullptr, nullptr, s->valid, s->xd_send));
+        CM(s, s->comm->alltoallv(s->xd_send, s->vsb.data(), s->xd_recv, s->vrb.data(), s->stream), "valid rows");
+        LAUNCH(s, K_SHARD_PACK,
+               launch_assemble_rows(s->stream, s->geom, s->xd_recv, nullptr, nullptr, nullptr, nullptr, s->valid_r));
+    }
     LAUNCH(s, K_CHAN_PARTIALS,
            launch_chan_partials(s->stream, 0, s->raw, s->w0, s->shift, nullptr, nullptr, nsub, nchan, nbin, s->part,
                                 nullptr, nullptr));
-    LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win, nullptr));
+    if (int rc = window_stage(s, nullptr)) return rc;
     LAUNCH(s, K_BASE,
            launch_base(s->stream, s->raw, s->shift, s->win, nullptr, nsub, nchan, nbin, s->width, s->base0));
     LAUNCH(s, K_FITCUBE, launch_fitcube(s->stream, s->raw, s->shift, s->base0, nsub, nchan, nbin, s->ldD, s->D));
@@ -254,7 +397,7 @@ int prepare(Session *s)
 // recomputed (flagged launches that are empty when nothing moved).
 int iteration_template(Session *s, int iter)
 {
-    const int nsub = s->p.nsub, nchan = s->p.nchan, nbin = s->p.nbin;
+    const int nsub = s->p.nsub, nchan = s->nchan, nbin = s->p.nbin;
     if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, 1, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
@@ -263,15 +406,40 @@ int iteration_template(Session *s, int iter)
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, 2, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
                                     s->part, s->part2, s->wpart));
-        LAUNCH(s, K_WINDOW, launch_window(s->stream, s->part, nsub, s->nsb, nbin, s->width, s->win, s->wflag));
+        if (int rc = window_stage(s, s->wflag)) return rc;
         LAUNCH(s, K_BASE,
                launch_base(s->stream, s->raw, s->shift, s->win, s->wflag, nsub, nchan, nbin, s->width, s->base));
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, 1, s->raw, s->W, s->shift, s->base, s->wflag, nsub, nchan, nbin,
                                     nullptr, s->part2, s->wpart));
     }
-    LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->part2, s->wpart, nsub, s->nsb, nbin, s->F, s->wf));
-    LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64));
+    return scrunch_stage(s);
+}
+
+// Row medians/MADs of a shard: the diagnostics rows go to their owners
+// (all-to-all), each owner runs the row selections over whole rows, and the
+// results are all-gathered into row_med/row_mad [4][nsub].
+int shard_rowstats(Session *s, const LineStatsArgs &la)
+{
+    LAUNCH(s, K_SHARD_PACK,
+           launch_pack_rows(s->stream, s->geom, s->nchan, s->std_, s->mean, s->fft, s->ptp, nullptr, s->xd_send));
+    CM(s, s->comm->alltoallv(s->xd_send, s->dsb.data(), s->xd_recv, s->drb.data(), s->stream), "diagnostics rows");
+    LAUNCH(s, K_SHARD_PACK,
+           launch_assemble_rows(s->stream, s->geom, s->xd_recv, s->std_r, s->mean_r, s->fft_r, s->ptp_r, nullptr));
+    LineStatsArgs lr;
+    lr.nsub = s->rows_own;
+    lr.nchan = s->geom.nchan_g;
+    lr.valid = s->valid_r;
+    lr.std_d = s->std_r;
+    lr.mean_d = s->mean_r;
+    lr.fft_d = s->fft_r;
+    lr.ptp_d = s->ptp_r;
+    lr.col_med = lr.col_mad = nullptr;
+    lr.row_med = s->xr_send;
+    lr.row_mad = s->xr_send + 4 * s->rows_own;
+    LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, lr, 2));
+    CM(s, s->comm->allgather(s->xr_send, s->xr_recv, sizeof(double) * 8 * s->rows_pad, s->stream), "row statistics");
+    LAUNCH(s, K_SHARD_PACK, launch_unpack_rowstats(s->stream, s->geom, s->rows_pad, s->xr_recv, la.row_med, la.row_mad));
     return 0;
 }
 
@@ -358,7 +526,17 @@ const char *ic_kernel_name(int kernel)
     return kKernelNames[kernel];
 }
 
-int ic_session_create(const ic_params *params, int device, void **out)
+}  // extern "C"
+
+namespace {
+
+// Shared by every create entry point.  sharded: this session is channel shard
+// `rank` of `world` (world may be 1: the exchanges then run over a one-rank
+// transport, which tests it end to end); make_comm() builds the transport
+// after the device is current.
+template <typename MakeComm>
+int create_session(const ic_params *params, int device, int rank, int world, bool sharded, MakeComm make_comm,
+                   void **out)
 {
     if (!params || !out) return fail(IC_EINVAL, "null argument");
     *out = nullptr;
@@ -370,15 +548,37 @@ int ic_session_create(const ic_params *params, int device, void **out)
         return fail(IC_EINVAL, "line length > 16384 unsupported (nsub=%d nchan=%d)", p.nsub, p.nchan);
     if (p.max_iter < 0) return fail(IC_EINVAL, "max_iter < 0");
     if (p.fit_mode != 0) return fail(IC_EINVAL, "fit_mode %d unsupported", p.fit_mode);
+    if (world < 1 || rank < 0 || rank >= world) return fail(IC_EINVAL, "bad rank %d / world %d", rank, world);
+    std::vector<int32_t> cr(2 * world), rr(2 * world);
+    if (const char *e = shard_layout(p.nsub, p.nchan, world, cr.data(), rr.data()))
+        return fail(IC_EINVAL, "cannot shard nchan=%d over %d: %s", p.nchan, world, e);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(IC_EHIP, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
     Session *s = new Session();
     s->p = p;
     s->device = device;
-    s->P = (size_t)p.nsub * p.nchan;
+    s->rank = rank;
+    s->world = world;
+    s->c0 = cr[2 * rank];
+    s->nchan = cr[2 * rank + 1] - cr[2 * rank];
+    s->P = (size_t)p.nsub * s->nchan;
     s->N = s->P * (size_t)p.nbin;
-    s->nsb = (p.nchan + kSuperBlock - 1) / kSuperBlock;
+    s->nsb = (s->nchan + kSuperBlock - 1) / kSuperBlock;
+    s->plan_sb = make_sb_plan(s->nsb);
+    s->plan_top = make_sb_plan(world);
+    s->geom.world = world;
+    s->geom.rank = rank;
+    s->geom.nsub = p.nsub;
+    s->geom.nchan_g = p.nchan;
+    for (int r = 0; r < world; ++r) {
+        s->geom.chan0[r] = cr[2 * r];
+        s->geom.row0[r] = rr[2 * r];
+    }
+    s->geom.chan0[world] = p.nchan;
+    s->geom.row0[world] = p.nsub;
+    s->rows_own = rr[2 * rank + 1] - rr[2 * rank];
+    s->rows_pad = (p.nsub + world - 1) / world;
     s->ldD = ((p.nbin + kFitTile - 1) / kFitTile) * kFitTile;
     s->Ppad = ((s->P + 63) / 64) * 64;
     s->width = (int)(p.baseline_duty * (double)p.nbin);
@@ -400,7 +600,7 @@ int ic_session_create(const ic_params *params, int device, void **out)
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(IC_EHIP, "hipStreamCreate failed"));
     const size_t P = s->P, N = s->N;
-    const int nsub = p.nsub, nchan = p.nchan, nbin = p.nbin;
+    const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
     AL(s->raw, N);
     AL(s->D, s->Ppad * (size_t)s->ldD);
     if (hipMemset(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD) != hipSuccess)
@@ -431,12 +631,52 @@ int ic_session_create(const ic_params *params, int device, void **out)
     AL(s->test, P);
     AL(s->hist, P * (size_t)(p.max_iter + 1));
     AL(s->lstat, (size_t)16 * (nchan + nsub));
-    AL(s->counters, (size_t)(p.max_iter + 4));
     AL(s->tw, (size_t)nbin);
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     AL(s->lists, 2 * P);
     AL(s->rcount, (size_t)kMaxRounds + 2);
+    if (sharded) {
+        const char *cerr = nullptr;
+        s->comm = make_comm(&cerr);
+        if (!s->comm) return bail(fail(IC_EINVAL, "shard transport: %s", cerr ? cerr : "failed"));
+        const size_t nchan_g = (size_t)p.nchan;
+        AL(s->std_r, (size_t)s->rows_own * nchan_g);
+        AL(s->mean_r, (size_t)s->rows_own * nchan_g);
+        AL(s->fft_r, (size_t)s->rows_own * nchan_g);
+        AL(s->ptp_r, (size_t)s->rows_own * nchan_g);
+        AL(s->valid_r, (size_t)s->rows_own * nchan_g);
+        size_t dsend = 0, drecv = 0;
+        for (int r = 0; r < world; ++r) {
+            const size_t rows_r = (size_t)(rr[2 * r + 1] - rr[2 * r]);
+            const size_t nch_r = (size_t)(cr[2 * r + 1] - cr[2 * r]);
+            s->dsb.push_back(shard_block_bytes(rows_r * nchan, 28));
+            s->vsb.push_back(shard_block_bytes(rows_r * nchan, 1));
+            s->drb.push_back(shard_block_bytes((size_t)s->rows_own * nch_r, 28));
+            s->vrb.push_back(shard_block_bytes((size_t)s->rows_own * nch_r, 1));
+            dsend += s->dsb.back();
+            drecv += s->drb.back();
+        }
+        const size_t L = (size_t)nsub * nbin + nsub;
+        struct {
+            void **ptr;
+            size_t bytes;
+            const char *name;
+        } xb[] = {{(void **)&s->xw_send, sizeof(double) * nsub * nbin, "window roots"},
+                  {(void **)&s->xw_recv, sizeof(double) * world * nsub * nbin, "gathered window roots"},
+                  {(void **)&s->xf_send, sizeof(double) * L, "fscrunch roots"},
+                  {(void **)&s->xf_recv, sizeof(double) * world * L, "gathered fscrunch roots"},
+                  {(void **)&s->xd_send, dsend, "diagnostics send"},
+                  {(void **)&s->xd_recv, drecv, "diagnostics receive"},
+                  {(void **)&s->xr_send, sizeof(double) * 8 * s->rows_pad, "row statistics"},
+                  {(void **)&s->xr_recv, sizeof(double) * 8 * s->rows_pad * world, "gathered row statistics"},
+                  {(void **)&s->counters, sizeof(int32_t) * (p.max_iter + 4), "counters"}};
+        for (auto &b : xb)
+            if (s->comm->alloc(b.ptr, b.bytes + 16) != 0 || !*b.ptr)
+                return bail(fail(IC_ENOMEM, "exchange buffer (%s, %zu bytes) failed", b.name, b.bytes));
+    } else {
+        AL(s->counters, (size_t)(p.max_iter + 4));
+    }
 #undef AL
     if (hipHostMalloc((void **)&s->h_rcount, sizeof(int32_t) * kMaxRounds, hipHostMallocDefault) != hipSuccess)
         return bail(fail(IC_ENOMEM, "hipHostMalloc(round counts) failed"));
@@ -475,6 +715,51 @@ int ic_session_create(const ic_params *params, int device, void **out)
     return IC_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int ic_session_create(const ic_params *params, int device, void **out)
+{
+    return create_session(params, device, 0, 1, false, [](const char **) -> Comm * { return nullptr; }, out);
+}
+
+int ic_shard_layout(int nsub, int nchan, int world, int32_t *chan_ranges, int32_t *row_ranges)
+{
+    if (!chan_ranges || !row_ranges || nsub <= 0 || nchan <= 0) return fail(IC_EINVAL, "bad argument");
+    if (const char *e = shard_layout(nsub, nchan, world, chan_ranges, row_ranges))
+        return fail(IC_EINVAL, "cannot shard nchan=%d over %d: %s", nchan, world, e);
+    return IC_OK;
+}
+
+int ic_session_create_shard(const ic_params *params, int device, int rank, int world, const ic_comm_ops *ops,
+                            void **out)
+{
+    if (!ops || !ops->alloc || !ops->release || !ops->allgather || !ops->alltoallv || !ops->allreduce_sum_i32)
+        return fail(IC_EINVAL, "incomplete ic_comm_ops");
+    const ic_comm_ops o = *ops;
+    return create_session(params, device, rank, world, true,
+                          [&](const char **) -> Comm * { return make_callback_comm(o, rank, world); }, out);
+}
+
+int ic_group_create(int world, void **group)
+{
+    if (!group) return fail(IC_EINVAL, "null argument");
+    *group = local_group_create(world);
+    if (!*group) return fail(IC_EINVAL, "bad group size %d", world);
+    return IC_OK;
+}
+
+void ic_group_destroy(void *group) { local_group_destroy((LocalGroup *)group); }
+
+int ic_session_create_grouped(const ic_params *params, int device, void *group, int rank, void **out)
+{
+    LocalGroup *g = (LocalGroup *)group;
+    if (!g) return fail(IC_EINVAL, "null group");
+    return create_session(params, device, rank, local_group_world(g), true,
+                          [&](const char **err) -> Comm * { return make_local_comm(g, rank, device, err); }, out);
+}
+
 void ic_session_destroy(void *session)
 {
     Session *s = (Session *)session;
@@ -489,11 +774,11 @@ int ic_upload(void *session, const float *cube, const float *w0, const int32_t *
     Session *s = (Session *)session;
     if (!s || !cube || !w0 || !shift) return fail(IC_EINVAL, "null argument");
     CK(hipSetDevice(s->device));
-    for (int c = 0; c < s->p.nchan; ++c)
+    for (int c = 0; c < s->nchan; ++c)
         if (shift[c] < 0 || shift[c] >= s->p.nbin) return fail(IC_EINVAL, "shift[%d]=%d out of [0,nbin)", c, shift[c]);
     CK(hipMemcpyAsync(s->raw, cube, sizeof(float) * s->N, hipMemcpyHostToDevice, s->stream));
     CK(hipMemcpyAsync(s->w0, w0, sizeof(float) * s->P, hipMemcpyHostToDevice, s->stream));
-    CK(hipMemcpyAsync(s->shift, shift, sizeof(int32_t) * s->p.nchan, hipMemcpyHostToDevice, s->stream));
+    CK(hipMemcpyAsync(s->shift, shift, sizeof(int32_t) * s->nchan, hipMemcpyHostToDevice, s->stream));
     CK(hipStreamSynchronize(s->stream));
     s->uploaded = true;
     s->ran = false;
@@ -507,7 +792,7 @@ int ic_upload_device(void *session, const float *d_cube, const float *d_w0, cons
     CK(hipSetDevice(s->device));
     CK(hipMemcpyAsync(s->raw, d_cube, sizeof(float) * s->N, hipMemcpyDeviceToDevice, s->stream));
     CK(hipMemcpyAsync(s->w0, d_w0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
-    CK(hipMemcpyAsync(s->shift, d_shift, sizeof(int32_t) * s->p.nchan, hipMemcpyDeviceToDevice, s->stream));
+    CK(hipMemcpyAsync(s->shift, d_shift, sizeof(int32_t) * s->nchan, hipMemcpyDeviceToDevice, s->stream));
     CK(hipStreamSynchronize(s->stream));
     s->uploaded = true;
     s->ran = false;
@@ -540,15 +825,17 @@ int ic_get_kernel_times(void *session, ic_kernel_time *out, int n)
     return m;
 }
 
-int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_out, int32_t *changed_out,
-           int32_t *nzero_out, int32_t *n_iter_out, int32_t *converged_out)
+}  // extern "C"
+
+namespace {
+
+int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_out, int32_t *changed_out,
+             int32_t *nzero_out, int32_t *n_iter_out, int32_t *converged_out)
 {
-    Session *s = (Session *)session;
-    if (!s) return fail(IC_EINVAL, "null session");
     if (!s->uploaded) return fail(IC_ESTATE, "ic_run before ic_upload");
     CK(hipSetDevice(s->device));
     const ic_params &p = s->p;
-    const int nsub = p.nsub, nchan = p.nchan, nbin = p.nbin;
+    const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
     int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > nbin ? nbin : p.pr_start);
     int pr_end = p.pr_end < 0 ? 0 : (p.pr_end > nbin ? nbin : p.pr_end);
     // fit cube (ic.py:96-100) + initial weights/history; a session can be re-run
@@ -577,12 +864,17 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
                launch_diag(s->stream, s->D, s->T64, s->amp, s->info, s->w0, s->shift, s->tw, s->tw_p2, s->plan, nsub,
                            nchan, nbin, s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, s->std_, s->mean, s->ptp,
                            s->fft));
-        LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, la));
+        // channel medians are local to a shard; row medians need whole rows
+        LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, la, s->comm ? 1 : 3));
+        if (s->comm)
+            if (int rc = shard_rowstats(s, la)) return rc;
         CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t) * (p.max_iter + 4), s->stream));
         LAUNCH(s, K_COMBINE,
                launch_combine(s->stream, nsub, nchan, s->valid, s->w0, s->std_, s->mean, s->ptp, s->fft,
                               la.col_med, la.col_mad, la.row_med, la.row_mad, p.chanthresh, p.subintthresh,
                               s->test, s->W, s->hist, n_iter, s->counters));
+        if (s->comm)
+            CM(s, s->comm->allreduce_sum_i32(s->counters, (size_t)(n_iter + 2), s->stream), "convergence counters");
         CK(hipMemcpyAsync(cnt.data(), s->counters, sizeof(int32_t) * (n_iter + 2), hipMemcpyDeviceToHost,
                           s->stream));
         CK(hipStreamSynchronize(s->stream));
@@ -616,6 +908,20 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
     return IC_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_out, int32_t *changed_out,
+           int32_t *nzero_out, int32_t *n_iter_out, int32_t *converged_out)
+{
+    Session *s = (Session *)session;
+    if (!s) return fail(IC_EINVAL, "null session");
+    const int rc = run_impl(s, test_out, weights_out, loops_out, changed_out, nzero_out, n_iter_out, converged_out);
+    if (rc && s->comm) s->comm->abort();   // peers must not wait for this shard
+    return rc;
+}
+
 int ic_get_residual(void *session, float *out)
 {
     Session *s = (Session *)session;
@@ -628,7 +934,7 @@ int ic_get_residual(void *session, float *out)
     // the fit cube buffer `base` is reused as scratch? no: allocate a temporary
     float *R = nullptr;
     CK(hipMalloc((void **)&R, sizeof(float) * s->N));
-    hipError_t e = launch_residual(s->stream, s->D, s->T64, s->amp, s->info, s->shift, p.nsub, p.nchan, p.nbin,
+    hipError_t e = launch_residual(s->stream, s->D, s->T64, s->amp, s->info, s->shift, p.nsub, s->nchan, p.nbin,
                                    s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, R);
     if (e == hipSuccess) e = hipMemcpyAsync(out, R, sizeof(float) * s->N, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);

@@ -2,9 +2,16 @@
 
 C1/C2/C5 are "replicas only" and C4 is a batch of independent archives: one
 process per GPU (torchrun), each cleaning its own archives, with no collective
-on the data path.  The only cross-rank operation is the timing reduction of
-bench.py (max over ranks).  The reference processes its archive list in one
-loop (iterative_cleaner.py:59-62); ``shard`` splits that list across ranks.
+on the data path.  The reference processes its archive list in one loop
+(iterative_cleaner.py:59-62); ``shard`` splits that list across ranks.
+
+C3 (one large archive) is channel-sharded: every rank runs a shard session
+(_native.ShardSession) whose four per-iteration exchanges go through
+``TorchComm`` — the ic_comm_ops transport of the C-ABI bound to
+torch.distributed: RCCL over xGMI on the "nccl" backend, host-staged on
+"gloo" (CPU tests, several ranks sharing one GPU).  Exchange buffers are torch
+tensors owned here (PyTorch provides buffer ownership, streams and the
+process group; the loop itself runs in libicgpu.so).
 """
 from __future__ import annotations
 
@@ -41,3 +48,127 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device or "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class TorchComm:
+    """ic_comm_ops over torch.distributed for one shard session.
+
+    Collectives run in stream order on the session's HIP stream (wrapped as a
+    torch ExternalStream): the RCCL kernels wait for the shard kernels that
+    wrote the send buffers, and the kernels after them wait for the RCCL
+    kernels.  On gloo the stream is synchronised and the buffers staged through
+    host memory.  A failing collective is recorded in ``error`` and reported to
+    the C++ side as a non-zero return code (the session then fails loudly).
+    """
+
+    def __init__(self, device, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.device = torch.device(device)
+        self.group = group
+        self.backend = dist.get_backend(group)
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.bufs = {}
+        self.error = None
+        self._ops = None
+
+    # ------------------------------------------------------------ buffers
+    def alloc(self, nbytes):
+        t = self.torch.empty(max(int(nbytes), 8), dtype=self.torch.uint8, device=self.device)
+        self.bufs[t.data_ptr()] = t
+        return t
+
+    def view(self, ptr, nbytes):
+        """uint8 view of ``nbytes`` at device address ``ptr`` inside a buffer from alloc()."""
+        for base_ptr, t in self.bufs.items():
+            if base_ptr <= ptr and ptr + nbytes <= base_ptr + t.numel():
+                off = ptr - base_ptr
+                return t[off:off + nbytes]
+        raise RuntimeError("address %#x (+%d) is not an exchange buffer" % (ptr, nbytes))
+
+    # ------------------------------------------------------------ collectives on tensors
+    def _stream_ctx(self, stream):
+        import contextlib
+        if stream and self.device.type == "cuda":
+            return self.torch.cuda.stream(self.torch.cuda.ExternalStream(stream, device=self.device))
+        return contextlib.nullcontext()
+
+    def _staged(self):
+        return self.backend == "gloo" and self.device.type == "cuda"
+
+    def allgather(self, send, recv, stream=None):
+        dist = self.dist
+        with self._stream_ctx(stream):
+            if self._staged():
+                self.torch.cuda.current_stream(self.device).synchronize()
+                s_c, r_c = send.cpu(), recv.new_empty(recv.shape, device="cpu")
+                dist.all_gather(list(r_c.chunk(self.world)), s_c, group=self.group)
+                recv.copy_(r_c)
+            elif self.backend == "gloo":
+                dist.all_gather(list(recv.chunk(self.world)), send, group=self.group)
+            else:
+                dist.all_gather_into_tensor(recv, send, group=self.group)
+
+    def alltoallv(self, send, send_sizes, recv, recv_sizes, stream=None):
+        dist = self.dist
+        with self._stream_ctx(stream):
+            if self._staged():
+                self.torch.cuda.current_stream(self.device).synchronize()
+                s_c, r_c = send.cpu(), recv.new_empty(recv.shape, device="cpu")
+                dist.all_to_all_single(r_c, s_c, list(recv_sizes), list(send_sizes), group=self.group)
+                recv.copy_(r_c)
+            else:
+                dist.all_to_all_single(recv, send, list(recv_sizes), list(send_sizes), group=self.group)
+
+    def allreduce_sum(self, t, stream=None):
+        dist = self.dist
+        with self._stream_ctx(stream):
+            if self._staged():
+                self.torch.cuda.current_stream(self.device).synchronize()
+                c = t.cpu()
+                dist.all_reduce(c, group=self.group)
+                t.copy_(c)
+            else:
+                dist.all_reduce(t, group=self.group)
+
+    # ------------------------------------------------------------ C callbacks
+    def ops(self):
+        """The CommOps struct handed to ic_session_create_shard (callbacks kept alive here)."""
+        from . import _native as nat
+        if self._ops is not None:
+            return self._ops
+
+        def guard(fn):
+            def run(*a):
+                try:
+                    fn(*a)
+                    return 0
+                except Exception as e:  # reported through the C++ error path
+                    self.error = repr(e)
+                    return -1
+            return run
+
+        def c_alloc(ctx, nbytes, out):
+            out[0] = self.alloc(nbytes).data_ptr()
+
+        def c_release(ctx, ptr):
+            self.bufs.pop(ptr, None)
+
+        def c_allgather(ctx, send, recv, nbytes, stream):
+            self.allgather(self.view(send, nbytes), self.view(recv, nbytes * self.world), stream)
+
+        def c_alltoallv(ctx, send, sb, recv, rb, stream):
+            ss = [int(sb[r]) for r in range(self.world)]
+            rs = [int(rb[r]) for r in range(self.world)]
+            self.alltoallv(self.view(send, sum(ss)), ss, self.view(recv, sum(rs)), rs, stream)
+
+        def c_allreduce(ctx, buf, n, stream):
+            self.allreduce_sum(self.view(buf, 4 * n).view(self.torch.int32), stream)
+
+        self._fns = (nat.ALLOC_FN(guard(c_alloc)), nat.RELEASE_FN(guard(c_release)),
+                     nat.ALLGATHER_FN(guard(c_allgather)), nat.ALLTOALLV_FN(guard(c_alltoallv)),
+                     nat.ALLREDUCE_FN(guard(c_allreduce)))
+        self._ops = nat.CommOps(None, *self._fns)
+        return self._ops

@@ -1,0 +1,129 @@
+"""Channel-sharded cleaning of one large archive (config C3).
+
+The reference cleans an archive in one process (iterative_cleaner.py:83-146).
+Here the same loop runs as ``world`` channel shards (shards.py), each a
+libicgpu shard session; results are bit-identical to one unsharded session.
+
+* ``clean_cube_local``: all shards in this process, one host thread each, on one
+  or several devices (in-process group: device-to-device / peer copies).
+* ``clean_cube_dist``: this rank's shard under torchrun, exchanging through
+  torch.distributed (dist.TorchComm: RCCL over xGMI on "nccl"); the full test /
+  weights arrays are all-gathered so every rank returns the same dict.
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+
+from . import _native
+
+
+def _gather_cols(parts, ranges, shape, dtype):
+    out = np.empty(shape, dtype)
+    for (c0, c1), part in zip(ranges, parts):
+        out[:, c0:c1] = part
+    return out
+
+
+def _loop_kwargs(args):
+    return dict(max_iter=args.get("max_iter", 5), chanthresh=args.get("chanthresh", 5.0),
+                subintthresh=args.get("subintthresh", 5.0),
+                pulse_region=args.get("pulse_region", (0, 0, 1)),
+                baseline_duty=args.get("baseline_duty", 0.15))
+
+
+def clean_cube_local(cube, w0, shift, world, devices=None, want_details=False, fit_tail=None, **args):
+    """Clean a (nsub, nchan, nbin) f32 cube as `world` in-process channel shards.
+    Returns the ic_run dict with full-archive ``test`` / ``weights`` (and, with
+    want_details, ``amp``, ``info``, ``std``, ``mean``, ``ptp``, ``fft``, ``T``)."""
+    nsub, nchan, nbin = cube.shape
+    devices = list(devices) if devices is not None else [0] * world
+    if len(devices) != world:
+        raise ValueError("need one device per shard")
+    chans, _ = _native.shard_layout(nsub, nchan, world)
+    kw = _loop_kwargs(args)
+    results = [None] * world
+    errors = []
+    with _native.ShardGroup(world) as group:
+        sessions = [_native.ShardSession(nsub, nchan, nbin, r, world, group=group, device=devices[r], **kw)
+                    for r in range(world)]
+        try:
+            for r, s in enumerate(sessions):
+                c0, c1 = chans[r]
+                if fit_tail is not None:
+                    s.set_fit_tail(fit_tail)
+                s.upload(cube[:, c0:c1], w0[:, c0:c1], np.asarray(shift)[c0:c1])
+
+            def work(r):
+                try:
+                    s = sessions[r]
+                    out = s.run()
+                    if want_details and out["n_iter"] > 0:
+                        out["amp"], out["info"] = s.fit()
+                        out["std"], out["mean"], out["ptp"], out["fft"] = s.diagnostics()
+                        out["T"] = s.template()
+                    results[r] = out
+                except Exception as e:  # noqa: BLE001 - re-raised below
+                    errors.append((r, e))
+
+            threads = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join()
+        finally:
+            for s in sessions:
+                s.close()
+    if errors:
+        r, e = errors[0]
+        raise _native.NativeError("shard %d failed: %s" % (r, e))
+    return _merge(results, chans, (nsub, nchan), want_details)
+
+
+def _merge(results, chans, shape2, want_details):
+    first = results[0]
+    for r, out in enumerate(results[1:], 1):
+        for key in ("loops", "n_iter", "converged"):
+            if out[key] != first[key]:
+                raise _native.NativeError("shard %d disagrees on %s" % (r, key))
+        if not (np.array_equal(out["changed"], first["changed"])
+                and np.array_equal(out["nzero"], first["nzero"])):
+            raise _native.NativeError("shard %d disagrees on the convergence counters" % r)
+    merged = dict(first)
+    merged["test"] = _gather_cols([o["test"] for o in results], chans, shape2, np.float64)
+    merged["weights"] = _gather_cols([o["weights"] for o in results], chans, shape2, np.float32)
+    if want_details and "amp" in first:
+        for key, dt in (("amp", np.float64), ("info", np.int32), ("std", np.float64),
+                        ("mean", np.float64), ("ptp", np.float32), ("fft", np.float64)):
+            merged[key] = _gather_cols([o[key] for o in results], chans, shape2, dt)
+        for r, o in enumerate(results[1:], 1):
+            if o["T"].tobytes() != first["T"].tobytes():
+                raise _native.NativeError("shard %d has a different template" % r)
+    return merged
+
+
+def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, group=None, **args):
+    """This rank's channel shard of one archive under torch.distributed.
+    `cube_slice` etc. are the rank's channel range (``_native.shard_layout``);
+    returns the merged full-archive dict on every rank."""
+    import torch.distributed as dist
+
+    from .dist import TorchComm
+    nsub, nchan, nbin = global_shape
+    comm = TorchComm(device, group)
+    world, rank = comm.world, comm.rank
+    chans, _ = _native.shard_layout(nsub, nchan, world)
+    with _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm,
+                              device=_device_index(device), **_loop_kwargs(args)) as s:
+        s.upload(cube_slice, w0_slice, shift_slice)
+        out = s.run()
+    every = [None] * world
+    dist.all_gather_object(every, out, group=group)
+    return _merge(every, chans, (nsub, nchan), False)
+
+
+def _device_index(device):
+    import torch
+    d = torch.device(device)
+    return d.index if d.index is not None else 0

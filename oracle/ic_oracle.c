@@ -28,6 +28,17 @@
 
 #define SUPER_BLOCK 256
 
+/* Canonical combine of super-block partials p[lo*stride], .. p[(hi-1)*stride]
+ * (archive.py sb_tree): halving tree, mid = lo + (hi - lo) / 2. */
+static double sb_tree1(const double *p, size_t stride, int lo, int hi)
+{
+    if (hi - lo == 1) return p[(size_t)lo * stride];
+    int mid = lo + (hi - lo) / 2;
+    double a = sb_tree1(p, stride, lo, mid);
+    double b = sb_tree1(p, stride, mid, hi);
+    return a + b;
+}
+
 /* ------------------------------------------------------------------ enorm */
 /* MINPACK enorm (sequential, three-accumulator scaled sum of squares).      */
 static double enorm_d(int n, const double *x)
@@ -342,20 +353,21 @@ void orc_baseline(int nsub, int nchan, int n, const float *raw, const float *W,
 {
     int width = (int)(duty * (double)n);
     if (width < 1) width = 1;
+    const int nsb = (nchan + SUPER_BLOCK - 1) / SUPER_BLOCK;
     double *tot = (double *)malloc(sizeof(double) * (size_t)n);
-    double *part = (double *)malloc(sizeof(double) * (size_t)n);
+    double *part = (double *)malloc(sizeof(double) * (size_t)n * nsb);
     for (int s = 0; s < nsub; ++s) {
-        for (int i = 0; i < n; ++i) tot[i] = 0.0;
         for (int b0 = 0; b0 < nchan; b0 += SUPER_BLOCK) {
-            for (int i = 0; i < n; ++i) part[i] = 0.0;
+            double *pb = part + (size_t)(b0 / SUPER_BLOCK) * n;
+            for (int i = 0; i < n; ++i) pb[i] = 0.0;
             int b1 = b0 + SUPER_BLOCK < nchan ? b0 + SUPER_BLOCK : nchan;
             for (int c = b0; c < b1; ++c) {
                 const float *prof = raw + ((size_t)s * nchan + c) * n;
                 double w = (double)W[(size_t)s * nchan + c];
-                for (int i = 0; i < n; ++i) part[i] = part[i] + w * (double)ded_at(prof, n, shift[c], i);
+                for (int i = 0; i < n; ++i) pb[i] = pb[i] + w * (double)ded_at(prof, n, shift[c], i);
             }
-            for (int i = 0; i < n; ++i) tot[i] = tot[i] + part[i];
         }
+        for (int i = 0; i < n; ++i) tot[i] = sb_tree1(part + i, (size_t)n, 0, nsb);
         /* first argmin of circular window sums, numpy NaN semantics */
         int best = 0;
         double bestv = 0.0;
@@ -405,30 +417,32 @@ void orc_template(int nsub, int nchan, int n, const float *raw, const float *W,
 {
     float *base = (float *)malloc(sizeof(float) * (size_t)nsub * nchan);
     orc_baseline(nsub, nchan, n, raw, W, shift, duty, base, NULL);
+    const int nsb = (nchan + SUPER_BLOCK - 1) / SUPER_BLOCK;
     double *num = (double *)malloc(sizeof(double) * (size_t)n);
-    double *part = (double *)malloc(sizeof(double) * (size_t)n);
+    double *part = (double *)malloc(sizeof(double) * (size_t)n * nsb);
+    double *wpart = (double *)malloc(sizeof(double) * (size_t)nsb);
     float *F = (float *)malloc(sizeof(float) * (size_t)nsub * n);
     float *wf = (float *)malloc(sizeof(float) * (size_t)nsub);
     for (int s = 0; s < nsub; ++s) {
-        double wsum = 0.0;
-        for (int i = 0; i < n; ++i) num[i] = 0.0;
         for (int b0 = 0; b0 < nchan; b0 += SUPER_BLOCK) {
             int b1 = b0 + SUPER_BLOCK < nchan ? b0 + SUPER_BLOCK : nchan;
-            double wpart = 0.0;
-            for (int i = 0; i < n; ++i) part[i] = 0.0;
+            double *pb = part + (size_t)(b0 / SUPER_BLOCK) * n;
+            double wp = 0.0;
+            for (int i = 0; i < n; ++i) pb[i] = 0.0;
             for (int c = b0; c < b1; ++c) {
                 const float *prof = raw + ((size_t)s * nchan + c) * n;
                 double w = (double)W[(size_t)s * nchan + c];
                 float b = base[(size_t)s * nchan + c];
-                wpart = wpart + w;
+                wp = wp + w;
                 for (int i = 0; i < n; ++i) {
                     float y = ded_at(prof, n, shift[c], i) - b;
-                    part[i] = part[i] + w * (double)y;
+                    pb[i] = pb[i] + w * (double)y;
                 }
             }
-            wsum = wsum + wpart;
-            for (int i = 0; i < n; ++i) num[i] = num[i] + part[i];
+            wpart[b0 / SUPER_BLOCK] = wp;
         }
+        const double wsum = sb_tree1(wpart, 1, 0, nsb);
+        for (int i = 0; i < n; ++i) num[i] = sb_tree1(part + i, (size_t)n, 0, nsb);
         for (int i = 0; i < n; ++i) F[(size_t)s * n + i] = (wsum != 0.0) ? (float)(num[i] / wsum) : 0.0f;
         wf[s] = (float)wsum;
     }
@@ -443,7 +457,7 @@ void orc_template(int nsub, int nchan, int n, const float *raw, const float *W,
         float t = (wt != 0.0) ? (float)(num[i] / wt) : 0.0f;
         T[i] = t * 10000.0f;
     }
-    free(base); free(num); free(part); free(F); free(wf);
+    free(base); free(num); free(part); free(wpart); free(F); free(wf);
 }
 
 /* ------------------------------------------------------ pairwise sums */

@@ -26,17 +26,43 @@ def test_dedisperse_roundtrip():
     assert np.array_equal(ar.get_data(), data)
 
 
-def test_chan_sum_order_is_superblock_sequential():
+def test_chan_sum_order_is_superblock_tree():
+    """Sequential inside 256-channel super-blocks, partials by the halving tree:
+    7 super-blocks -> (p0 + (p1 + p2)) + ((p3 + p4) + (p5 + p6))."""
     from iterative_cleaner_amd.archive import SUPER_BLOCK, chan_sum
     rng = np.random.default_rng(0)
-    t = rng.standard_normal(600) * 10.0 ** rng.uniform(-8, 8, 600)
-    want = 0.0
-    for b0 in range(0, 600, SUPER_BLOCK):
+    n = 7 * SUPER_BLOCK - 100
+    t = rng.standard_normal(n) * 10.0 ** rng.uniform(-8, 8, n)
+    p = []
+    for b0 in range(0, n, SUPER_BLOCK):
         part = 0.0
-        for c in range(b0, min(600, b0 + SUPER_BLOCK)):
+        for c in range(b0, min(n, b0 + SUPER_BLOCK)):
             part = part + t[c]
-        want = want + part
+        p.append(part)
+    assert len(p) == 7
+    want = (p[0] + (p[1] + p[2])) + ((p[3] + p[4]) + (p[5] + p[6]))
     assert chan_sum(t, 0) == want
+    assert chan_sum(t[:SUPER_BLOCK], 0) == p[0]
+
+
+@pytest.mark.parametrize("nsb", [1, 2, 3, 5, 8, 13, 32, 64])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_sb_tree_shards_reproduce_single(nsb, world):
+    """2^d shards each own one depth-d node of the tree; combining their roots
+    with the same tree over `world` leaves gives the single-device bits."""
+    from iterative_cleaner_amd.archive import sb_tree
+    from iterative_cleaner_amd.shards import channel_shards
+    if nsb < world:
+        with pytest.raises(ValueError):
+            channel_shards(nsb * 256, world)
+        return
+    rng = np.random.default_rng(nsb * 10 + world)
+    parts = list(rng.standard_normal(nsb) * 10.0 ** rng.uniform(-12, 12, nsb))
+    ranges = channel_shards(nsb * 256 - 17, world)
+    roots = [sb_tree(parts[c0 // 256:(c1 + 255) // 256]) for c0, c1 in ranges]
+    assert sb_tree(roots) == sb_tree(parts)
+    assert ranges[0][0] == 0 and ranges[-1][1] == nsb * 256 - 17
+    assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
 
 
 def test_window_argmin_nan_and_ties():
