@@ -83,14 +83,19 @@ def _output_name(ar, args):
 def main(args):
     """CLI driver (iterative_cleaner.py:59-62).  Under torchrun each rank cleans
     its round-robin share of the archive list on its own GPU (batch mode,
-    SURVEY.md §8(e): no collective)."""
-    from .dist import rank_world, shard
+    SURVEY.md §8(e): no collective).  With IC_CHANNEL_SHARDS=1 the ranks instead
+    clean every archive together, each on its channel shard (config C3), and
+    rank 0 writes the outputs."""
+    from .dist import channel_sharding, rank_world, shard
     rank, world, _ = rank_world()
     backend = archive_backend()
-    for arch in shard(args.archive, rank, world):
+    together = channel_sharding()
+    for arch in (args.archive if together else shard(args.archive, rank, world)):
         ar = backend.Archive_load(arch)
         o_name = _output_name(ar, args)
         ar = clean(ar, args, arch)
+        if together and rank != 0:
+            continue
         ar.unload(o_name)
         if not args.quiet:
             print("Cleaned archive: %s" % o_name)
@@ -130,8 +135,24 @@ def _device() -> int:
 
 def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15):
     """Run the GPU loop on a (nsub, nchan, nbin) f32 cube; returns the ic_run dict
-    (+ ``residual`` when requested)."""
+    (+ ``residual`` when requested).  Under channel sharding (dist.channel_sharding)
+    every rank runs its channel shard and gets the merged result."""
     nsub, nchan, nbin = cube.shape
+    from .dist import channel_sharding
+    if channel_sharding():
+        import torch
+
+        from . import sharded
+        from .dist import rank_world
+        rank, world, local = rank_world()
+        chans, _ = _native.shard_layout(nsub, nchan, world)
+        c0, c1 = chans[rank]
+        dev = torch.device("cuda", _device() if device is None else device)
+        return sharded.clean_cube_dist(
+            np.ascontiguousarray(cube[:, c0:c1]), np.ascontiguousarray(np.asarray(w0)[:, c0:c1]),
+            np.asarray(shift)[c0:c1], (nsub, nchan, nbin), dev, want_residual=want_residual,
+            max_iter=args.max_iter, chanthresh=args.chanthresh, subintthresh=args.subintthresh,
+            pulse_region=args.pulse_region, baseline_duty=baseline_duty)
     with _native.GpuSession(nsub, nchan, nbin, args.max_iter, args.chanthresh, args.subintthresh,
                             args.pulse_region, baseline_duty,
                             device=_device() if device is None else device) as s:
@@ -186,7 +207,14 @@ def _plot_zap(test, ar_name, args):
 
 
 def clean(ar, args, arch):
-    """Surgical cleaning of one archive (iterative_cleaner.py:65-178)."""
+    """Surgical cleaning of one archive (iterative_cleaner.py:65-178).  Under
+    channel sharding only rank 0 prints and writes files."""
+    from .dist import channel_sharding, rank_world
+    if channel_sharding() and rank_world()[0] != 0:
+        args = argparse.Namespace(**dict(vars(args), quiet=True, no_log=True, print_zap=False))
+        _side_effects = False
+    else:
+        _side_effects = True
     backend = archive_backend()
     orig_weights = ar.get_weights()
     if not (args.memory and not args.pscrunch):
@@ -230,7 +258,7 @@ def clean(ar, args, arch):
     set_weights_archive(ar, avg_test_results)
     if args.bad_chan != 1 or args.bad_subint != 1:
         ar = find_bad_parts(ar, args)
-    if args.unload_res:
+    if args.unload_res and _side_effects:
         _residual_archive(ar, out["residual"], orig_weights, shift, backend).unload(
             "%s_residual_%s.ar" % (ar_name, loops))
     if args.print_zap:

@@ -31,6 +31,28 @@ def rank_world() -> tuple[int, int, int]:
     return rank, world, local
 
 
+def channel_sharding() -> bool:
+    """True when the CLI should clean each archive as channel shards across the
+    torchrun ranks (IC_CHANNEL_SHARDS=1 and WORLD_SIZE > 1).  The process group
+    ("nccl": RCCL over xGMI; IC_SHARD_BACKEND=gloo for several ranks on one GPU)
+    is created on first use."""
+    if os.environ.get("IC_CHANNEL_SHARDS", "0") in ("", "0"):
+        return False
+    rank, world, local = rank_world()
+    if world == 1:
+        return False
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        backend = os.environ.get("IC_SHARD_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return True
+
+
 def shard(items: Sequence[T], rank: int, world: int) -> list[T]:
     """Round-robin share of ``items`` for ``rank`` (disjoint, covers every item once,
     keeps the reference's processing order within a rank)."""

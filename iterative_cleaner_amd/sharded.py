@@ -103,10 +103,12 @@ def _merge(results, chans, shape2, want_details):
     return merged
 
 
-def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, group=None, **args):
+def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, group=None,
+                    want_residual=False, **args):
     """This rank's channel shard of one archive under torch.distributed.
     `cube_slice` etc. are the rank's channel range (``_native.shard_layout``);
-    returns the merged full-archive dict on every rank."""
+    returns the merged full-archive dict on every rank (with want_residual, the
+    full residual cube on rank 0 only)."""
     import torch.distributed as dist
 
     from .dist import TorchComm
@@ -118,9 +120,19 @@ def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, gro
                               device=_device_index(device), **_loop_kwargs(args)) as s:
         s.upload(cube_slice, w0_slice, shift_slice)
         out = s.run()
+        res = s.residual() if want_residual and out["n_iter"] > 0 else None
     every = [None] * world
     dist.all_gather_object(every, out, group=group)
-    return _merge(every, chans, (nsub, nchan), False)
+    merged = _merge(every, chans, (nsub, nchan), False)
+    if want_residual:
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object(res, parts, dst=0, group=group)
+        if rank == 0 and merged["n_iter"] > 0:
+            R = np.empty((nsub, nchan, nbin), np.float32)
+            for (c0, c1), part in zip(chans, parts):
+                R[:, c0:c1] = part
+            merged["residual"] = R
+    return merged
 
 
 def _device_index(device):
