@@ -25,7 +25,8 @@ import os
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SOURCES = ("iterative_cleaner_amd/csrc/ic_kernels.hip", "iterative_cleaner_amd/csrc/ic_session.hip",
-           "iterative_cleaner_amd/csrc/ic_internal.h")
+           "iterative_cleaner_amd/csrc/ic_internal.h", "iterative_cleaner_amd/csrc/ic_comm.hip",
+           "iterative_cleaner_amd/csrc/ic_comm.h")
 
 
 def source_sha() -> str:
