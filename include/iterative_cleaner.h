@@ -73,6 +73,20 @@ int ic_upload(void *session, const float *cube, const float *w0, const int32_t *
 int ic_upload_device(void *session, const float *d_cube, const float *d_w0,
                      const int32_t *d_shift);
 
+/* Batch pipelining (config C4: many archives of one shape per GPU).  Queue the
+ * host->device copy of the NEXT archive on the session's copy stream and return
+ * at once; the next ic_run waits for the copy and cleans that archive.  Two input
+ * slots: at most two uploads may be pending, so the pattern
+ *     ic_upload_async(a0); for k: { ic_upload_async(a[k+1]); ic_run(); }
+ * overlaps every archive's copy with the previous archive's cleaning.  The host
+ * arrays of an upload must stay untouched until the ic_run that consumes it
+ * returns, and must be page-locked (ic_host_alloc) for the copy to overlap.
+ * ic_upload / ic_upload_device fail with IC_ESTATE while uploads are pending.
+ * Replaces the per-archive reload of iterative_cleaner.py:60 (main loop). */
+int ic_upload_async(void *session, const float *cube, const float *w0, const int32_t *shift);
+int ic_host_alloc(size_t bytes, void **ptr);
+void ic_host_free(void *ptr);
+
 /* Run the cleaning loop to convergence or max_iter (iterative_cleaner.py:83-146).
  * Outputs (host, any may be NULL):
  *   test_out        [nsub*nchan] f64 : avg_test_results of the last loop (:120)

@@ -20,7 +20,7 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_get_fit", "ic_get_diagnostics", "ic_get_kernel_times", "ic_kernel_name",
            "ic_set_timing", "ic_get_run_stats", "ic_set_fit_tail", "ic_last_error",
            "ic_shard_layout", "ic_session_create_shard", "ic_group_create", "ic_group_destroy",
-           "ic_session_create_grouped")
+           "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free")
 
 
 class NativeError(RuntimeError):
@@ -114,6 +114,10 @@ def load_library(path: str = LIB_PATH):
     lib.ic_set_timing.argtypes = [vp, C.c_int]
     lib.ic_get_run_stats.argtypes = [vp, C.POINTER(RunStats)]
     lib.ic_set_fit_tail.argtypes = [vp, C.c_int64]
+    lib.ic_upload_async.argtypes = [vp, vp, vp, vp]
+    lib.ic_host_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
+    lib.ic_host_free.argtypes = [vp]
+    lib.ic_host_free.restype = None
     lib.ic_shard_layout.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
     lib.ic_session_create_shard.argtypes = [C.POINTER(Params), C.c_int, C.c_int, C.c_int,
                                             C.POINTER(CommOps), C.POINTER(vp)]
@@ -205,6 +209,16 @@ class GpuSession:
         shift = np.ascontiguousarray(np.mod(shift, nbin), dtype=np.int32).reshape(nchan)
         self._check(self.lib.ic_upload(self.h, _ptr(cube), _ptr(w0), _ptr(shift)), "ic_upload")
 
+    def upload_async(self, cube, w0, shift):
+        """Queue the copy of the next archive (see ic_upload_async); the arrays
+        must stay alive and unmodified until the run() that consumes them returns."""
+        nsub, nchan, nbin = self.shape
+        for a, shape, dt in ((cube, (nsub, nchan, nbin), np.float32), (w0, (nsub, nchan), np.float32),
+                             (shift, (nchan,), np.int32)):
+            if a.dtype != dt or a.shape != shape or not a.flags.c_contiguous:
+                raise ValueError("upload_async needs C-contiguous %s %s arrays" % (dt.__name__, shape))
+        self._check(self.lib.ic_upload_async(self.h, _ptr(cube), _ptr(w0), _ptr(shift)), "ic_upload_async")
+
     def upload_device(self, cube_ptr: int, w0_ptr: int, shift_ptr: int):
         """Device pointers (e.g. torch tensor .data_ptr()) on this session's GPU."""
         self._check(self.lib.ic_upload_device(self.h, C.c_void_p(cube_ptr), C.c_void_p(w0_ptr),
@@ -274,6 +288,34 @@ class GpuSession:
             name = self.lib.ic_kernel_name(buf[q].kernel).decode()
             out[name] = dict(ms=buf[q].ms, launches=buf[q].launches)
         return out
+
+
+class PinnedArray:
+    """Page-locked host memory (ic_host_alloc) viewed as a numpy array, so that
+    ic_upload_async copies overlap the cleaning of the previous archive."""
+
+    def __init__(self, shape, dtype=np.float32):
+        self.lib = load_library()
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        p = C.c_void_p()
+        if self.lib.ic_host_alloc(n, C.byref(p)) != 0:
+            raise NativeError("ic_host_alloc: %s" % _err(self.lib))
+        self.ptr = p
+        buf = (C.c_char * max(n, 1)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dt, count=int(np.prod(shape))).reshape(shape)
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            self.lib.ic_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------- channel shards

@@ -1637,7 +1637,7 @@ __global__ __launch_bounds__(256) void k_diag(
 }
 
 // ---------------------------------------------------------------------------
-// k_diag_p2<N>: the same diagnostics for power-of-two nbin = N (64..2048).
+// k_diag_p2<N>: the same diagnostics for power-of-two nbin = N (64..4096).
 // numpy's pairwise sum for N = 2^k is a balanced tree over leaves of
 // min(N,128) samples, each leaf 8 strided chains of min(N,128)/8 samples:
 // chain c = (leaf c/8, accumulator c%8) lives in lane c%64, slot c/64, and the
@@ -1661,6 +1661,10 @@ struct P2 {
     static constexpr int WAVE_BYTES = XBYTES > CBYTES ? XBYTES : CBYTES;
     static constexpr int LG = __builtin_ctz(M);
     static constexpr int TW = 2 * M;   // twiddle entries: M post-processing + <= M stage tables
+    // N >= 4096: the 64-KiB table would cut a CU to two waves; read it through
+    // L1/L2 instead and keep the LDS for the per-wave work arrays (32 KiB each)
+    static constexpr bool TWG = N >= 4096;
+    static constexpr int TW_LDS = TWG ? 0 : TW;
 };
 
 __device__ __forceinline__ int xaddr(int idx) { return idx + 8 * (idx >> 7); }
@@ -1747,7 +1751,7 @@ __device__ __forceinline__ void p2_fft(double2 *C, const float *X, double mu, co
 }
 
 template <int N>
-__global__ __launch_bounds__(512) void k_diag_p2(
+__global__ __launch_bounds__(N >= 4096 ? 256 : 512) void k_diag_p2(
     const float *__restrict__ D, const double *__restrict__ T64g, const double *__restrict__ amp,
     const int32_t *__restrict__ info, const float *__restrict__ w0, const int32_t *__restrict__ shift,
     const double2 *__restrict__ tw_g, int nsub, int nchan, int ldD, int pr_on, double pr_factor,
@@ -1756,14 +1760,17 @@ __global__ __launch_bounds__(512) void k_diag_p2(
 {
     using C = P2<N>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double2 *tw = (double2 *)smem;   // [M] post-processing twiddles, then the stage tables
+    // [M] post-processing twiddles, then the stage tables (LDS copy unless TWG)
+    const double2 *tw = C::TWG ? tw_g : (const double2 *)smem;
     const double *T = T64g;          // L1/L2-resident, read coalesced
     const int wpb = blockDim.x >> 6;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    for (int q = threadIdx.x; q < C::TW; q += blockDim.x) tw[q] = tw_g[q];
-    __syncthreads();
-    unsigned char *wb = smem + (size_t)C::TW * 16 + (size_t)wave * C::WAVE_BYTES;
+    if (!C::TWG) {
+        for (int q = threadIdx.x; q < C::TW; q += blockDim.x) ((double2 *)smem)[q] = tw_g[q];
+        __syncthreads();
+    }
+    unsigned char *wb = smem + (size_t)C::TW_LDS * 16 + (size_t)wave * C::WAVE_BYTES;
     float *X = (float *)wb;
     double2 *Cb = (double2 *)wb;   // aliases X after the first FFT stage has read it
     const unsigned P = (unsigned)nsub * (unsigned)nchan;
@@ -2556,8 +2563,8 @@ hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const 
 {
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
-        const size_t fixed = (size_t)P2<NN>::TW * 16;                                               \
-        int wpb = 8;                                                                               \
+        const size_t fixed = (size_t)P2<NN>::TW_LDS * 16;                                           \
+        int wpb = NN >= 4096 ? 4 : 8;                                                              \
         while (wpb > 1 && fixed + wpb * (size_t)P2<NN>::WAVE_BYTES > 150 * 1024) --wpb;            \
         const size_t shm = fixed + wpb * (size_t)P2<NN>::WAVE_BYTES;                               \
         const size_t P = (size_t)nsub * nchan;                                                     \
@@ -2567,7 +2574,7 @@ hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const 
                            mean_o, ptp_o, fft_o);                                                  \
         return hipGetLastError();                                                                  \
     }
-    IC_P2(64) IC_P2(128) IC_P2(256) IC_P2(512) IC_P2(1024) IC_P2(2048)
+    IC_P2(64) IC_P2(128) IC_P2(256) IC_P2(512) IC_P2(1024) IC_P2(2048) IC_P2(4096)
 #undef IC_P2
     // nleaf/nops upper bound from nbin: leaves >= 64 samples except tiny n
     const int nleaf_ub = nbin <= 128 ? 1 : (nbin / 64 + 1);

@@ -84,6 +84,14 @@ struct Session {
     uint8_t *valid_r = nullptr;
     // device buffers
     float *raw = nullptr, *D = nullptr, *w0 = nullptr, *W = nullptr, *base = nullptr, *base0 = nullptr;
+    // input slots (raw/w0/shift alias slot `cur`); slot 1 is allocated by the first
+    // ic_upload_async that needs it.  Pending async uploads queue in `fifo`.
+    float *slot_raw[2] = {nullptr, nullptr}, *slot_w0[2] = {nullptr, nullptr};
+    int32_t *slot_shift[2] = {nullptr, nullptr};
+    hipEvent_t slot_ev[2] = {nullptr, nullptr};
+    hipStream_t copy_stream = nullptr;
+    int cur = 0, fifo[2] = {0, 0}, fifo_n = 0;
+    bool ever_uploaded = false;
     float *F = nullptr, *wf = nullptr, *T = nullptr, *ptp = nullptr, *hist = nullptr;
     uint8_t *valid = nullptr;
     int32_t *shift = nullptr, *win = nullptr, *wflag = nullptr, *info = nullptr, *counters = nullptr;
@@ -215,8 +223,15 @@ int collect_timing(Session *s)
 
 void free_all(Session *s)
 {
-    void *bufs[] = {s->raw,  s->D,     s->w0,   s->W,   s->base, s->base0, s->F,   s->wf,
-                    s->T,    s->ptp,   s->hist, s->valid, s->shift, s->win, s->info, s->comm ? nullptr : s->counters,
+    for (int q = 0; q < 2; ++q) {
+        void *sb[] = {s->slot_raw[q], s->slot_w0[q], s->slot_shift[q]};
+        for (void *b : sb)
+            if (b) (void)hipFree(b);
+        if (s->slot_ev[q]) (void)hipEventDestroy(s->slot_ev[q]);
+    }
+    if (s->copy_stream) (void)hipStreamDestroy(s->copy_stream);
+    void *bufs[] = {s->D,     s->W,   s->base, s->base0, s->F,   s->wf,
+                    s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
                     s->wflag};
@@ -601,16 +616,19 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         return bail(fail(IC_EHIP, "hipStreamCreate failed"));
     const size_t P = s->P, N = s->N;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
-    AL(s->raw, N);
+    AL(s->slot_raw[0], N);
+    s->raw = s->slot_raw[0];
     AL(s->D, s->Ppad * (size_t)s->ldD);
     if (hipMemset(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD) != hipSuccess)
         return bail(fail(IC_EHIP, "hipMemset(D) failed"));
-    AL(s->w0, P);
+    AL(s->slot_w0[0], P);
+    s->w0 = s->slot_w0[0];
     AL(s->W, P);
     AL(s->base, P);
     AL(s->base0, P);
     AL(s->valid, P);
-    AL(s->shift, (size_t)nchan);
+    AL(s->slot_shift[0], (size_t)nchan);
+    s->shift = s->slot_shift[0];
     AL(s->win, (size_t)nsub);
     AL(s->wflag, (size_t)nsub + 1);   // + window-moves counter
     AL(s->part, (size_t)nsub * s->nsb * nbin);
@@ -773,9 +791,11 @@ int ic_upload(void *session, const float *cube, const float *w0, const int32_t *
 {
     Session *s = (Session *)session;
     if (!s || !cube || !w0 || !shift) return fail(IC_EINVAL, "null argument");
+    if (s->fifo_n) return fail(IC_ESTATE, "ic_upload with %d asynchronous upload(s) pending", s->fifo_n);
     CK(hipSetDevice(s->device));
     for (int c = 0; c < s->nchan; ++c)
         if (shift[c] < 0 || shift[c] >= s->p.nbin) return fail(IC_EINVAL, "shift[%d]=%d out of [0,nbin)", c, shift[c]);
+    s->ever_uploaded = true;
     CK(hipMemcpyAsync(s->raw, cube, sizeof(float) * s->N, hipMemcpyHostToDevice, s->stream));
     CK(hipMemcpyAsync(s->w0, w0, sizeof(float) * s->P, hipMemcpyHostToDevice, s->stream));
     CK(hipMemcpyAsync(s->shift, shift, sizeof(int32_t) * s->nchan, hipMemcpyHostToDevice, s->stream));
@@ -789,7 +809,9 @@ int ic_upload_device(void *session, const float *d_cube, const float *d_w0, cons
 {
     Session *s = (Session *)session;
     if (!s || !d_cube || !d_w0 || !d_shift) return fail(IC_EINVAL, "null argument");
+    if (s->fifo_n) return fail(IC_ESTATE, "ic_upload_device with %d asynchronous upload(s) pending", s->fifo_n);
     CK(hipSetDevice(s->device));
+    s->ever_uploaded = true;
     CK(hipMemcpyAsync(s->raw, d_cube, sizeof(float) * s->N, hipMemcpyDeviceToDevice, s->stream));
     CK(hipMemcpyAsync(s->w0, d_w0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
     CK(hipMemcpyAsync(s->shift, d_shift, sizeof(int32_t) * s->nchan, hipMemcpyDeviceToDevice, s->stream));
@@ -797,6 +819,47 @@ int ic_upload_device(void *session, const float *d_cube, const float *d_w0, cons
     s->uploaded = true;
     s->ran = false;
     return IC_OK;
+}
+
+int ic_upload_async(void *session, const float *cube, const float *w0, const int32_t *shift)
+{
+    Session *s = (Session *)session;
+    if (!s || !cube || !w0 || !shift) return fail(IC_EINVAL, "null argument");
+    if (s->fifo_n == 2) return fail(IC_ESTATE, "two asynchronous uploads already pending (run one first)");
+    for (int c = 0; c < s->nchan; ++c)
+        if (shift[c] < 0 || shift[c] >= s->p.nbin) return fail(IC_EINVAL, "shift[%d]=%d out of [0,nbin)", c, shift[c]);
+    CK(hipSetDevice(s->device));
+    // the slot not holding the newest data: after the queued upload, else after the current archive
+    const int target = s->fifo_n ? 1 - s->fifo[s->fifo_n - 1] : (s->ever_uploaded ? 1 - s->cur : s->cur);
+    if (!s->slot_raw[target]) {
+        if (dalloc(&s->slot_raw[target], s->N) != hipSuccess || dalloc(&s->slot_w0[target], s->P) != hipSuccess ||
+            dalloc(&s->slot_shift[target], (size_t)s->nchan) != hipSuccess)
+            return fail(IC_ENOMEM, "second input slot (%zu bytes) failed", sizeof(float) * (s->N + s->P));
+    }
+    if (!s->copy_stream) CK(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));
+    if (!s->slot_ev[target]) CK(hipEventCreateWithFlags(&s->slot_ev[target], hipEventDisableTiming));
+    CK(hipMemcpyAsync(s->slot_raw[target], cube, sizeof(float) * s->N, hipMemcpyHostToDevice, s->copy_stream));
+    CK(hipMemcpyAsync(s->slot_w0[target], w0, sizeof(float) * s->P, hipMemcpyHostToDevice, s->copy_stream));
+    CK(hipMemcpyAsync(s->slot_shift[target], shift, sizeof(int32_t) * s->nchan, hipMemcpyHostToDevice,
+                      s->copy_stream));
+    CK(hipEventRecord(s->slot_ev[target], s->copy_stream));
+    s->fifo[s->fifo_n++] = target;
+    s->ever_uploaded = true;
+    return IC_OK;
+}
+
+int ic_host_alloc(size_t bytes, void **ptr)
+{
+    if (!ptr) return fail(IC_EINVAL, "null argument");
+    *ptr = nullptr;
+    if (hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess || !*ptr)
+        return fail(IC_ENOMEM, "hipHostMalloc(%zu) failed", bytes);
+    return IC_OK;
+}
+
+void ic_host_free(void *ptr)
+{
+    if (ptr) (void)hipHostFree(ptr);
 }
 
 int ic_set_timing(void *session, int enabled)
@@ -832,8 +895,20 @@ namespace {
 int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_out, int32_t *changed_out,
              int32_t *nzero_out, int32_t *n_iter_out, int32_t *converged_out)
 {
-    if (!s->uploaded) return fail(IC_ESTATE, "ic_run before ic_upload");
     CK(hipSetDevice(s->device));
+    if (s->fifo_n) {   // the oldest asynchronous upload becomes the current archive
+        const int slot = s->fifo[0];
+        s->fifo[0] = s->fifo[1];
+        --s->fifo_n;
+        CK(hipStreamWaitEvent(s->stream, s->slot_ev[slot], 0));
+        s->cur = slot;
+        s->raw = s->slot_raw[slot];
+        s->w0 = s->slot_w0[slot];
+        s->shift = s->slot_shift[slot];
+        s->uploaded = true;
+        s->ran = false;
+    }
+    if (!s->uploaded) return fail(IC_ESTATE, "ic_run before ic_upload");
     const ic_params &p = s->p;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
     int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > nbin ? nbin : p.pr_start);

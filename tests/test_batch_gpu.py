@@ -1,0 +1,76 @@
+"""GPU tests of the batch scheduler (config C4): archives cleaned through the
+double-buffered asynchronous uploads (ic_upload_async) and the page-locked
+staging ring must give exactly the results of one synchronous session per
+archive, in order; misuse of the upload queue fails loudly."""
+import numpy as np
+import pytest
+
+from helpers import bits_equal
+
+pytestmark = pytest.mark.gpu
+
+SHAPE = (6, 96, 128)
+
+
+def _archives(n):
+    from iterative_cleaner_amd import synth
+    out = []
+    for k in range(n):
+        data, w0, shift = synth.make_cube(*SHAPE, seed=200 + k, rfi_frac=0.1 + 0.05 * (k % 3))
+        out.append((np.ascontiguousarray(data[:, 0]), w0, shift))
+    return out
+
+
+def _one(cube, w0, shift):
+    from iterative_cleaner_amd import _native
+    with _native.GpuSession(*SHAPE, device=0) as s:
+        s.upload(cube, w0, shift)
+        return s.run()
+
+
+def test_clean_batch_matches_single_sessions():
+    from iterative_cleaner_amd import batch
+    arcs = _archives(7)
+    got = list(batch.clean_batch(iter(arcs), SHAPE, device=0))
+    assert len(got) == len(arcs)
+    for (cube, w0, shift), out in zip(arcs, got):
+        ref = _one(cube, w0, shift)
+        assert out["loops"] == ref["loops"] and np.array_equal(out["changed"], ref["changed"])
+        assert bits_equal(out["weights"], ref["weights"]) and bits_equal(out["test"], ref["test"])
+
+
+def test_pipeline_on_pinned_arrays_and_queue_rules():
+    from iterative_cleaner_amd import _native, batch
+    arcs = _archives(3)
+    pinned = []
+    for cube, w0, shift in arcs:
+        trio = (_native.PinnedArray(cube.shape), _native.PinnedArray(w0.shape),
+                _native.PinnedArray(shift.shape, np.int32))
+        trio[0].array[:] = cube
+        trio[1].array[:] = w0
+        trio[2].array[:] = shift
+        pinned.append(trio)
+    items = [tuple(p.array for p in trio) for trio in pinned]
+    with _native.GpuSession(*SHAPE, device=0) as s:
+        # the same archive twice in a row, then the others: the slots rotate correctly
+        outs = list(batch.pipeline(s, [items[0], items[0], items[1], items[2], items[1]]))
+        refs = [_one(*arcs[i]) for i in (0, 0, 1, 2, 1)]
+        for out, ref in zip(outs, refs):
+            assert bits_equal(out["weights"], ref["weights"]) and out["loops"] == ref["loops"]
+        # at most two pending uploads; synchronous uploads refuse while any is pending
+        s.upload_async(*items[0])
+        s.upload_async(*items[1])
+        with pytest.raises(_native.NativeError):
+            s.upload_async(*items[2])
+        with pytest.raises(_native.NativeError):
+            s.upload(*arcs[2])
+        a = s.run()
+        b = s.run()
+        assert bits_equal(a["weights"], refs[0]["weights"]) and bits_equal(b["weights"], refs[2]["weights"])
+        # queue drained: a synchronous upload works again, and a re-run repeats the last archive
+        s.upload(*arcs[2])
+        assert bits_equal(s.run()["weights"], refs[3]["weights"])
+        assert bits_equal(s.run()["weights"], refs[3]["weights"])
+    for trio in pinned:
+        for p in trio:
+            p.close()

@@ -109,14 +109,14 @@ def cli_check(a):
     ok = True
     if rank == 0:
         sharded_out = buf.getvalue()
-        w_sh = ica.Archive_load("cli.ar_cleaned.ar").get_weights()
+        w_sh = ica.Archive_load("cli_cleaned.ar").get_weights()
         res = sorted(f for f in os.listdir(".") if "_residual_" in f)
         r_sh = ica.Archive_load(res[-1]).get_data()
         os.environ["IC_CHANNEL_SHARDS"] = "0"
         buf1 = io.StringIO()
         with contextlib.redirect_stdout(buf1):
             cleaner.main(cleaner.parse_arguments(argv))
-        w_1 = ica.Archive_load("cli.ar_cleaned.ar").get_weights()
+        w_1 = ica.Archive_load("cli_cleaned.ar").get_weights()
         r_1 = ica.Archive_load(res[-1]).get_data()
         ok = (sharded_out == buf1.getvalue() and w_sh.tobytes() == w_1.tobytes()
               and np.array_equal(r_sh, r_1))
