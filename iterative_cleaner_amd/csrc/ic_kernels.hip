@@ -1077,15 +1077,21 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 
 // Consume the sweep result, run lmdif's scalar logic to the next request.
 // Survivors (profiles still needing a sweep) are appended to next_list;
-// *next_n counts them (order within the list is irrelevant: profiles are independent).
-__global__ __launch_bounds__(256) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
-                                                   const int32_t *__restrict__ nlist, double *__restrict__ amp_o,
-                                                   int32_t *__restrict__ info_o, int32_t *__restrict__ next_list,
-                                                   int32_t *__restrict__ next_n)
+// *next_n counts them (order within the list is irrelevant: profiles are
+// independent).  The append is aggregated per block (one atomic per 512
+// profiles), and the last block to finish publishes the final count to
+// host-mapped memory (host_n), so the host needs no copy dispatch to learn it.
+#define FIT_STATE_BS 512
+__global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
+                                                            const int32_t *__restrict__ nlist,
+                                                            double *__restrict__ amp_o, int32_t *__restrict__ info_o,
+                                                            int32_t *__restrict__ next_list, int32_t *__restrict__ next_n,
+                                                            int32_t *__restrict__ done_n, int32_t *host_n)
 {
+    __shared__ int wcnt[FIT_STATE_BS / 64];
+    __shared__ int woff[FIT_STATE_BS / 64];
     const long slot = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long nact = list ? (long)*nlist : P;
-    if ((long)blockIdx.x * blockDim.x >= nact) return;
     int still = 0;
     long k = 0;
     if (slot < nact) {
@@ -1122,17 +1128,28 @@ __global__ __launch_bounds__(256) void k_fit_state(FitStateArrays S, long P, con
             }
         }
     }
-    // wave-aggregated append
+    // block-aggregated append
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned long long m = __ballot(still);
-    const int cnt = __popcll(m);
-    int base = 0;
-    const int lane = threadIdx.x & 63;
-    if (cnt) {
-        if (lane == __ffsll((long long)m) - 1) base = atomicAdd(next_n, cnt);
-        base = __shfl(base, __ffsll((long long)m) - 1);
-        if (still) {
-            const int rank = __popcll(m & ((1ull << lane) - 1ull));
-            next_list[base + rank] = (int32_t)k;
+    if (lane == 0) wcnt[wave] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += wcnt[w];
+        int base = tot ? atomicAdd(next_n, tot) : 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+            woff[w] = base;
+            base += wcnt[w];
+        }
+    }
+    __syncthreads();
+    if (still) next_list[woff[wave] + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
+    // last block out publishes the count
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(done_n, 1) == (int)gridDim.x - 1) {
+            const int c = atomicAdd(next_n, 0);
+            __hip_atomic_store(host_n, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -2534,12 +2551,12 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
 
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
-                            int32_t *next_n)
+                            int32_t *next_n, int32_t *done_n, int32_t *host_n)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, 256)), dim3(256), 0, st, S, P, list, nlist, amp, info,
-                       next_list, next_n);
+    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nlist, amp,
+                       info, next_list, next_n, done_n, host_n);
     return hipGetLastError();
 }
 

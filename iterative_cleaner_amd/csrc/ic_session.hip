@@ -102,7 +102,9 @@ struct Session {
     FitStateArrays fs{};
     int32_t *lists = nullptr;   // two active-profile lists of P entries
     int32_t *rcount = nullptr;  // per-round survivor counts [kMaxRounds] (+ tail sweep counter)
-    int32_t *h_rcount = nullptr;  // pinned host mirror
+                                // then per-round finished-block counters [kMaxRounds]
+    int32_t *h_rcount = nullptr;  // host-mapped mirror, written by k_fit_state's last block
+    int32_t *d_h_rcount = nullptr;  // its device address
     hipEvent_t rev[2] = {nullptr, nullptr};
     void *fs_block = nullptr;   // one allocation backing fs
     int fit_rounds = 0;
@@ -471,7 +473,7 @@ int run_fit(Session *s)
     const long P = (long)s->P;
     const int nbin = s->p.nbin;
     CK(launch_fit_init(s->stream, s->fs, P));
-    CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * (kMaxRounds + 2), s->stream));
+    CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * (2 * kMaxRounds + 2), s->stream));
     unsigned long long *tail_sweeps = (unsigned long long *)(s->rcount + kMaxRounds);
     int32_t *bufs[2] = {s->lists, s->lists + P};
     const int32_t *cur = nullptr, *cin = nullptr;   // round 0: all profiles
@@ -488,9 +490,9 @@ int run_fit(Session *s)
         }
         int32_t *next = bufs[r & 1];
         LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, cur, cin, bound, s->fs));
+        s->h_rcount[r] = -1;
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
-                                                s->rcount + r));
-        CK(hipMemcpyAsync(s->h_rcount + r, s->rcount + r, sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+                                                s->rcount + r, s->rcount + kMaxRounds + 2 + r, s->d_h_rcount + r));
         CK(hipEventRecord(s->rev[r & 1], s->stream));
         ++rounds;
         cur = next;
@@ -653,7 +655,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     AL(s->lists, 2 * P);
-    AL(s->rcount, (size_t)kMaxRounds + 2);
+    AL(s->rcount, (size_t)2 * kMaxRounds + 2);
     if (sharded) {
         const char *cerr = nullptr;
         s->comm = make_comm(&cerr);
@@ -696,7 +698,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         AL(s->counters, (size_t)(p.max_iter + 4));
     }
 #undef AL
-    if (hipHostMalloc((void **)&s->h_rcount, sizeof(int32_t) * kMaxRounds, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void **)&s->h_rcount, sizeof(int32_t) * kMaxRounds,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&s->d_h_rcount, s->h_rcount, 0) != hipSuccess)
         return bail(fail(IC_ENOMEM, "hipHostMalloc(round counts) failed"));
     for (auto &e : s->rev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
