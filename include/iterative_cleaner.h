@@ -68,6 +68,13 @@ void ic_session_destroy(void *session);
  * read by iterative_cleaner.py:97-100 (fit cube) and :88-93 (template). */
 int ic_upload(void *session, const float *cube, const float *w0, const int32_t *shift);
 
+/* Full-polarisation upload: data [nsub][npol][nchan][nbin] f32 as the archive
+ * holds it (psrchive get_data), pscrunched ON THE DEVICE to the total intensity
+ * f32(pol0 + pol1) (npol >= 2; npol == 1: pol0), the pscrunch of
+ * iterative_cleaner.py:70/:89/:100 (archive.py pscrunch).  The host then never
+ * pscrunches a copy of the archive. */
+int ic_upload_pols(void *session, const float *data, int npol, const float *w0, const int32_t *shift);
+
 /* Same from device pointers already resident in HBM on the session's device
  * (e.g. torch-ROCm tensors): a device-to-device copy, no PCIe. */
 int ic_upload_device(void *session, const float *d_cube, const float *d_w0,

@@ -20,7 +20,8 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_get_fit", "ic_get_diagnostics", "ic_get_kernel_times", "ic_kernel_name",
            "ic_set_timing", "ic_get_run_stats", "ic_set_fit_tail", "ic_last_error",
            "ic_shard_layout", "ic_session_create_shard", "ic_group_create", "ic_group_destroy",
-           "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free")
+           "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free",
+           "ic_upload_pols")
 
 
 class NativeError(RuntimeError):
@@ -115,6 +116,7 @@ def load_library(path: str = LIB_PATH):
     lib.ic_get_run_stats.argtypes = [vp, C.POINTER(RunStats)]
     lib.ic_set_fit_tail.argtypes = [vp, C.c_int64]
     lib.ic_upload_async.argtypes = [vp, vp, vp, vp]
+    lib.ic_upload_pols.argtypes = [vp, vp, C.c_int, vp, vp]
     lib.ic_host_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
     lib.ic_host_free.argtypes = [vp]
     lib.ic_host_free.restype = None
@@ -208,6 +210,17 @@ class GpuSession:
         w0 = np.ascontiguousarray(w0, dtype=np.float32).reshape(nsub, nchan)
         shift = np.ascontiguousarray(np.mod(shift, nbin), dtype=np.int32).reshape(nchan)
         self._check(self.lib.ic_upload(self.h, _ptr(cube), _ptr(w0), _ptr(shift)), "ic_upload")
+
+    def upload_pols(self, data, w0, shift):
+        """Full-polarisation data (nsub, npol, nchan, nbin): pscrunched on the GPU."""
+        nsub, nchan, nbin = self.shape
+        data = np.ascontiguousarray(data, dtype=np.float32)
+        if data.ndim != 4 or data.shape[0] != nsub or data.shape[2:] != (nchan, nbin):
+            raise ValueError("upload_pols: data shape %s != (%d, npol, %d, %d)" % (data.shape, nsub, nchan, nbin))
+        w0 = np.ascontiguousarray(w0, dtype=np.float32).reshape(nsub, nchan)
+        shift = np.ascontiguousarray(np.mod(shift, nbin), dtype=np.int32).reshape(nchan)
+        self._check(self.lib.ic_upload_pols(self.h, _ptr(data), int(data.shape[1]), _ptr(w0), _ptr(shift)),
+                    "ic_upload_pols")
 
     def upload_async(self, cube, w0, shift):
         """Queue the copy of the next archive (see ic_upload_async); the arrays

@@ -118,12 +118,14 @@ def _dm_shift(ar) -> np.ndarray:
     return out
 
 
-def _total_intensity(ar) -> np.ndarray:
-    """(nsub, nchan, nbin) f32 total intensity as pscrunch defines it."""
+def _loop_input(ar) -> np.ndarray:
+    """What the loop cleans: (nsub, nchan, nbin) f32 when the archive holds one
+    polarisation, else the full-pol (nsub, npol, nchan, nbin) f32 data, which
+    the GPU pscrunches (ic_upload_pols: total intensity f32(pol0 + pol1))."""
     data = ar.get_data()
     if data.shape[1] == 1:
         return np.ascontiguousarray(data[:, 0], dtype=np.float32)
-    return np.ascontiguousarray((data[:, 0] + data[:, 1]).astype(np.float32))
+    return np.ascontiguousarray(data, dtype=np.float32)
 
 
 def _device() -> int:
@@ -134,10 +136,12 @@ def _device() -> int:
 
 
 def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15):
-    """Run the GPU loop on a (nsub, nchan, nbin) f32 cube; returns the ic_run dict
+    """Run the GPU loop on a (nsub, nchan, nbin) f32 cube, or on full-polarisation
+    data (nsub, npol, nchan, nbin) that the GPU pscrunches; returns the ic_run dict
     (+ ``residual`` when requested).  Under channel sharding (dist.channel_sharding)
     every rank runs its channel shard and gets the merged result."""
-    nsub, nchan, nbin = cube.shape
+    pols = cube.ndim == 4
+    nsub, nchan, nbin = (cube.shape[0], cube.shape[2], cube.shape[3]) if pols else cube.shape
     from .dist import channel_sharding
     if channel_sharding():
         import torch
@@ -148,15 +152,19 @@ def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_d
         chans, _ = _native.shard_layout(nsub, nchan, world)
         c0, c1 = chans[rank]
         dev = torch.device("cuda", _device() if device is None else device)
+        part = cube[:, :, c0:c1] if pols else cube[:, c0:c1]
         return sharded.clean_cube_dist(
-            np.ascontiguousarray(cube[:, c0:c1]), np.ascontiguousarray(np.asarray(w0)[:, c0:c1]),
+            np.ascontiguousarray(part), np.ascontiguousarray(np.asarray(w0)[:, c0:c1]),
             np.asarray(shift)[c0:c1], (nsub, nchan, nbin), dev, want_residual=want_residual,
             max_iter=args.max_iter, chanthresh=args.chanthresh, subintthresh=args.subintthresh,
             pulse_region=args.pulse_region, baseline_duty=baseline_duty)
     with _native.GpuSession(nsub, nchan, nbin, args.max_iter, args.chanthresh, args.subintthresh,
                             args.pulse_region, baseline_duty,
                             device=_device() if device is None else device) as s:
-        s.upload(cube, w0, shift)
+        if pols:
+            s.upload_pols(cube, w0, shift)
+        else:
+            s.upload(cube, w0, shift)
         out = s.run()
         if want_residual and out["n_iter"] > 0:
             out["residual"] = s.residual()
@@ -217,14 +225,18 @@ def clean(ar, args, arch):
         _side_effects = True
     backend = archive_backend()
     orig_weights = ar.get_weights()
-    if not (args.memory and not args.pscrunch):
+    # The reference pscrunches the archive in memory unless --memory without -p
+    # (iterative_cleaner.py:67-70).  Only -p keeps that pscrunched copy as the
+    # output; otherwise the archive is reloaded (or kept full-pol with --memory),
+    # so its data go to the GPU full-pol and are pscrunched there.
+    if args.pscrunch:
         ar.pscrunch()
     ar_name = ar.get_filename().split()[-1]
     max_iterations = args.max_iter
     if not args.quiet:
         print("Total number of profiles: %s" % orig_weights.size)
 
-    cube = _total_intensity(ar)
+    cube = _loop_input(ar)
     shift = _dm_shift(ar)
     duty = ar.get_baseline_duty() if hasattr(ar, "get_baseline_duty") else 0.15
     out = run_loop(cube, orig_weights, shift, args, want_residual=args.unload_res,

@@ -99,6 +99,8 @@ hipError_t launch_window(hipStream_t st, const double *part, long ss, long sl, c
 // flags != nullptr: only subints with flags[s] != 0
 hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, const int32_t *win,
                        const int32_t *flags, int nsub, int nchan, int nbin, int width, float *base);
+// total intensity in place: raw[i] = f32(raw[i] + pol1[i])  (archive.py pscrunch)
+hipError_t launch_pscrunch(hipStream_t st, float *raw, const float *pol1, size_t n);
 hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
                           int nsub, int nchan, int nbin, int ldD, float *D);
 // num (s, leaf, i) = part[s*ss + leaf*sl + i], weight (s, leaf) = wpart[s*wss + leaf*wsl]

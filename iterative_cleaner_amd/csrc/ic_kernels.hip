@@ -318,6 +318,25 @@ __global__ __launch_bounds__(256) void k_base(const float *__restrict__ raw, con
     }
 }
 
+// pscrunch on the device: raw = f32(pol0 + pol1), float4 grid-stride
+__global__ __launch_bounds__(256) void k_pscrunch(float *__restrict__ raw, const float *__restrict__ pol1, size_t n)
+{
+    const size_t n4 = n / 4;
+    float4 *r4 = (float4 *)raw;
+    const float4 *p4 = (const float4 *)pol1;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        float4 a = r4[i];
+        const float4 b = p4[i];
+        a.x = a.x + b.x;
+        a.y = a.y + b.y;
+        a.z = a.z + b.z;
+        a.w = a.w + b.w;
+        r4[i] = a;
+    }
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        raw[i] = raw[i] + pol1[i];
+}
+
 // D[k][i] = f32(ded[k][i] - base0[k])  (fit cube, dedispersed frame); one row per wave step
 __global__ __launch_bounds__(256) void k_fitcube(const float *__restrict__ raw, const int32_t *__restrict__ shift,
                                                  const float *__restrict__ base, int nsub, int nchan,
@@ -2459,6 +2478,12 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
     const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
     hipLaunchKernelGGL(k_base, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_pscrunch(hipStream_t st, float *raw, const float *pol1, size_t n)
+{
+    hipLaunchKernelGGL(k_pscrunch, dim3(std::min<unsigned>(cdiv(n / 4 + 1, 256), 8192)), dim3(256), 0, st, raw, pol1, n);
     return hipGetLastError();
 }
 

@@ -809,6 +809,33 @@ int ic_upload(void *session, const float *cube, const float *w0, const int32_t *
     return IC_OK;
 }
 
+int ic_upload_pols(void *session, const float *data, int npol, const float *w0, const int32_t *shift)
+{
+    Session *s = (Session *)session;
+    if (!s || !data || !w0 || !shift) return fail(IC_EINVAL, "null argument");
+    if (npol < 1) return fail(IC_EINVAL, "npol=%d", npol);
+    if (s->fifo_n) return fail(IC_ESTATE, "ic_upload_pols with %d asynchronous upload(s) pending", s->fifo_n);
+    CK(hipSetDevice(s->device));
+    for (int c = 0; c < s->nchan; ++c)
+        if (shift[c] < 0 || shift[c] >= s->p.nbin) return fail(IC_EINVAL, "shift[%d]=%d out of [0,nbin)", c, shift[c]);
+    s->ever_uploaded = true;
+    const size_t row = sizeof(float) * (size_t)s->nchan * s->p.nbin;   // one subint of one polarisation
+    // pol 0 -> raw; pol 1 -> the fit-cube buffer as scratch (rebuilt, and re-zeroed, below)
+    CK(hipMemcpy2DAsync(s->raw, row, data, row * npol, row, s->p.nsub, hipMemcpyHostToDevice, s->stream));
+    if (npol >= 2) {
+        CK(hipMemcpy2DAsync(s->D, row, (const char *)data + row, row * npol, row, s->p.nsub,
+                            hipMemcpyHostToDevice, s->stream));
+        CK(launch_pscrunch(s->stream, s->raw, s->D, s->N));
+        CK(hipMemsetAsync(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD, s->stream));
+    }
+    CK(hipMemcpyAsync(s->w0, w0, sizeof(float) * s->P, hipMemcpyHostToDevice, s->stream));
+    CK(hipMemcpyAsync(s->shift, shift, sizeof(int32_t) * s->nchan, hipMemcpyHostToDevice, s->stream));
+    CK(hipStreamSynchronize(s->stream));
+    s->uploaded = true;
+    s->ran = false;
+    return IC_OK;
+}
+
 int ic_upload_device(void *session, const float *d_cube, const float *d_w0, const int32_t *d_shift)
 {
     Session *s = (Session *)session;

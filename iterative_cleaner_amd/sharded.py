@@ -118,7 +118,10 @@ def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, gro
     chans, _ = _native.shard_layout(nsub, nchan, world)
     with _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm,
                               device=_device_index(device), **_loop_kwargs(args)) as s:
-        s.upload(cube_slice, w0_slice, shift_slice)
+        if np.ndim(cube_slice) == 4:   # full-pol: pscrunched on the GPU
+            s.upload_pols(cube_slice, w0_slice, shift_slice)
+        else:
+            s.upload(cube_slice, w0_slice, shift_slice)
         out = s.run()
         res = s.residual() if want_residual and out["n_iter"] > 0 else None
     every = [None] * world

@@ -74,3 +74,25 @@ def test_pipeline_on_pinned_arrays_and_queue_rules():
     for trio in pinned:
         for p in trio:
             p.close()
+
+
+@pytest.mark.parametrize("npol", [1, 2, 4])
+def test_device_pscrunch_matches_host_pscrunch(npol):
+    """ic_upload_pols: the GPU's f32(pol0 + pol1) gives exactly the loop of the
+    host-pscrunched cube (archive.py pscrunch), including a second run after
+    the fit-cube buffer served as scratch."""
+    from iterative_cleaner_amd import _native, synth
+    data, w0, shift = synth.make_cube(5, 72, 256, seed=77, rfi_frac=0.2, npol=npol)
+    host = data[:, 0] if npol == 1 else (data[:, 0] + data[:, 1]).astype(np.float32)
+    with _native.GpuSession(5, 72, 256, device=0) as s:
+        s.upload(np.ascontiguousarray(host), w0, shift)
+        ref = s.run()
+        amp_ref, _ = s.fit()
+        R_ref = s.residual()
+    with _native.GpuSession(5, 72, 256, device=0) as s:
+        for _ in range(2):
+            s.upload_pols(data, w0, shift)
+            out = s.run()
+            amp, _ = s.fit()
+            assert bits_equal(out["weights"], ref["weights"]) and bits_equal(out["test"], ref["test"])
+            assert bits_equal(amp, amp_ref) and bits_equal(s.residual(), R_ref)
