@@ -1,10 +1,17 @@
 """Archive file I/O for the NumPy stand-in (reference load/unload sites:
 iterative_cleaner.py:47, :60, :150, :162).
 
-Format: an uncompressed ``.npz`` container (no pickles) holding
-``data`` (nsub, npol, nchan, nbin) f32, ``weights`` (nsub, nchan) f32,
-``dm_shift`` (nchan,) i64, ``dedispersed`` (bool scalar) and a JSON ``meta``
-string.  The extension of the path is kept as given (``*.ar`` works).
+Two formats:
+
+* PSRFITS (fold mode, int16 samples; psrfits.py) — read whenever a file starts
+  with a FITS primary header, written for archives loaded from PSRFITS (as
+  psrchive keeps an archive's format on unload) and for paths ending in
+  .fits / .sf / .rf;
+* otherwise an uncompressed ``.npz`` container (no pickles) holding ``data``
+  (nsub, npol, nchan, nbin) f32, ``weights`` (nsub, nchan) f32, ``dm_shift``
+  (nchan,) i64, ``dedispersed`` (bool scalar) and a JSON ``meta`` string.
+
+The extension of the path is kept as given (``*.ar`` works for both).
 """
 from __future__ import annotations
 
@@ -12,12 +19,17 @@ import json
 
 import numpy as np
 
+from . import psrfits
 from .archive import Archive
 
 FORMAT_VERSION = 1
+PSRFITS_SUFFIXES = (".fits", ".sf", ".rf")
 
 
 def save(ar: Archive, path: str) -> None:
+    if getattr(ar, "_format", "") == "PSRFITS" or path.lower().endswith(PSRFITS_SUFFIXES):
+        psrfits.save(ar, path)
+        return
     meta = {
         "format": "iterative_cleaner_amd.npz-archive",
         "version": FORMAT_VERSION,
@@ -35,6 +47,8 @@ def save(ar: Archive, path: str) -> None:
 
 
 def load(path: str) -> Archive:
+    if psrfits.is_psrfits(path):
+        return psrfits.load(path)
     with np.load(path, allow_pickle=False) as z:
         meta = json.loads(str(z["meta"]))
         return Archive(z["data"], z["weights"], z["dm_shift"],

@@ -1,0 +1,85 @@
+"""PSRFITS I/O of the archive stand-in: FITS block and
+card structure, int16 quantisation bounds, exact second round trip, weights /
+shifts / metadata preserved, DM-derived shifts for files without the stand-in
+keywords, and the format an archive keeps on unload."""
+import os
+
+import numpy as np
+import pytest
+
+from iterative_cleaner_amd import archive as ica
+from iterative_cleaner_amd import psrfits, synth
+
+
+@pytest.mark.parametrize("npol", [1, 2, 4])
+def test_roundtrip(tmp_path, npol):
+    ar = synth.make_archive(6, 40, 64, seed=5, rfi_frac=0.2, npol=npol)
+    ar.get_Integration(3).set_weight(7, 0.0)
+    p = str(tmp_path / "a.fits")
+    ar.unload(p)
+    assert psrfits.is_psrfits(p)
+    raw = open(p, "rb").read()
+    assert len(raw) % psrfits.BLOCK == 0
+    br = ica.Archive_load(p)
+    assert br._format == "PSRFITS"
+    assert br.get_data().shape == ar.get_data().shape
+    q, scl, offs = br._psrfits_q
+    err = np.abs(br.get_data().astype(np.float64) - ar.get_data())
+    assert np.all(err <= 0.5 * scl[..., None] * (1 + 1e-5) + 1e-6 * np.abs(ar.get_data()) + 1e-30)
+    assert np.array_equal(br.get_weights(), ar.get_weights())
+    assert np.array_equal(br.get_dm_shift(), ar.get_dm_shift())
+    assert br.get_source() == ar.get_source()
+    assert br.get_baseline_duty() == ar.get_baseline_duty()
+    assert abs(br.start_time().in_days() - ar.start_time().in_days()) < 1e-9
+    # unloading a PSRFITS archive keeps the format, whatever the extension; the
+    # second round trip reuses the quantisation: bit-exact
+    p2 = str(tmp_path / "b_cleaned.ar")
+    br.unload(p2)
+    cr = ica.Archive_load(p2)
+    assert cr._format == "PSRFITS" and np.array_equal(cr.get_data(), br.get_data())
+    assert np.array_equal(cr._psrfits_q[0], q)
+
+
+def test_header_cards_and_columns(tmp_path):
+    ar = synth.make_archive(3, 16, 32, seed=1, npol=2)
+    p = str(tmp_path / "h.sf")
+    ar.unload(p)
+    with open(p, "rb") as fh:
+        prim = psrfits._read_header(fh)
+        fh.seek(psrfits.BLOCK * ((fh.tell() + psrfits.BLOCK - 1) // psrfits.BLOCK))
+        sub = psrfits._read_header(fh)
+    assert prim["FITSTYPE"] == "PSRFITS" and prim["NAXIS"] == 0 and prim["EXTEND"] is True
+    assert sub["XTENSION"] == "BINTABLE" and sub["EXTNAME"] == "SUBINT"
+    assert (sub["NPOL"], sub["NCHAN"], sub["NBIN"], sub["NAXIS2"]) == (2, 16, 32, 3)
+    names = [sub["TTYPE%d" % i] for i in range(1, sub["TFIELDS"] + 1)]
+    for c in ("TSUBINT", "OFFS_SUB", "PERIOD", "DAT_FREQ", "DAT_WTS", "DAT_OFFS", "DAT_SCL", "DATA"):
+        assert c in names
+    i = names.index("DATA") + 1
+    assert sub["TFORM%d" % i] == "%dI" % (2 * 16 * 32) and sub["TDIM%d" % i] == "(32,16,2)"
+    dt, _ = psrfits._columns(sub)
+    assert dt.itemsize == sub["NAXIS1"]
+    # every header card is 80 printable ASCII characters
+    raw = open(p, "rb").read(2 * psrfits.BLOCK)
+    assert all(32 <= b < 127 for b in raw[:psrfits.BLOCK])
+
+
+def test_foreign_file_shifts_from_dm(tmp_path):
+    """Without the stand-in's IC_SHIFT column the integer delays come from DM,
+    DAT_FREQ and PERIOD (cleaner._dm_shift's integer approximation)."""
+    ar = synth.make_archive(2, 8, 64, seed=2)
+    ar._dm, ar._period = 30.0, 0.05
+    ar._chan_freqs = 1400.0 + np.arange(8) * 10.0 - 35.0
+    p = str(tmp_path / "f.fits")
+    psrfits.save(ar, p, stand_in_meta=False)
+    br = psrfits.load(p)
+    delay = 4.148808e3 * 30.0 * (ar._chan_freqs ** -2 - 1400.0 ** -2)
+    assert np.array_equal(br.get_dm_shift(), np.rint(delay / 0.05 * 64).astype(np.int64) % 64)
+    assert br.get_dedispersed() is False and br.get_baseline_duty() == 0.15
+
+
+def test_npz_archives_stay_npz(tmp_path):
+    ar = synth.make_archive(2, 4, 8, seed=3)
+    p = str(tmp_path / "n.ar")
+    ar.unload(p)
+    assert not psrfits.is_psrfits(p)
+    assert os.path.getsize(p) > 0 and ica.Archive_load(p).get_data().shape == (2, 1, 4, 8)
