@@ -683,8 +683,15 @@ __device__ int lm_after_a2(LmState &L, double fnorm1)
 
 // Exact fast path.  enorm: while every component is 0 or inside
 // (RDWARF, agiant) MINPACK's enorm reduces to sqrt(sum_seq a*a); that range is
-// verified per lane with integer compares on the high words (conservatively:
-// equal high words count as out of range).  Division: q = RN(a/b) from the
+// verified per lane with integer compares on the high words of the SQUARES
+// a*a, which the sum needs anyway (no |a| masking): RN is monotone, so
+// hi(RN(a^2)) < hi(RN(agiant^2)) implies |a| < agiant and, for a != 0,
+// hi(RN(a^2)) > hi(RN(RDWARF^2)) implies |a| > RDWARF (conservatively: equal
+// high words count as out of range).  A nonzero a whose square underflowed to
+// 0 would slip through, so the A sweep takes this path only for
+// |x| in [2^-100, 2^100]: there every nonzero f = RN(RN(x t) - p) (t, p from
+// f32) is >= 2^-301 and every nonzero J >= 2^-427 in magnitude, |J| <= 2^355,
+// and all squares are normal.  Division: q = RN(a/b) from the
 // correctly rounded reciprocal y = RN(1/b) with two FMA corrections; after
 // the first, q1 is within one ulp, so the second (Markstein) correction is
 // exactly RN(a/b) barring over/underflow — which would push J out of the
@@ -703,10 +710,9 @@ __device__ __forceinline__ void fa_zero(FastAcc &a)
 
 __device__ __forceinline__ void fa_add(FastAcc &a, double v)
 {
-    const double av = fabs(v);
-    const double sq = av * av;
+    const double sq = v * v;   // == RN(|v| * |v|)
     a.s2 = a.s2 + sq;
-    const uint32_t hi = (uint32_t)((unsigned long long)__double_as_longlong(av) >> 32);
+    const uint32_t hi = (uint32_t)((unsigned long long)__double_as_longlong(sq) >> 32);
     a.maxhi = max(a.maxhi, hi);
     a.minhm1 = min(a.minhm1, hi - 1u);   // zero -> 0xffffffff
 }
@@ -732,6 +738,13 @@ __device__ __forceinline__ bool x_in_fast_range(double x)
 {
     const double ax = fabs(x);
     return ax >= 0x1p-500 && ax <= 0x1p500;
+}
+
+// the A sweep's squared-high-word range check (see fa_add) needs the tighter range
+__device__ __forceinline__ bool x_in_sq_range(double x)
+{
+    const double ax = fabs(x);
+    return ax >= 0x1p-100 && ax <= 0x1p100;
 }
 
 // ---- data movement of a sweep: LDS-DMA, double buffered ----------------------
@@ -880,15 +893,97 @@ struct FastBody {
         for (int i = 0; i < FIT_TB; ++i) tv[i] = T64[b0 + i];
     }
 
+    // Four samples at a time, stage by stage: the four dependent chains (the
+    // products, the differences, the five-step division) are interleaved so
+    // that every f64 op has independent neighbours to hide its latency behind;
+    // the accumulations still run in sample order.  Same IEEE ops as sample().
+    __device__ __forceinline__ void group4(const double (&t)[4], const fv4 &pv4, bool first)
+    {
+        const float pf[4] = {pv4.x, pv4.y, pv4.z, pv4.w};
+        double p[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[k] = (double)pf[k];
+        if (DA) {
+            double f[4], d[4], q[4], r[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) f[k] = in.xa * t[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = in.xha * t[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) f[k] = f[k] - p[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = d[k] - p[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = d[k] - f[k];
+            // J = mdiv(d, ha, yha), stage-interleaved
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = d[k] * in.yha;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = fma(-in.ha, q[k], d[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yha, q[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = fma(-in.ha, q[k], d[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yha, q[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                fa_add(fF, f[k]);
+                fa_add(fJ, q[k]);
+            }
+            if (first) {
+                fa0 = f[0];
+                Ja0 = q[0];
+            }
+        }
+        if (DB) {
+            double f[4], d[4], q[4], r[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) f[k] = in.xb * t[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = in.xhb * t[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) f[k] = f[k] - p[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = d[k] - p[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = d[k] - f[k];
+            // J = mdiv(d, hb, yhb)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = d[k] * in.yhb;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = fma(-in.hb, q[k], d[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yhb, q[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = fma(-in.hb, q[k], d[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yhb, q[k]);
+            // Jn = mdiv(J, ajb, yaj)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = q[k] * in.yaj;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = fma(-in.ajb, d[k], q[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = fma(r[k], in.yaj, d[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = fma(-in.ajb, d[k], q[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = fma(r[k], in.yaj, d[k]);
+            if (first) d[0] = d[0] + 1.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = d[k] * f[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sum = sum + d[k];
+        }
+    }
+
     __device__ __forceinline__ void operator()(int b0, const fv4 (&v)[4])
     {
-        sample(tv[0], (double)v[0].x, b0 == 0);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            if (c) sample(tv[4 * c], (double)v[c].x, false);
-            sample(tv[4 * c + 1], (double)v[c].y, false);
-            sample(tv[4 * c + 2], (double)v[c].z, false);
-            sample(tv[4 * c + 3], (double)v[c].w, false);
+            const double t4[4] = {tv[4 * c], tv[4 * c + 1], tv[4 * c + 2], tv[4 * c + 3]};
+            group4(t4, v[c], c == 0 && b0 == 0);
         }
     }
 };
@@ -959,8 +1054,8 @@ __device__ __forceinline__ void fast_sweep(const DmaTiles &d, int ldD, const Pas
 {
     FastBody<DA, DB> body(in, T64);
     sweep_dma(d, ldD, body);
-    const uint32_t hr1 = (uint32_t)((unsigned long long)__double_as_longlong(kRdwarf) >> 32) + 1u;
-    const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant) >> 32);
+    const uint32_t hr1 = (uint32_t)((unsigned long long)__double_as_longlong(kRdwarf * kRdwarf) >> 32) + 1u;
+    const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant * agiant) >> 32);
     out.f0 = body.fa0;
     out.J0 = body.Ja0;
     out.sum = body.sum;
@@ -1054,7 +1149,7 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     in.ajb = reqB ? S.aj[k] : 1.0;
     in.yaj = 1.0 / in.ajb;
     const bool slow = reqB && S.slow[k];
-    const bool fastA = reqA && x_in_fast_range(in.xa);
+    const bool fastA = reqA && x_in_sq_range(in.xa);
     const bool fastB = reqB && !slow && x_in_fast_range(in.xb) && x_in_fast_range(in.ajb);
     in.A = fastA;
     in.B = fastB;

@@ -192,3 +192,29 @@ def test_moving_baseline_window_matches_c_oracle(oracle_lib):
     assert bits_equal(out["weights"], ref["weights"])
     assert bits_equal(amp, ref["amp"]) and bits_equal(info, ref["info"])
     assert _close_test(out["test"], ref["test"])
+
+
+@pytest.mark.parametrize("fit_mode", ["rounds", "default"])
+def test_extreme_amplitudes_match_c_oracle(fit_mode, oracle_lib):
+    """Profiles whose fitted amplitudes fall outside the fast sweep's ranges
+    (|x| < 2^-100 or > 2^100 for the A sweep, 2^+-500 for B) or whose samples
+    are tiny / huge: the exact re-sweeps must reproduce MINPACK bit for bit."""
+    from iterative_cleaner_amd import synth
+    data, w0, shift = synth.make_cube(6, 40, 128, 321, 0.1)
+    raw = np.ascontiguousarray(data[:, 0])
+    raw[1, 3] *= np.float32(1e-33)           # amplitude ~1e-33: exact A sweeps
+    raw[2, 4] *= np.float32(3e33)            # huge samples, amplitude ~1e33
+    raw[3, 5] *= np.float32(1e-25)
+    raw[4, 6] = np.float32(1e-38) * (np.arange(128) % 3)   # near-denormal samples
+    raw[5, 7, 10] = np.float32(3e38)         # one huge spike
+    ref = oracle_lib.clean_loop(raw, w0, shift, want_details=True)
+    args = dict(max_iter=5, chanthresh=5, subintthresh=5, pulse_region=[0, 0, 1])
+    with _session(raw.shape, args, fit_mode=fit_mode) as s:
+        s.upload(raw, w0, shift)
+        out = s.run()
+        amp, info = s.fit()
+        sd, mn, pt, ff = s.diagnostics()
+    assert out["loops"] == ref["loops"]
+    assert bits_equal(out["weights"], ref["weights"])
+    assert bits_equal(amp, ref["amp"]) and bits_equal(info, ref["info"])
+    assert bits_equal(sd, ref["std"]) and bits_equal(mn, ref["mean"])
