@@ -295,12 +295,20 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
     workload = a.workload or ("C2" if world == 1 else "C3")
     sharded = (world > 1 and workload in BLOCKWISE) or a.sharded
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # IC_BENCH_BACKEND=gloo rehearses an N-rank run on fewer GPUs (ranks share
+    # devices, exchanges staged through the host); the measurement is "nccl" (RCCL)
+    backend = os.environ.get("IC_BENCH_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     elif sharded:
         dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    local = gpu   # the device the sessions below run on
 
     nsub, nchan, nbin, seed, rfi = WORKLOADS[workload]
     P_total = nsub * nchan
