@@ -171,7 +171,8 @@ def pmc_traffic(workload, kernel):
 def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
     """Reference-like loop (per-profile scipy leastsq + numpy.ma), one thread,
     on the first subints of the workload shape: a 2-subint probe sizes the
-    sample to about half of ``budget_s``."""
+    sample to 0.8 * ``budget_s`` by linear extrapolation (about 10-20 s of CPU
+    work in practice: later subints converge in fewer loops)."""
     from threadpoolctl import threadpool_limits
 
     from iterative_cleaner_amd import archive as ica
@@ -184,7 +185,7 @@ def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
         t0 = time.perf_counter()
         reference_like.clean_loop(ar, 5, 5, 5, [0, 0, 1])
         probe = time.perf_counter() - t0
-    nsub = int(max(2, min(64, 2 * 0.5 * budget_s / max(probe, 1e-3))))
+    nsub = int(max(2, min(64, 2 * 0.8 * budget_s / max(probe, 1e-3))))
     data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
     ar = ica.Archive(data, w0, shift)
     ar.pscrunch()
