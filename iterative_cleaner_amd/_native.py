@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libicgpu.so")
+# IC_LIBRARY: an alternative build of the same library (A/B measurements)
+LIB_PATH = os.environ.get("IC_LIBRARY") or os.path.join(HERE, "libicgpu.so")
 ABI_VERSION = 3
 
 # symbols exported by libicgpu.so, as declared in include/iterative_cleaner.h

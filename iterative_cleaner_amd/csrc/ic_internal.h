@@ -130,11 +130,12 @@ hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
 // (the host sizes grids from a count it already knows: counts only shrink).
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S);
-// next_n: device survivor counter (zeroed); done_n: finished-block counter
-// (zeroed); host_n: host-mapped int the last block writes the final count to
+// ctr: zeroed device counter, finished blocks << 32 | survivors (its low word,
+// little-endian, is the next round's list length); host_n: host-mapped int the
+// last block writes the final count to
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
-                            int32_t *next_n, int32_t *done_n, int32_t *host_n);
+                            unsigned long long *ctr, int32_t *host_n);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
                            double *amp, int32_t *info, unsigned long long *sweeps);

@@ -1195,12 +1195,14 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 // independent).  The append is aggregated per block (one atomic per 512
 // profiles), and the last block to finish publishes the final count to
 // host-mapped memory (host_n), so the host needs no copy dispatch to learn it.
-#define FIT_STATE_BS 512
+#ifndef FIT_STATE_BS
+#define FIT_STATE_BS 256
+#endif
 __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
                                                             const int32_t *__restrict__ nlist,
                                                             double *__restrict__ amp_o, int32_t *__restrict__ info_o,
-                                                            int32_t *__restrict__ next_list, int32_t *__restrict__ next_n,
-                                                            int32_t *__restrict__ done_n, int32_t *host_n)
+                                                            int32_t *__restrict__ next_list,
+                                                            unsigned long long *__restrict__ ctr, int32_t *host_n)
 {
     __shared__ int wcnt[FIT_STATE_BS / 64];
     __shared__ int woff[FIT_STATE_BS / 64];
@@ -1250,22 +1252,18 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
     if (threadIdx.x == 0) {
         int tot = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += wcnt[w];
-        int base = tot ? atomicAdd(next_n, tot) : 0;
+        // one atomic per block: finished blocks in the high word, survivors in the low
+        const unsigned long long old = atomicAdd(ctr, (1ull << 32) | (unsigned long long)(unsigned)tot);
+        int base = (int)(uint32_t)old;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
             woff[w] = base;
             base += wcnt[w];
         }
+        if ((old >> 32) == (unsigned long long)gridDim.x - 1)   // last block: base is the final count
+            __hip_atomic_store(host_n, base, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
     if (still) next_list[woff[wave] + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
-    // last block out publishes the count
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(done_n, 1) == (int)gridDim.x - 1) {
-            const int c = atomicAdd(next_n, 0);
-            __hip_atomic_store(host_n, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
 }
 
 // ---- tail: the last few thousand profiles, one wave each, to completion ----
@@ -2426,8 +2424,9 @@ __global__ __launch_bounds__(256) void k_combine(
             ze += red[1][w];
             df |= dred[w];
         }
-        if (ch) atomicAdd(&counters[0], ch);
-        if (ze) atomicAdd(&counters[1], ze);
+        // counters[0..1] (changed, zero) as one u64 add: both < 2^32, no carry
+        if (ch || ze)
+            atomicAdd((unsigned long long *)counters, ((unsigned long long)(unsigned)ze << 32) | (unsigned)ch);
         for (int h = 0; h < hmax; ++h)
             if ((df >> h) & 1ull) atomicOr(&counters[2 + h], 1);
     }
@@ -2671,12 +2670,12 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
 
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
-                            int32_t *next_n, int32_t *done_n, int32_t *host_n)
+                            unsigned long long *ctr, int32_t *host_n)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nlist, amp,
-                       info, next_list, next_n, done_n, host_n);
+                       info, next_list, ctr, host_n);
     return hipGetLastError();
 }
 

@@ -101,8 +101,7 @@ struct Session {
     PwPlan *plan = nullptr;
     FitStateArrays fs{};
     int32_t *lists = nullptr;   // two active-profile lists of P entries
-    int32_t *rcount = nullptr;  // per-round survivor counts [kMaxRounds] (+ tail sweep counter)
-                                // then per-round finished-block counters [kMaxRounds]
+    int32_t *rcount = nullptr;  // u64 per round (blocks done << 32 | survivors) + tail sweep counter
     int32_t *h_rcount = nullptr;  // host-mapped mirror, written by k_fit_state's last block
     int32_t *d_h_rcount = nullptr;  // its device address
     hipEvent_t rev[2] = {nullptr, nullptr};
@@ -463,7 +462,7 @@ int shard_rowstats(Session *s, const LineStatsArgs &la)
 // exact scipy leastsq for every profile (ic.py:266-272).
 // Rounds of k_fit_pass + k_fit_state over a compacted list of the profiles
 // that still need a data sweep.  Each round's survivor count lands in
-// rcount[r] on the device; kernels read their list length from there, so the
+// the low word of ctr[r] on the device; kernels read their list length there, so the
 // host only needs an UPPER bound to size grids (counts never grow) and reads
 // the counts one round behind: the stream always has the next round queued.
 // Once the bound drops to tail_threshold (default kTailProfiles; 0 = never),
@@ -474,7 +473,9 @@ int run_fit(Session *s)
     const int nbin = s->p.nbin;
     CK(launch_fit_init(s->stream, s->fs, P));
     CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * (2 * kMaxRounds + 2), s->stream));
-    unsigned long long *tail_sweeps = (unsigned long long *)(s->rcount + kMaxRounds);
+    // per round: blocks done << 32 | survivors; then the tail's sweep counter
+    unsigned long long *ctr = (unsigned long long *)s->rcount;
+    unsigned long long *tail_sweeps = ctr + kMaxRounds;
     int32_t *bufs[2] = {s->lists, s->lists + P};
     const int32_t *cur = nullptr, *cin = nullptr;   // round 0: all profiles
     long bound = P;                                 // >= the active count of the next round
@@ -492,11 +493,11 @@ int run_fit(Session *s)
         LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, cur, cin, bound, s->fs));
         s->h_rcount[r] = -1;
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
-                                                s->rcount + r, s->rcount + kMaxRounds + 2 + r, s->d_h_rcount + r));
+                                                ctr + r, s->d_h_rcount + r));
         CK(hipEventRecord(s->rev[r & 1], s->stream));
         ++rounds;
         cur = next;
-        cin = s->rcount + r;
+        cin = (const int32_t *)(ctr + r);   // low word: the survivor count
         if (r >= 1) {
             // count after round r-1 (= input of round r) bounds the count after round r
             CK(hipEventSynchronize(s->rev[(r - 1) & 1]));
