@@ -393,8 +393,8 @@ def main():
         iter_bytes = 8 * per_rank_P * nbin + 64 * per_rank_P    # SURVEY §8(d) B_iter, one GPU's share
         loop_gbs = iter_bytes * n_iter / (elapsed / a.steps) / 1e9
         if sharded:
-            parallelism = "channel-sharded x%d (RCCL: 2 all-gathers, 1 all-to-all, 1 all-gather, " \
-                          "1 all-reduce per iteration)" % world
+            parallelism = "channel-sharded x%d (RCCL per iteration: 3 all-to-alls to row owners, " \
+                          "3 all-gathers of owner results, 1 all-reduce)" % world
         else:
             parallelism = "replicas" if world > 1 else "single"
         rec = {

@@ -156,10 +156,12 @@ const char *ic_last_error(void);
  * channel blocks.  Rank r owns the channels of one node of the canonical
  * super-block tree (archive.py sb_tree / shards.py channel_shards) and the
  * subint rows [r*nsub/world, (r+1)*nsub/world) of the row medians.  Per
- * iteration a shard exchanges: the template's per-subint channel-sum roots
- * (two all-gathers of nsub*nbin f64), its diagnostics rows with the row owners
- * (one all-to-all), the row medians/MADs (one all-gather of 8*rows doubles) and
- * the convergence counters (one all-reduce).  Results are bit-identical to an
+ * iteration a shard exchanges: the template's per-subint channel-sum roots,
+ * each row sent to its row owner (two all-to-alls, nsub*nbin f64 out per rank),
+ * the owners' windows and fscrunch rows (two small all-gathers), its
+ * diagnostics rows with the row owners (one all-to-all), the row medians/MADs
+ * (one all-gather of 8*rows doubles) and the convergence counters (one
+ * all-reduce).  Results are bit-identical to an
  * unsharded session.  world must be a power of two <= the number of 256-channel
  * super-blocks.
  *

@@ -106,10 +106,16 @@ hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift
 // num (s, leaf, i) = part[s*ss + leaf*sl + i], weight (s, leaf) = wpart[s*wss + leaf*wsl]
 hipError_t launch_fscrunch(hipStream_t st, const double *part, long ss, long sl, const double *wpart, long wss,
                            long wsl, const SbPlan &plan, int nsub, int nbin, float *F, float *wf);
-// shard root of the local super-block partials: out[s][i] = tree(part[s][*][i]),
-// outw[s] = tree(wpart[s][*]) (wpart/outw may be null); flags: only flagged subints
+// shard root of the local super-block partials, one row of ostr doubles per
+// subint: out[s*ostr + i] = tree(part[s][*][i]), out[s*ostr + nbin] =
+// tree(wpart[s][*]) (wpart may be null)
 hipError_t launch_sb_tree(hipStream_t st, const double *part, const double *wpart, const SbPlan &plan, int nsub,
-                          int nbin, const int32_t *flags, double *out, double *outw);
+                          int nbin, long ostr, double *out);
+// windows / fscrunch rows all-gathered from the row owners -> full arrays
+hipError_t launch_unpack_windows(hipStream_t st, const ShardGeom &g, int blk, const int32_t *recv, int32_t *win,
+                                 int32_t *flags);
+hipError_t launch_unpack_fscrunch(hipStream_t st, const ShardGeom &g, int rows_pad, long blk, int nbin,
+                                  const float *recv, float *F, float *wf);
 // diagnostics rows -> per-destination blocks [std|mean|fft (f64)|ptp (f32)] x rows_d x nchan_loc
 // (valid == true: the single u8 field `valid` instead)
 hipError_t launch_pack_rows(hipStream_t st, const ShardGeom &g, int nchan_loc, const double *std_d,

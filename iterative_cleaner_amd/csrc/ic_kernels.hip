@@ -375,22 +375,22 @@ __global__ __launch_bounds__(256) void k_fscrunch(const double *__restrict__ par
 }
 
 // Shard root of local super-block partials [s][nsb_loc][nbin] (channel shards):
-// out[s][i] = sb_tree(part[s][*][i]); outw[s] = sb_tree(wpart[s][*]).
+// out[s*ostr + i] = sb_tree(part[s][*][i]); out[s*ostr + nbin] = sb_tree(wpart[s][*])
+// (wpart optional; ostr >= nbin + 1 then): one row per subint, so the rows a
+// rank owns are one contiguous all-to-all block.
 __global__ __launch_bounds__(256) void k_sb_tree(const double *__restrict__ part, const double *__restrict__ wpart,
-                                                 SbPlan plan, int nbin, const int32_t *__restrict__ flags,
-                                                 double *__restrict__ out, double *__restrict__ outw)
+                                                 SbPlan plan, int nbin, long ostr, double *__restrict__ out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int s = blockIdx.y;
-    if (flags && flags[s] == 0) return;
     const int n = plan.n;
     if (i < nbin) {
         const double *src = part + (size_t)s * n * nbin + i;
-        out[(size_t)s * nbin + i] = sb_eval(plan, [&](int j) { return src[(size_t)j * nbin]; });
+        out[(size_t)s * ostr + i] = sb_eval(plan, [&](int j) { return src[(size_t)j * nbin]; });
     }
     if (wpart && i == 0) {
         const double *w = wpart + (size_t)s * n;
-        outw[s] = sb_eval(plan, [&](int j) { return w[j]; });
+        out[(size_t)s * ostr + nbin] = sb_eval(plan, [&](int j) { return w[j]; });
     }
 }
 
@@ -2525,6 +2525,40 @@ __global__ __launch_bounds__(256) void k_unpack_rowstats(ShardGeom g, int rows_p
     row_mad[k] = slot[4 * rows_p + q * rows_p + r];
 }
 
+// Window positions gathered from the row owners (blocks of `blk` ints per
+// rank) -> win[nsub] on every rank; flags (optional): moved per subint and the
+// moves counter flags[nsub], as k_window does unsharded.
+__global__ __launch_bounds__(256) void k_unpack_windows(ShardGeom g, int blk, const int32_t *__restrict__ recv,
+                                                        int32_t *__restrict__ win, int32_t *__restrict__ flags)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= g.nsub) return;
+    const int p = geom_row_owner(g, s);
+    const int w = recv[(size_t)p * blk + (s - g.row0[p])];
+    if (flags) {
+        const int moved = win[s] != w;
+        flags[s] = moved;
+        if (moved) atomicAdd(&flags[g.nsub], 1);
+    }
+    win[s] = w;
+}
+
+// fscrunch rows gathered from the row owners: rank p's block (blk floats) holds
+// F rows [rows_pad][nbin] then wf [rows_pad] -> F[nsub][nbin], wf[nsub]
+__global__ __launch_bounds__(256) void k_unpack_fscrunch(ShardGeom g, int rows_pad, long blk, int nbin,
+                                                         const float *__restrict__ recv, float *__restrict__ F,
+                                                         float *__restrict__ wf)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = blockIdx.y;
+    if (i >= nbin) return;
+    const int p = geom_row_owner(g, s);
+    const float *b = recv + (size_t)p * blk;
+    const int t = s - g.row0[p];
+    F[(size_t)s * nbin + i] = b[(size_t)t * nbin + i];
+    if (i == 0) wf[s] = b[(size_t)rows_pad * nbin + t];
+}
+
 __global__ void k_sum_i32(const int32_t *__restrict__ gathered, int world, int n, int32_t *__restrict__ buf)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2601,12 +2635,28 @@ hipError_t launch_fscrunch(hipStream_t st, const double *part, long ss, long sl,
 }
 
 hipError_t launch_sb_tree(hipStream_t st, const double *part, const double *wpart, const SbPlan &plan, int nsub,
-                          int nbin, const int32_t *flags, double *out, double *outw)
+                          int nbin, long ostr, double *out)
 {
     if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
+    if (ostr < nbin + (wpart ? 1 : 0)) return hipErrorInvalidValue;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
-    hipLaunchKernelGGL(k_sb_tree, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, wpart, plan, nbin, flags, out,
-                       outw);
+    hipLaunchKernelGGL(k_sb_tree, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, wpart, plan, nbin, ostr, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_windows(hipStream_t st, const ShardGeom &g, int blk, const int32_t *recv, int32_t *win,
+                                 int32_t *flags)
+{
+    hipLaunchKernelGGL(k_unpack_windows, dim3(cdiv(g.nsub, 256)), dim3(256), 0, st, g, blk, recv, win, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_fscrunch(hipStream_t st, const ShardGeom &g, int rows_pad, long blk, int nbin,
+                                  const float *recv, float *F, float *wf)
+{
+    const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
+    hipLaunchKernelGGL(k_unpack_fscrunch, dim3(cdiv(nbin, bs), g.nsub), dim3(bs), 0, st, g, rows_pad, blk, nbin,
+                       recv, F, wf);
     return hipGetLastError();
 }
 

@@ -74,8 +74,13 @@ struct Session {
     SbPlan plan_sb{};               // the session's super-blocks
     SbPlan plan_top{};              // the shard roots (world leaves)
     int rows_own = 0, rows_pad = 0;
-    double *xw_send = nullptr, *xw_recv = nullptr;          // window-total roots
-    double *xf_send = nullptr, *xf_recv = nullptr;          // fscrunch roots + weight roots
+    double *xw_send = nullptr, *xw_recv = nullptr;          // window-total roots -> row owners
+    double *xf_send = nullptr, *xf_recv = nullptr;          // fscrunch + weight roots -> row owners
+    int32_t *xwg_send = nullptr, *xwg_recv = nullptr;       // owners' windows, all-gathered
+    float *xfg_send = nullptr, *xfg_recv = nullptr;         // owners' fscrunch rows, all-gathered
+    int wg_blk = 0;                                          // ints per rank in xwg (rows_pad, even)
+    long fg_blk = 0;                                         // floats per rank in xfg (even)
+    std::vector<size_t> wsb, wrb, fsb, frb;                 // block bytes: window / fscrunch roots
     unsigned char *xd_send = nullptr, *xd_recv = nullptr;   // diagnostics / valid rows
     double *xr_send = nullptr, *xr_recv = nullptr;          // row medians / MADs
     std::vector<size_t> dsb, drb, vsb, vrb;                 // block bytes: diag, valid
@@ -242,8 +247,8 @@ void free_all(Session *s)
     for (void *b : rbufs)
         if (b) (void)hipFree(b);
     if (s->comm) {
-        void *xbufs[] = {s->xw_send, s->xw_recv, s->xf_send, s->xf_recv, s->xd_send, s->xd_recv, s->xr_send,
-                         s->xr_recv, s->counters};
+        void *xbufs[] = {s->xw_send, s->xw_recv, s->xf_send, s->xf_recv, s->xwg_send, s->xwg_recv, s->xfg_send,
+                         s->xfg_recv, s->xd_send, s->xd_recv, s->xr_send, s->xr_recv, s->counters};
         for (void *b : xbufs)
             if (b) s->comm->release(b);
         s->counters = nullptr;
@@ -337,8 +342,11 @@ const char *shard_layout(int nsub, int nchan, int world, int32_t *chan0, int32_t
 }
 
 // Window stage: per-subint window from the W-weighted total of `part`
-// (unsharded: combine the super-blocks; sharded: reduce the local
-// super-blocks to this shard's root, all-gather the roots, combine them).
+// (unsharded: combine the super-blocks).  Sharded: reduce the local
+// super-blocks to this shard's root, send each subint's root row to the rank
+// that owns the row (all-to-all), the owner combines the world's roots in
+// canonical order and searches the window, and the owners' windows are
+// all-gathered (4 B per subint) - each root crosses the fabric once.
 int window_stage(Session *s, int32_t *flags)
 {
     const int nsub = s->p.nsub, nbin = s->p.nbin;
@@ -347,15 +355,18 @@ int window_stage(Session *s, int32_t *flags)
                                           s->width, s->win, flags));
         return 0;
     }
-    LAUNCH(s, K_SB_TREE, launch_sb_tree(s->stream, s->part, nullptr, s->plan_sb, nsub, nbin, nullptr, s->xw_send,
-                                        nullptr));
-    CM(s, s->comm->allgather(s->xw_send, s->xw_recv, sizeof(double) * nsub * nbin, s->stream), "window roots");
-    LAUNCH(s, K_WINDOW, launch_window(s->stream, s->xw_recv, nbin, (long)nsub * nbin, s->plan_top, nsub, nbin,
-                                      s->width, s->win, flags));
+    LAUNCH(s, K_SB_TREE, launch_sb_tree(s->stream, s->part, nullptr, s->plan_sb, nsub, nbin, nbin, s->xw_send));
+    CM(s, s->comm->alltoallv(s->xw_send, s->wsb.data(), s->xw_recv, s->wrb.data(), s->stream), "window roots");
+    if (s->rows_own > 0)
+        LAUNCH(s, K_WINDOW, launch_window(s->stream, s->xw_recv, nbin, (long)s->rows_own * nbin, s->plan_top,
+                                          s->rows_own, nbin, s->width, s->xwg_send, nullptr));
+    CM(s, s->comm->allgather(s->xwg_send, s->xwg_recv, sizeof(int32_t) * s->wg_blk, s->stream), "windows");
+    LAUNCH(s, K_SHARD_PACK, launch_unpack_windows(s->stream, s->geom, s->wg_blk, s->xwg_recv, s->win, flags));
     return 0;
 }
 
-// fscrunch + tscrunch from part2/wpart (same sharding as window_stage)
+// fscrunch + tscrunch from part2/wpart (sharded as window_stage: root rows of
+// nbin + 1 doubles to the row owners, owners' F rows + wf all-gathered)
 int scrunch_stage(Session *s)
 {
     const int nsub = s->p.nsub, nbin = s->p.nbin;
@@ -363,12 +374,16 @@ int scrunch_stage(Session *s)
         LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->part2, (long)s->nsb * nbin, nbin, s->wpart, s->nsb, 1,
                                               s->plan_sb, nsub, nbin, s->F, s->wf));
     } else {
-        const long L = (long)nsub * nbin + nsub;   // one shard's roots: [nsub][nbin] + [nsub]
-        LAUNCH(s, K_SB_TREE, launch_sb_tree(s->stream, s->part2, s->wpart, s->plan_sb, nsub, nbin, nullptr,
-                                            s->xf_send, s->xf_send + (size_t)nsub * nbin));
-        CM(s, s->comm->allgather(s->xf_send, s->xf_recv, sizeof(double) * L, s->stream), "fscrunch roots");
-        LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->xf_recv, nbin, L, s->xf_recv + (size_t)nsub * nbin, 1, L,
-                                              s->plan_top, nsub, nbin, s->F, s->wf));
+        const long row = nbin + 1, own = (long)s->rows_own * row;
+        LAUNCH(s, K_SB_TREE, launch_sb_tree(s->stream, s->part2, s->wpart, s->plan_sb, nsub, nbin, row, s->xf_send));
+        CM(s, s->comm->alltoallv(s->xf_send, s->fsb.data(), s->xf_recv, s->frb.data(), s->stream), "fscrunch roots");
+        if (s->rows_own > 0)
+            LAUNCH(s, K_FSCRUNCH, launch_fscrunch(s->stream, s->xf_recv, row, own, s->xf_recv + nbin, row, own,
+                                                  s->plan_top, s->rows_own, nbin, s->xfg_send,
+                                                  s->xfg_send + (size_t)s->rows_pad * nbin));
+        CM(s, s->comm->allgather(s->xfg_send, s->xfg_recv, sizeof(float) * s->fg_blk, s->stream), "fscrunch rows");
+        LAUNCH(s, K_SHARD_PACK, launch_unpack_fscrunch(s->stream, s->geom, s->rows_pad, s->fg_blk, nbin, s->xfg_recv,
+                                                       s->F, s->wf));
     }
     LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64));
     return 0;
@@ -678,15 +693,28 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
             dsend += s->dsb.back();
             drecv += s->drb.back();
         }
-        const size_t L = (size_t)nsub * nbin + nsub;
+        // root rows to their owners: rank r's block = its rows, contiguous in the send buffer
+        for (int r = 0; r < world; ++r) {
+            const size_t rows_r = (size_t)(rr[2 * r + 1] - rr[2 * r]);
+            s->wsb.push_back(sizeof(double) * rows_r * nbin);
+            s->wrb.push_back(sizeof(double) * s->rows_own * nbin);
+            s->fsb.push_back(sizeof(double) * rows_r * (nbin + 1));
+            s->frb.push_back(sizeof(double) * s->rows_own * (nbin + 1));
+        }
+        s->wg_blk = (s->rows_pad + 1) & ~1;
+        s->fg_blk = ((long)s->rows_pad * (nbin + 1) + 1) & ~1L;
         struct {
             void **ptr;
             size_t bytes;
             const char *name;
         } xb[] = {{(void **)&s->xw_send, sizeof(double) * nsub * nbin, "window roots"},
-                  {(void **)&s->xw_recv, sizeof(double) * world * nsub * nbin, "gathered window roots"},
-                  {(void **)&s->xf_send, sizeof(double) * L, "fscrunch roots"},
-                  {(void **)&s->xf_recv, sizeof(double) * world * L, "gathered fscrunch roots"},
+                  {(void **)&s->xw_recv, sizeof(double) * world * s->rows_own * nbin, "owned window roots"},
+                  {(void **)&s->xf_send, sizeof(double) * nsub * (nbin + 1), "fscrunch roots"},
+                  {(void **)&s->xf_recv, sizeof(double) * world * s->rows_own * (nbin + 1), "owned fscrunch roots"},
+                  {(void **)&s->xwg_send, sizeof(int32_t) * s->wg_blk, "owned windows"},
+                  {(void **)&s->xwg_recv, sizeof(int32_t) * s->wg_blk * world, "gathered windows"},
+                  {(void **)&s->xfg_send, sizeof(float) * s->fg_blk, "owned fscrunch rows"},
+                  {(void **)&s->xfg_recv, sizeof(float) * s->fg_blk * world, "gathered fscrunch rows"},
                   {(void **)&s->xd_send, dsend, "diagnostics send"},
                   {(void **)&s->xd_recv, drecv, "diagnostics receive"},
                   {(void **)&s->xr_send, sizeof(double) * 8 * s->rows_pad, "row statistics"},
