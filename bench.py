@@ -136,7 +136,6 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, stats, steps):
     per_launch = {
         "k_chan_partials": 4 * N + 8 * nsub * nsb * nbin,
         "k_base": int(4 * P * max(1, int(0.15 * nbin))),
-        "k_fitcube": 8 * N,
         "k_diag": 4 * N + 44 * P,
         "k_linestats": 2 * 4 * 8 * P,
         "k_combine": 4 * 8 * P + 2 * 4 * P,
@@ -146,6 +145,8 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, stats, steps):
         return 4 * nbin * stats["fit_profile_sweeps"] * steps
     if name == "k_fit_tail":
         return 4 * nbin * stats["fit_tail_sweeps"] * steps
+    if name == "k_chan_partials":   # + the fit cube written by iteration 1's pass (mode 3)
+        return per_launch[name] * launches + 4 * N * steps
     if name in per_launch:
         return per_launch[name] * launches
     return None

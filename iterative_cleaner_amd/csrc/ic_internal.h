@@ -50,7 +50,6 @@ enum KernelId {
     K_CHAN_PARTIALS = 0,
     K_WINDOW,
     K_BASE,
-    K_FITCUBE,
     K_FSCRUNCH,
     K_TSCRUNCH,
     K_FIT_PASS,
@@ -85,11 +84,12 @@ struct LineStatsArgs {
 };
 
 // ---- launch wrappers (ic_kernels.hip); all asynchronous on `st` ----
-// mode 0: part = sum W*ded; 1: part2 = sum W*f32(ded-base) + wpart; 2: both.
+// mode 0: part = sum W*ded; 1: part2 = sum W*f32(ded-base) + wpart; 2: both;
+// 3: mode 1 + the fit cube D[k][i] = f32(ded-base) (row stride ldD).
 // flags: only subints with flags[s] != 0 (nullptr: all)
 hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, const float *W, const int32_t *shift,
                                 const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
-                                double *part, double *part2, double *wpart);
+                                double *part, double *part2, double *wpart, float *D = nullptr, int ldD = 0);
 // flags != nullptr: flags[s] = window of subint s moved (win updated in place)
 // element (s, leaf, i) of `part` is part[s*ss + leaf*sl + i]; the leaves are
 // combined with `plan` (single device: the nsb super-blocks; sharded: the
@@ -101,8 +101,6 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
                        const int32_t *flags, int nsub, int nchan, int nbin, int width, float *base);
 // total intensity in place: raw[i] = f32(raw[i] + pol1[i])  (archive.py pscrunch)
 hipError_t launch_pscrunch(hipStream_t st, float *raw, const float *pol1, size_t n);
-hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
-                          int nsub, int nchan, int nbin, int ldD, float *D);
 // num (s, leaf, i) = part[s*ss + leaf*sl + i], weight (s, leaf) = wpart[s*wss + leaf*wsl]
 hipError_t launch_fscrunch(hipStream_t st, const double *part, long ss, long sl, const double *wpart, long wss,
                            long wsl, const SbPlan &plan, int nsub, int nbin, float *F, float *wf);

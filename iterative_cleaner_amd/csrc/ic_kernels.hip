@@ -116,14 +116,18 @@ struct OpOr {
 //   MODE 0: part  = sum_c W*ded                     (baseline window total)
 //   MODE 1: part2 = sum_c W*f32(ded - base), wpart  (fscrunch)
 //   MODE 2: both, in one read of the cube (base = the previous iteration's)
+//   MODE 3: MODE 1 that also writes the fit cube D[k][i] = f32(ded - base)
+//           (iteration 1: base = base0, W = w0: the fit cube of ic.py:96-100 comes
+//           out of the same read of the cube)
 // flags != nullptr: only subints with flags[s] != 0 (a moved window) run.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_chan_partials(
     const float *__restrict__ raw, const float *__restrict__ W, const int32_t *__restrict__ shift,
     const float *__restrict__ base, const int32_t *__restrict__ flags, int nsub, int nchan, int nbin, int nsb,
-    double *__restrict__ part, double *__restrict__ part2, double *__restrict__ wpart)
+    double *__restrict__ part, double *__restrict__ part2, double *__restrict__ wpart, float *__restrict__ D,
+    int ldD)
 {
-    constexpr bool A = MODE != 1, F = MODE != 0;
+    constexpr bool A = MODE == 0 || MODE == 2, F = MODE != 0, WD = MODE == 3;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int sb = blockIdx.y;
     const int s = blockIdx.z;
@@ -150,8 +154,10 @@ __global__ __launch_bounds__(256) void k_chan_partials(
 #pragma unroll
             for (int q = 0; q < B; ++q) {
                 const double w = (double)wv[q];
+                const float d = xv[q] - bv[q];
                 if (A) acc = acc + w * (double)xv[q];
-                if (F) acc2 = acc2 + w * (double)(xv[q] - bv[q]);
+                if (F) acc2 = acc2 + w * (double)d;
+                if (WD) D[(krow + c + q) * (size_t)ldD + i] = d;
             }
         }
         for (; c < c1; ++c) {
@@ -160,8 +166,10 @@ __global__ __launch_bounds__(256) void k_chan_partials(
             if (j >= nbin) j -= nbin;
             const float x = raw[k * nbin + j];
             const double w = (double)W[k];
+            const float d = F ? x - base[k] : 0.0f;
             if (A) acc = acc + w * (double)x;
-            if (F) acc2 = acc2 + w * (double)(x - base[k]);
+            if (F) acc2 = acc2 + w * (double)d;
+            if (WD) D[k * (size_t)ldD + i] = d;
         }
         if (A) part[((size_t)s * nsb + sb) * nbin + i] = acc;
         if (F) part2[((size_t)s * nsb + sb) * nbin + i] = acc2;
@@ -335,26 +343,6 @@ __global__ __launch_bounds__(256) void k_pscrunch(float *__restrict__ raw, const
     }
     for (size_t i = 4 * n4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         raw[i] = raw[i] + pol1[i];
-}
-
-// D[k][i] = f32(ded[k][i] - base0[k])  (fit cube, dedispersed frame); one row per wave step
-__global__ __launch_bounds__(256) void k_fitcube(const float *__restrict__ raw, const int32_t *__restrict__ shift,
-                                                 const float *__restrict__ base, int nsub, int nchan,
-                                                 int nbin, int ldD, float *__restrict__ D)
-{
-    const size_t P = (size_t)nsub * nchan;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (size_t k = (size_t)blockIdx.x * 4 + wave; k < P; k += (size_t)gridDim.x * 4) {
-        const int sh = shift[k % nchan];
-        const float b = base[k];
-        const float *src = raw + k * nbin;
-        float *dst = D + k * ldD;
-        for (int i = lane; i < nbin; i += 64) {
-            int j = i + sh;
-            if (j >= nbin) j -= nbin;
-            dst[i] = src[j] - b;
-        }
-    }
 }
 
 // F[s][i] = f32(num/wsum) (0 if wsum == 0); wf[s] = f32(wsum); num and wsum
@@ -2574,20 +2562,24 @@ static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) 
 
 hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, const float *W, const int32_t *shift,
                                 const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
-                                double *part, double *part2, double *wpart)
+                                double *part, double *part2, double *wpart, float *D, int ldD)
 {
     const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
     dim3 grid(cdiv(nbin, bs), nsb, nsub);
+    if (mode == 3 && (!D || ldD < nbin)) return hipErrorInvalidValue;
+#define IC_CP(M)                                                                                                  \
+    hipLaunchKernelGGL(k_chan_partials<M>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin, \
+                       nsb, part, part2, wpart, D, ldD)
     if (mode == 0)
-        hipLaunchKernelGGL(k_chan_partials<0>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin,
-                           nsb, part, part2, wpart);
+        IC_CP(0);
     else if (mode == 1)
-        hipLaunchKernelGGL(k_chan_partials<1>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin,
-                           nsb, part, part2, wpart);
+        IC_CP(1);
+    else if (mode == 2)
+        IC_CP(2);
     else
-        hipLaunchKernelGGL(k_chan_partials<2>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin,
-                           nsb, part, part2, wpart);
+        IC_CP(3);
+#undef IC_CP
     return hipGetLastError();
 }
 
@@ -2612,15 +2604,6 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
 hipError_t launch_pscrunch(hipStream_t st, float *raw, const float *pol1, size_t n)
 {
     hipLaunchKernelGGL(k_pscrunch, dim3(std::min<unsigned>(cdiv(n / 4 + 1, 256), 8192)), dim3(256), 0, st, raw, pol1, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_fitcube(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
-                          int nsub, int nchan, int nbin, int ldD, float *D)
-{
-    const size_t P = (size_t)nsub * nchan;
-    const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
-    hipLaunchKernelGGL(k_fitcube, dim3(grid), dim3(256), 0, st, raw, shift, base, nsub, nchan, nbin, ldD, D);
     return hipGetLastError();
 }
 

@@ -43,7 +43,7 @@ int fail(int code, const char *fmt, ...)
                         __LINE__);                                                                \
     } while (0)
 
-const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",     "k_fitcube",
+const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",
                                      "k_fscrunch",      "k_tscrunch",  "k_fit_pass", "k_fit_state",
                                      "k_diag",          "k_linestats", "k_combine",  "k_residual",
                                      "k_fit_tail",      "k_sb_tree",   "k_shard_pack", "exchange"};
@@ -412,7 +412,8 @@ int prepare(Session *s)
     if (int rc = window_stage(s, nullptr)) return rc;
     LAUNCH(s, K_BASE,
            launch_base(s->stream, s->raw, s->shift, s->win, nullptr, nsub, nchan, nbin, s->width, s->base0));
-    LAUNCH(s, K_FITCUBE, launch_fitcube(s->stream, s->raw, s->shift, s->base0, nsub, nchan, nbin, s->ldD, s->D));
+    // the fit cube D = f32(ded - base0) is written by iteration 1's template
+    // pass (chan_partials mode 3), which reads the same values
     CK(hipMemcpyAsync(s->base, s->base0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
     CK(hipMemsetAsync(s->wflag + nsub, 0, sizeof(int32_t), s->stream));
     return 0;
@@ -429,10 +430,10 @@ int prepare(Session *s)
 int iteration_template(Session *s, int iter)
 {
     const int nsub = s->p.nsub, nchan = s->nchan, nbin = s->p.nbin;
-    if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s
+    if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s; also writes D
         LAUNCH(s, K_CHAN_PARTIALS,
-               launch_chan_partials(s->stream, 1, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
-                                    nullptr, s->part2, s->wpart));
+               launch_chan_partials(s->stream, 3, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
+                                    nullptr, s->part2, s->wpart, s->D, s->ldD));
     } else {
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, 2, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
@@ -1066,7 +1067,7 @@ int ic_get_residual(void *session, float *out)
     const ic_params &p = s->p;
     int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > p.nbin ? p.nbin : p.pr_start);
     int pr_end = p.pr_end < 0 ? 0 : (p.pr_end > p.nbin ? p.nbin : p.pr_end);
-    // the fit cube buffer `base` is reused as scratch? no: allocate a temporary
+    // temporary output buffer
     float *R = nullptr;
     CK(hipMalloc((void **)&R, sizeof(float) * s->N));
     hipError_t e = launch_residual(s->stream, s->D, s->T64, s->amp, s->info, s->shift, p.nsub, s->nchan, p.nbin,

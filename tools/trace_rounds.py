@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Per-dispatch view of one cleaning run from a rocprofv3 --kernel-trace CSV:
 kernel, grid size (workgroups), duration and the gap before it, for the
-dispatches of the LAST ic_run in the trace (from its last k_fitcube on)."""
+dispatches of the LAST ic_run in the trace (from its last k_chan_partials<0>,
+the first pass of a run, on)."""
 import csv
 import sys
 
@@ -10,10 +11,7 @@ def main(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"].split("(")[0].replace("void ", "").replace("icgpu::", "") for r in rows]
-    last = max(i for i, n in enumerate(names) if n.startswith("k_fitcube"))
-    first = last
-    while first > 0 and names[first - 1].startswith("k_") and not names[first - 1].startswith("k_fitcube"):
-        first -= 1
+    first = max(i for i, n in enumerate(names) if n.startswith("k_chan_partials<0>"))
     prev_end = None
     tot = {}
     for r, n in zip(rows[first - 4:], names[first - 4:]):
