@@ -172,8 +172,9 @@ def pmc_traffic(workload, kernel):
 def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
     """Reference-like loop (per-profile scipy leastsq + numpy.ma), one thread,
     on the first subints of the workload shape: a 2-subint probe sizes the
-    sample to 0.8 * ``budget_s`` by linear extrapolation (about 10-20 s of CPU
-    work in practice: later subints converge in fewer loops)."""
+    sample to 1.3 * ``budget_s`` by linear extrapolation, which lands at about
+    10-20 s of CPU work in practice (the probe's subints need more loops than
+    the whole sample's average)."""
     from threadpoolctl import threadpool_limits
 
     from iterative_cleaner_amd import archive as ica
@@ -186,7 +187,7 @@ def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
         t0 = time.perf_counter()
         reference_like.clean_loop(ar, 5, 5, 5, [0, 0, 1])
         probe = time.perf_counter() - t0
-    nsub = int(max(2, min(64, 2 * 0.8 * budget_s / max(probe, 1e-3))))
+    nsub = int(max(2, min(64, 2 * 1.3 * budget_s / max(probe, 1e-3))))
     data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
     ar = ica.Archive(data, w0, shift)
     ar.pscrunch()
