@@ -224,10 +224,10 @@ def batch_main(a, workload, rank, world, local, dev):
         trio[2].array[:] = shift
         pinned.append(trio)
         items.append(tuple(p.array for p in trio))
-    sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local)
+    sessions = [_native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local) for _ in range(a.lanes)]
     stream = [items[k % 3] for k in range(a.batch)]
     for _ in range(a.warmup):
-        for _out in batch.pipeline(sess, stream, fetch=False):
+        for _out in batch.run_lanes(sessions, stream, fetch=False):
             pass
 
     def barrier():
@@ -239,12 +239,13 @@ def batch_main(a, workload, rank, world, local, dev):
     t0 = time.perf_counter()
     loops = []
     for _ in range(a.steps):
-        for out in batch.pipeline(sess, stream, fetch=False):
+        for out in batch.run_lanes(sessions, stream, fetch=False):
             loops.append(out["loops"])
     t1 = time.perf_counter()
     barrier()
     elapsed = max_over_ranks(t1 - t0, device=dev)
-    sess.close()
+    for sess in sessions:
+        sess.close()
     if rank == 0:
         n_arch = a.steps * a.batch * world
         bytes_arch = 4 * P * nbin
@@ -254,8 +255,8 @@ def batch_main(a, workload, rank, world, local, dev):
             "ms_per_step": round(1000.0 * elapsed / a.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": "%s batch: %d archives of %dx%dx%d per GPU per step from page-locked "
-                                   "host memory, H2D overlapped with cleaning (included)"
-                                   % (workload, a.batch, nsub, nchan, nbin),
+                                   "host memory, H2D overlapped with cleaning (included), %d concurrent "
+                                   "session(s) per GPU" % (workload, a.batch, nsub, nchan, nbin, a.lanes),
                        "archives_per_s": round(n_arch / elapsed, 2),
                        "ms_per_archive": round(1000.0 * elapsed / (a.steps * a.batch), 3),
                        "h2d_gbs_per_gpu": round(bytes_arch * a.steps * a.batch / elapsed / 1e9, 1),
@@ -283,6 +284,8 @@ def main():
                     help="batch mode (config C4): clean this many archives per step per GPU from "
                          "page-locked host memory, each upload overlapped with the previous cleaning "
                          "(H2D included in the time)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="batch mode: concurrent sessions per GPU (each on its own HIP streams)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the channel-shard session even on one GPU (one-rank RCCL group)")
     a = ap.parse_args()

@@ -7,8 +7,14 @@ for every archive of a shape, and the host->device copy of archive k+1 runs on
 the session's copy stream while archive k is cleaned (ic_upload_async, two
 device input slots).  Host staging goes through a ring of page-locked buffers
 filled by a loader thread, so reading/decoding archive k+2 overlaps too.
-Under torchrun every rank runs its own batch (dist.shard of the list): no
-collective.
+
+A C4 archive (128 x 1024 x 512) is too small to fill an MI355X on its own:
+its later fit rounds, the tail and the small reductions leave most CUs idle.
+`lanes` > 1 runs that many sessions, each on its own HIP streams and host
+thread (ctypes drops the GIL during ic_run), pulling archives from one queue,
+so the kernels of different archives overlap on the GPU.  Results come back in
+input order.  Under torchrun every rank runs its own batch (dist.shard of the
+list): no collective.
 """
 from __future__ import annotations
 
@@ -36,6 +42,89 @@ def pipeline(session, items, fetch=True):
     yield session.run(fetch)
 
 
+def run_lanes(sessions, items, fetch=True):
+    """Clean every (cube, w0, shift) of `items` on `len(sessions)` sessions of one
+    shape concurrently (one host thread per session, shared work queue; each
+    session overlaps its next upload with its current run).  The arrays must
+    stay valid until their result is yielded.  Yields the ic_run dicts in input
+    order.  One session: exactly `pipeline`."""
+    if len(sessions) == 1:
+        yield from pipeline(sessions[0], items, fetch)
+        return
+    work = queue.Queue(maxsize=2 * len(sessions))
+    done = queue.Queue()
+
+    def worker(sess):
+        pending = None   # index uploaded to this session, not yet run
+        try:
+            while True:
+                try:
+                    item = work.get_nowait()
+                except queue.Empty:
+                    if pending is not None:   # nothing queued: run what we hold
+                        done.put((pending, sess.run(fetch)))
+                        pending = None
+                        continue
+                    item = work.get()
+                if item is None:
+                    break
+                idx, arrays = item
+                sess.upload_async(*arrays)
+                if pending is not None:
+                    done.put((pending, sess.run(fetch)))
+                pending = idx
+            if pending is not None:
+                done.put((pending, sess.run(fetch)))
+        except BaseException as e:  # noqa: BLE001 - re-raised by the consumer
+            done.put((-1, e))
+
+    threads = [threading.Thread(target=worker, args=(sess,), daemon=True) for sess in sessions]
+    for th in threads:
+        th.start()
+    n = 0
+    feed_error = []
+
+    def feed():
+        nonlocal n
+        try:
+            for arrays in items:
+                work.put((n, arrays))
+                n += 1
+        except BaseException as e:  # noqa: BLE001
+            feed_error.append(e)
+        finally:
+            for _ in threads:
+                work.put(None)
+
+    feeder = threading.Thread(target=feed, daemon=True)
+    feeder.start()
+    ready, nxt, live = {}, 0, len(threads)
+    try:
+        while True:
+            if nxt in ready:
+                yield ready.pop(nxt)
+                nxt += 1
+                continue
+            if live == 0 and not feeder.is_alive():
+                break
+            try:
+                idx, out = done.get(timeout=0.5)
+            except queue.Empty:
+                live = sum(th.is_alive() for th in threads)
+                continue
+            if idx < 0:
+                raise out
+            ready[idx] = out
+        if feed_error:
+            raise feed_error[0]
+        if ready or nxt != n:
+            raise RuntimeError("batch lanes lost archives %d..%d" % (nxt, n - 1))
+    finally:
+        feeder.join(timeout=60)
+        for th in threads:
+            th.join(timeout=60)
+
+
 class _Ring:
     """`n` page-locked (cube, w0, shift) slots."""
 
@@ -53,16 +142,21 @@ class _Ring:
                 p.close()
 
 
-def clean_batch(loader, shape, device=0, ring=3, max_iter=5, chanthresh=5.0, subintthresh=5.0,
-                pulse_region=(0, 0, 1), baseline_duty=0.15):
+def clean_batch(loader, shape, device=0, ring=None, max_iter=5, chanthresh=5.0, subintthresh=5.0,
+                pulse_region=(0, 0, 1), baseline_duty=0.15, lanes=1):
     """Clean the archives produced by `loader` (an iterable of (cube, w0, shift)
     host arrays of one (nsub, nchan, nbin) shape; shift is reduced mod nbin).
     A loader thread copies them into a ring of page-locked slots; the GPU
-    pipeline overlaps each upload with the previous cleaning.  Yields one
-    ic_run dict per archive, in order."""
+    pipeline overlaps each upload with the previous cleaning, on `lanes`
+    concurrent sessions.  Yields one ic_run dict per archive, in order."""
     nsub, nchan, nbin = (int(x) for x in shape)
-    if ring < 3:
-        raise ValueError("ring must hold >= 3 slots (loading, copying, cleaning)")
+    lanes = int(lanes)
+    if lanes < 1:
+        raise ValueError("lanes must be >= 1")
+    if ring is None:
+        ring = 3 * lanes + 1
+    if ring < 3 * lanes:
+        raise ValueError("ring must hold >= 3 slots per lane (loading, copying, cleaning)")
     free = queue.Queue()
     full = queue.Queue(maxsize=ring)
     stop = threading.Event()
@@ -99,15 +193,19 @@ def clean_batch(loader, shape, device=0, ring=3, max_iter=5, chanthresh=5.0, sub
             yield rg.arrays(i)
 
     order = []
+    sessions = []
     try:
-        with _native.GpuSession(nsub, nchan, nbin, max_iter, chanthresh, subintthresh, pulse_region,
-                                baseline_duty, device=device) as sess:
-            for k, out in enumerate(pipeline(sess, staged())):
-                free.put(order[k])          # archive k's slot is free once its run returned
-                yield out
+        for _ in range(lanes):
+            sessions.append(_native.GpuSession(nsub, nchan, nbin, max_iter, chanthresh, subintthresh,
+                                               pulse_region, baseline_duty, device=device))
+        for k, out in enumerate(run_lanes(sessions, staged())):
+            free.put(order[k])          # archive k's slot is free once its result is yielded
+            yield out
         if error:
             raise error[0]
     finally:
+        for sess in sessions:
+            sess.close()
         stop.set()
         for _ in range(ring):
             free.put(0)

@@ -39,6 +39,20 @@ def test_clean_batch_matches_single_sessions():
         assert bits_equal(out["weights"], ref["weights"]) and bits_equal(out["test"], ref["test"])
 
 
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_clean_batch_concurrent_lanes_match_single_sessions(lanes):
+    """Several sessions cleaning concurrently on their own streams: same bits,
+    results in input order."""
+    from iterative_cleaner_amd import batch
+    arcs = _archives(8)
+    got = list(batch.clean_batch(iter(arcs), SHAPE, device=0, lanes=lanes))
+    assert len(got) == len(arcs)
+    for (cube, w0, shift), out in zip(arcs, got):
+        ref = _one(cube, w0, shift)
+        assert out["loops"] == ref["loops"] and np.array_equal(out["changed"], ref["changed"])
+        assert bits_equal(out["weights"], ref["weights"]) and bits_equal(out["test"], ref["test"])
+
+
 def test_pipeline_on_pinned_arrays_and_queue_rules():
     from iterative_cleaner_amd import _native, batch
     arcs = _archives(3)

@@ -1,0 +1,54 @@
+"""Host logic of the batch scheduler's concurrent lanes (batch.run_lanes), on
+stand-in sessions: results in input order, every archive exactly once, the
+upload-before-run discipline per session, and errors re-raised."""
+import random
+import threading
+import time
+
+import pytest
+
+
+class FakeSession:
+    """Records the ic_upload_async / ic_run protocol of one session."""
+
+    def __init__(self, fail_on=None):
+        self.queue = []        # uploaded, not yet run (FIFO, at most 2 deep)
+        self.ran = []
+        self.fail_on = fail_on
+        self.lock = threading.Lock()
+
+    def upload_async(self, tag, *_):
+        with self.lock:
+            assert len(self.queue) < 2, "more than two uploads in flight"
+            self.queue.append(tag)
+
+    def run(self, fetch=True):
+        with self.lock:
+            tag = self.queue.pop(0)
+        time.sleep(random.random() * 0.003)
+        if tag == self.fail_on:
+            raise RuntimeError("boom %d" % tag)
+        self.ran.append(tag)
+        return {"tag": tag}
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 3, 5])
+def test_run_lanes_order_and_coverage(lanes):
+    from iterative_cleaner_amd import batch
+    random.seed(lanes)
+    sessions = [FakeSession() for _ in range(lanes)]
+    items = [(k, None, None) for k in range(23)]
+    got = [out["tag"] for out in batch.run_lanes(sessions, items)]
+    assert got == list(range(23))
+    assert sorted(t for s in sessions for t in s.ran) == list(range(23))
+    assert all(not s.queue for s in sessions)
+    if lanes > 1:
+        assert sum(1 for s in sessions if s.ran) > 1   # the work was actually shared
+
+
+def test_run_lanes_empty_and_error():
+    from iterative_cleaner_amd import batch
+    assert list(batch.run_lanes([FakeSession(), FakeSession()], [])) == []
+    sessions = [FakeSession(fail_on=7), FakeSession(fail_on=7)]
+    with pytest.raises(RuntimeError, match="boom 7"):
+        list(batch.run_lanes(sessions, [(k, None, None) for k in range(12)]))
