@@ -169,6 +169,26 @@ def pmc_traffic(workload, kernel):
     return None, None
 
 
+VALU_PEAK_G = 614.4   # wave64 VALU instructions/s (G): 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles each
+
+
+def pmc_valu(workload):
+    """SQ_INSTS_VALU per launch for every kernel from the committed SQ pass
+    (tools/pmc_valu.sh), only when it was measured on the HIP sources being
+    timed (source_sha).  The kernels of the exact fit and the diagnostics are
+    f64-VALU-bound, not HBM-bound: this is the roof they are priced against."""
+    import glob
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from pmc_traffic import source_sha
+    sha = source_sha()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_valu*.json")), reverse=True):
+        with open(path) as f:
+            rec = json.load(f)
+        if rec.get("workload") == workload and rec.get("source_sha") == sha:
+            return rec["kernels"], os.path.basename(path)
+    return None, None
+
+
 def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
     """Reference-like loop (per-profile scipy leastsq + numpy.ma), one thread,
     on the first subints of the workload shape: a 2-subint probe sizes the
@@ -394,6 +414,20 @@ def main():
         traffic, src = pmc_traffic(workload if not sharded else "%s/%d" % (workload, world), dom)
         roof["traffic"] = traffic
         roof["traffic_source"] = src if traffic else "no PMC summary for these HIP sources"
+        valu, vsrc = pmc_valu(workload if not sharded else "%s/%d" % (workload, world))
+        if valu:
+            for kname, pk in per_kernel.items():
+                v = valu.get(kname)
+                kv = ktimes[kname]
+                if v and v["launches"] and kv["launches"]:
+                    g = v["valu_insts_per_launch"] / (kv["ms"] / kv["launches"] / 1000.0) / 1e9
+                    pk["valu_frac"] = round(g / VALU_PEAK_G, 3)
+            v = valu.get(dom)
+            if v:
+                g = v["valu_insts_per_launch"] / avg_s / 1e9
+                roof["valu"] = {"achieved": round(g, 1), "peak": VALU_PEAK_G, "unit": "G wave64 VALU inst/s",
+                                "frac": round(g / VALU_PEAK_G, 4), "insts_per_launch": v["valu_insts_per_launch"],
+                                "f64_share": v["f64_share_of_valu"], "source": vsrc}
         roof["per_kernel"] = per_kernel
         iter_bytes = 8 * per_rank_P * nbin + 64 * per_rank_P    # SURVEY §8(d) B_iter, one GPU's share
         loop_gbs = iter_bytes * n_iter / (elapsed / a.steps) / 1e9
