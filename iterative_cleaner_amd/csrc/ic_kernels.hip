@@ -390,7 +390,26 @@ __global__ __launch_bounds__(256) void k_tscrunch(const float *__restrict__ F, c
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nbin) return;
     double wt = 0.0, num = 0.0;
-    for (int s = 0; s < nsub; ++s) {
+    // batches of 16 subints: the 16 loads are in flight together, then the
+    // sums run in subint order (the chain is latency-bound with 16 blocks)
+    constexpr int B = 16;
+    int s = 0;
+    for (; s + B <= nsub; s += B) {
+        float fv[B], wv[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            wv[q] = wf[s + q];
+            fv[q] = F[(size_t)(s + q) * nbin + i];
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            const double w = (double)wv[q];
+            wt = wt + w;
+            const double t = w * (double)fv[q];
+            num = num + t;
+        }
+    }
+    for (; s < nsub; ++s) {
         const double w = (double)wf[s];
         wt = wt + w;
         const double t = w * (double)F[(size_t)s * nbin + i];
