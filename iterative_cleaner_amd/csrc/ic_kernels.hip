@@ -218,15 +218,19 @@ __device__ __forceinline__ bool argmin_better(double va, int ia, double vb, int 
 
 // One block per subint: tot[i] = sb_tree over the leaves of part; m[j] =
 // sum_{k<width} tot[(j+k)%n]; win[s] = first argmin.
-// flags != nullptr: flags[s] = (window moved), win[s] updated in place
-__global__ __launch_bounds__(256) void k_window(const double *__restrict__ part, long ss, long sl, SbPlan plan,
+// flags != nullptr: flags[s] = (window moved), win[s] updated in place.
+// kWindowThreads threads, so each window sum (a width-long in-order chain) has
+// its own thread up to nbin = 1024.  The argmin order (NaN first, then value,
+// then index) is total, so the result does not depend on the block size.
+constexpr int kWindowThreads = 1024;
+__global__ __launch_bounds__(kWindowThreads) void k_window(const double *__restrict__ part, long ss, long sl, SbPlan plan,
                                                 int nbin, int width, int32_t *__restrict__ win,
                                                 int32_t *__restrict__ flags)
 {
     extern __shared__ double sh[];
     double *tot = sh;                       // nbin
-    double *bv = sh + nbin;                 // 256
-    int *bi = (int *)(bv + 256);            // 256
+    double *bv = sh + nbin;                 // blockDim
+    int *bi = (int *)(bv + blockDim.x);     // blockDim
     const int s = blockIdx.x;
     for (int i = threadIdx.x; i < nbin; i += blockDim.x) {
         const double *src = part + (size_t)s * ss + i;
@@ -2606,8 +2610,8 @@ hipError_t launch_window(hipStream_t st, const double *part, long ss, long sl, c
                          int nbin, int width, int32_t *win, int32_t *flags)
 {
     if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
-    const size_t shm = (size_t)nbin * 8 + 256 * 8 + 256 * 4;
-    hipLaunchKernelGGL(k_window, dim3(nsub), dim3(256), shm, st, part, ss, sl, plan, nbin, width, win, flags);
+    const size_t shm = (size_t)nbin * 8 + kWindowThreads * (8 + 4);
+    hipLaunchKernelGGL(k_window, dim3(nsub), dim3(kWindowThreads), shm, st, part, ss, sl, plan, nbin, width, win, flags);
     return hipGetLastError();
 }
 
