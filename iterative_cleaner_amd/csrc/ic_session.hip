@@ -488,8 +488,9 @@ int run_fit(Session *s)
     const long P = (long)s->P;
     const int nbin = s->p.nbin;
     CK(launch_fit_init(s->stream, s->fs, P));
-    CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * (2 * kMaxRounds + 2), s->stream));
-    // per round: blocks done << 32 | survivors; then the tail's sweep counter
+    // per round: blocks done << 32 | survivors; then the tail's sweep counter,
+    // which accumulates over the run (zeroed and read once per run by ic_run)
+    CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * 2 * kMaxRounds, s->stream));
     unsigned long long *ctr = (unsigned long long *)s->rcount;
     unsigned long long *tail_sweeps = ctr + kMaxRounds;
     int32_t *bufs[2] = {s->lists, s->lists + P};
@@ -522,7 +523,9 @@ int run_fit(Session *s)
             bound = c;
         }
     }
-    CK(hipStreamSynchronize(s->stream));
+    // no stream synchronisation: the counts below were all read by the loop
+    // (after the event of their round), so the diagnostics queue right behind
+    // the last fit kernel
     int64_t swept = rounds > 0 ? P : 0;   // round 0 input
     for (int r = 0; r + 1 < rounds; ++r) swept += s->h_rcount[r];
     int effective = rounds;
@@ -530,12 +533,9 @@ int run_fit(Session *s)
         // trailing rounds that had an empty input list
         while (effective > 1 && s->h_rcount[effective - 2] == 0) --effective;
     }
-    unsigned long long tsw = 0;
-    CK(hipMemcpy(&tsw, tail_sweeps, sizeof tsw, hipMemcpyDeviceToHost));
     s->fit_rounds = effective;
     s->stats.fit_rounds += effective;
     s->stats.fit_profile_sweeps += swept;
-    s->stats.fit_tail_sweeps += (int64_t)tsw;
     return 0;
 }
 
@@ -991,6 +991,8 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     la.row_mad = s->lstat + 8 * nchan + 4 * nsub;
     std::vector<int32_t> cnt(p.max_iter + 4);
     int x = 0, loops = -1, n_iter = 0, converged = 0;
+    // k_fit_tail's sweep counter (after the per-round counters): one run's total
+    CK(hipMemsetAsync((unsigned long long *)s->rcount + kMaxRounds, 0, sizeof(unsigned long long), s->stream));
     while (x < p.max_iter) {
         x += 1;
         ++n_iter;
@@ -1034,6 +1036,9 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         int32_t moves = 0;
         CK(hipMemcpy(&moves, s->wflag + nsub, sizeof moves, hipMemcpyDeviceToHost));
         s->stats.window_moves = moves;
+        unsigned long long tsw = 0;
+        CK(hipMemcpy(&tsw, (unsigned long long *)s->rcount + kMaxRounds, sizeof tsw, hipMemcpyDeviceToHost));
+        s->stats.fit_tail_sweeps += (int64_t)tsw;
     }
     if (int rc = collect_timing(s)) return rc;
     if (loops_out) *loops_out = loops;
