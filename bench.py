@@ -126,10 +126,27 @@ def make_block_cube_device(nsub, nchan, nbin, seed, rfi, c0, c1, device):
     return cube.contiguous(), w0.contiguous(), shift.contiguous()
 
 
+def s8d_bytes(name, nsub, nchan, nbin, launches, iterations, steps):
+    """SURVEY.md §8(d) algorithmic bytes of a kernel over the timed region: the
+    cube is read once per iteration by the template stage (k_chan_partials) and
+    once by the fit + diagnostics stage (k_fit_pass + k_diag together in the
+    exact mode, k_diag alone in the closed-form mode); the 4 f64 diagnostics
+    are written and read once (64 B per profile).  Re-reads an implementation
+    chooses (lmdif's 5.5 sweeps per profile) are NOT algorithmic."""
+    P = nsub * nchan
+    N = P * nbin
+    per_iter = {"k_chan_partials": 4 * N, "k_fit_pass": 4 * N, "k_diag": 4 * N + 32 * P,
+                "k_linestats": 16 * P, "k_combine": 16 * P}
+    if name not in per_iter:
+        return None
+    return per_iter[name] * iterations * steps
+
+
 def algorithmic_bytes(name, nsub, nchan, nbin, launches, stats, steps):
-    """Algorithmic bytes a kernel must move, summed over the timed region
-    (kernel table).  k_fit_pass: every profile-sweep reads its
-    4*nbin-byte profile once (sweep counts come from ic_get_run_stats)."""
+    """Bytes a kernel's launches actually sweep, summed over the timed region
+    (kernel table) - the implementation's own traffic model, not
+    §8(d)'s.  k_fit_pass: every profile-sweep reads its 4*nbin-byte profile once
+    (sweep counts come from ic_get_run_stats)."""
     P = nsub * nchan
     N = P * nbin
     nsb = (nchan + 255) // 256
@@ -217,9 +234,23 @@ def cpu_baseline(nchan, nbin, seed, rfi, budget_s):
         dt = time.perf_counter() - t0
     P = nsub * nchan
     return {"value": P / dt, "unit": "profiles/s", "cores": 1, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": "%dx%dx%d subset of the workload shape, full loop to convergence "
-                      "(%d loops) in %.1f s, single thread (oracle/reference_like.py)"
+                      "(%d loops) in %.1f s, single thread (oracle/reference_like.py); profiles/s of the "
+                      "sample, i.e. extrapolated linearly per profile to the full archive"
                       % (nsub, nchan, nbin, loops, dt)}
+
+
+def cpu_model() -> str:
+    """The host CPU model (lscpu's "Model name", read from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def batch_main(a, workload, rank, world, local, dev):
@@ -308,6 +339,10 @@ def main():
                     help="batch mode: concurrent sessions per GPU (each on its own HIP streams)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the channel-shard session even on one GPU (one-rank RCCL group)")
+    ap.add_argument("--fit-mode", choices=("exact", "closed"), default="exact",
+                    help="exact: scipy leastsq emulated bit for bit (the reference's arithmetic, default); "
+                         "closed: the closed-form amplitude fused with the diagnostics (fit_mode 1, fast mode; "
+                         "also reports the zap-mask flips against the exact mode on the same archive)")
     a = ap.parse_args()
 
     import torch
@@ -316,6 +351,7 @@ def main():
     from iterative_cleaner_amd import _native
     from iterative_cleaner_amd.dist import TorchComm, max_over_ranks, rank_world
 
+    fit_mode = _native.FIT_CLOSED if a.fit_mode == "closed" else _native.FIT_EXACT
     rank, world, local = rank_world()
     if world != a.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
@@ -345,19 +381,29 @@ def main():
         c0, c1 = chans[rank]
         cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, c0, c1, dev)
         comm = TorchComm(dev)
-        sess = _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm, max_iter=5, device=local)
+        sess = _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm, max_iter=5, device=local,
+                                    fit_mode=fit_mode)
         per_rank_P = nsub * (c1 - c0)
     else:
         if workload in BLOCKWISE:
             cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, 0, nchan, dev)
         else:
             cube, w0, shift = make_cube_device(nsub, nchan, nbin, seed + 7919 * rank, rfi, dev)
-        sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local)
+        sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local, fit_mode=fit_mode)
         per_rank_P = P_total
         if world > 1:
             P_total = P_total * world          # replicas: every rank cleans its own archive
     torch.cuda.synchronize()
     sess.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
+    flips = None
+    if fit_mode == _native.FIT_CLOSED and not sharded:
+        # zap-mask flips of the fast mode against the exact fit on this archive (untimed)
+        fast = sess.run()
+        with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local) as ex:
+            ex.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
+            exact = ex.run()
+        flips = {"profiles": int(np.count_nonzero(fast["weights"] != exact["weights"])),
+                 "loops_fast": fast["loops"], "loops_exact": exact["loops"]}
     del cube
     torch.cuda.empty_cache()
     for _ in range(a.warmup):
@@ -393,28 +439,42 @@ def main():
         dom = max(kernels, key=lambda k: kernels[k]["ms"])
         dk = kernels[dom]
         avg_s = dk["ms"] / 1000.0 / max(1, dk["launches"])
+        # implementation bytes (every sweep the kernel makes) and SURVEY §8(d) bytes
         total_bytes = algorithmic_bytes(dom, nsub, lnchan, nbin, dk["launches"], stats, a.steps)
-        bytes_launch = total_bytes / max(1, dk["launches"]) if total_bytes else None
-        achieved = bytes_launch / avg_s / 1e9 if bytes_launch else None
-        roof = {"bound": "hbm", "kernel": dom,
-                "achieved": round(achieved, 1) if achieved else None,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": None, "avg_launch_ms": round(1000 * avg_s, 3),
-                "algorithmic_bytes_per_launch": int(bytes_launch) if bytes_launch else None,
-                "kernel_share": round(dk["ms"] / total_k, 3)}
+        sweep_launch = total_bytes / max(1, dk["launches"]) if total_bytes else None
+        s8d_total = s8d_bytes(dom, nsub, lnchan, nbin, dk["launches"], n_iter, a.steps)
+        s8d_launch = s8d_total / max(1, dk["launches"]) if s8d_total else None
+        hbm_s8d = s8d_launch / avg_s / 1e9 if s8d_launch else None
+        sweep_gbs = sweep_launch / avg_s / 1e9 if sweep_launch else None
         per_kernel = {}
         for kname, kv in ktimes.items():
             if kv["launches"] == 0:
                 continue
             tb = algorithmic_bytes(kname, nsub, lnchan, nbin, kv["launches"], stats, a.steps)
-            per_kernel[kname] = {"ms_per_step": round(kv["ms"] / a.steps, 3),
-                                 "launches_per_step": kv["launches"] // a.steps,
-                                 "gbs": round(tb / (kv["ms"] / 1000.0) / 1e9, 1) if tb else None}
-        traffic, src = pmc_traffic(workload if not sharded else "%s/%d" % (workload, world), dom)
-        roof["traffic"] = traffic
-        roof["traffic_source"] = src if traffic else "no PMC summary for these HIP sources"
-        valu, vsrc = pmc_valu(workload if not sharded else "%s/%d" % (workload, world))
+            pk = {"ms_per_step": round(kv["ms"] / a.steps, 3), "launches_per_step": kv["launches"] // a.steps,
+                  "sweep_gbs": round(tb / (kv["ms"] / 1000.0) / 1e9, 1) if tb else None}
+            sb = s8d_bytes(kname, nsub, lnchan, nbin, kv["launches"], n_iter, a.steps)
+            if sb:
+                pk["s8d_gbs"] = round(sb / (kv["ms"] / 1000.0) / 1e9, 1)
+            per_kernel[kname] = pk
+        wl_key = workload if not sharded else "%s/%d" % (workload, world)
+        if fit_mode == _native.FIT_CLOSED:
+            wl_key += "/closed"
+        traffic, src = pmc_traffic(wl_key, dom)
+        valu, vsrc = pmc_valu(wl_key)
+        hbm = {"achieved": round(hbm_s8d, 1) if hbm_s8d else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(hbm_s8d / HBM_PEAK_GBS, 4) if hbm_s8d else None,
+               "algorithmic_bytes_per_launch": int(s8d_launch) if s8d_launch else None,
+               "definition": "SURVEY §8(d) bytes: one 4N cube read per iteration for the fit (+ diagnostics) "
+                             "and one for the template, divided over the kernel's launches"}
+        roof = {"bound": "hbm", "kernel": dom, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": hbm["frac"], "traffic": traffic,
+                "traffic_source": src if traffic else "no PMC summary for these HIP sources",
+                "avg_launch_ms": round(1000 * avg_s, 3), "kernel_share": round(dk["ms"] / total_k, 3),
+                "hbm_frac_s8d": hbm["frac"], "hbm_s8d": hbm,
+                "sweep_bytes": {"per_launch": int(sweep_launch) if sweep_launch else None,
+                                "gbs": round(sweep_gbs, 1) if sweep_gbs else None,
+                                "definition": "every data sweep the kernel makes (lmdif re-sweeps included)"}}
         if valu:
             for kname, pk in per_kernel.items():
                 v = valu.get(kname)
@@ -425,12 +485,15 @@ def main():
             v = valu.get(dom)
             if v:
                 g = v["valu_insts_per_launch"] / avg_s / 1e9
-                roof["valu"] = {"achieved": round(g, 1), "peak": VALU_PEAK_G, "unit": "G wave64 VALU inst/s",
-                                "frac": round(g / VALU_PEAK_G, 4), "insts_per_launch": v["valu_insts_per_launch"],
-                                "f64_share": v["f64_share_of_valu"], "source": vsrc}
+                # the dominant kernel is f64-VALU-bound: that is its roof
+                roof.update({"bound": "valu", "achieved": round(g, 1), "peak": VALU_PEAK_G,
+                             "unit": "G wave64 VALU inst/s", "frac": round(g / VALU_PEAK_G, 4),
+                             "insts_per_launch": v["valu_insts_per_launch"],
+                             "f64_share": v["f64_share_of_valu"], "valu_source": vsrc})
         roof["per_kernel"] = per_kernel
         iter_bytes = 8 * per_rank_P * nbin + 64 * per_rank_P    # SURVEY §8(d) B_iter, one GPU's share
         loop_gbs = iter_bytes * n_iter / (elapsed / a.steps) / 1e9
+        roof["loop_hbm_frac"] = round(loop_gbs / HBM_PEAK_GBS, 4)
         if sharded:
             parallelism = "channel-sharded x%d (RCCL per iteration: 3 all-to-alls to row owners, " \
                           "3 all-gathers of owner results, 1 all-reduce)" % world
@@ -442,8 +505,11 @@ def main():
             "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "strong" if sharded else "weak",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "%s %dx%dx%d (nsub x nchan x nbin), max_iter 5, thresholds 5/5,"
-                                   " exact leastsq fit" % (workload, nsub, nchan, nbin),
+            "config": {"workload": "%s %dx%dx%d (nsub x nchan x nbin), max_iter 5, thresholds 5/5, %s"
+                                   % (workload, nsub, nchan, nbin,
+                                      "exact leastsq fit" if fit_mode == _native.FIT_EXACT else
+                                      "closed-form fit (fit_mode 1: fast mode, not the reference's arithmetic)"),
+                       "fit_mode": a.fit_mode,
                        "profiles_per_archive": nsub * nchan, "loops": loops[-1], "iterations": n_iter,
                        "fit_rounds": stats["fit_rounds"],
                        "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"])
@@ -454,6 +520,8 @@ def main():
                        "loop_hbm_frac": round(loop_gbs / HBM_PEAK_GBS, 4)},
             "roofline": roof,
         }
+        if flips is not None:
+            rec["config"]["mask_flips_vs_exact"] = flips
         if "exchange" in ktimes and ktimes["exchange"]["launches"]:
             rec["config"]["exchange_ms_per_step"] = round(ktimes["exchange"]["ms"] / a.steps, 3)
         if world == 1 and not a.no_cpu_baseline:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define IC_ABI_VERSION 3
+#define IC_ABI_VERSION 4
 
 #define IC_OK 0
 #define IC_EINVAL -1   /* bad argument / shape                         */
@@ -53,8 +53,23 @@ typedef struct {
     double pr_factor;          /* pulse_region[0] (:283)                       */
     int32_t pr_start, pr_end;  /* slice(int(pr[1]), int(pr[2])).indices(nbin) */
     double baseline_duty;      /* archive stand-in remove_baseline duty (0.15) */
-    int32_t fit_mode;          /* 0 = exact scipy leastsq emulation (default)  */
+    int32_t fit_mode;          /* IC_FIT_EXACT (default) or IC_FIT_CLOSED       */
 } ic_params;
+
+/* ic_params.fit_mode.
+ *   IC_FIT_EXACT   scipy.optimize.leastsq(a*T - p, [1.0]) emulated bit for bit
+ *                  (MINPACK lmdif, n = 1; iterative_cleaner.py:277-278): the
+ *                  reference's arithmetic, zap masks identical to it.
+ *   IC_FIT_CLOSED  the closed-form least-squares amplitude
+ *                  a = sum_i T_i p_i / sum_i T_i^2 (f64 numpy pairwise sums over
+ *                  the dedispersed profile; a = 0 when the template is all zero;
+ *                  info = 1, or 5 (residual zeroed) when a is not finite), fused
+ *                  with the residual and the diagnostics in one sweep of the raw
+ *                  cube: the HBM-bound fast mode of the north star.  It is NOT
+ *                  the reference's arithmetic: amplitudes differ from leastsq in
+ *                  the last bits, and rarely a profile's zap decision flips. */
+#define IC_FIT_EXACT 0
+#define IC_FIT_CLOSED 1
 
 /* Library / device info. */
 int ic_abi_version(void);
@@ -148,6 +163,16 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
 int ic_set_fit_tail(void *session, int64_t threshold);
 
 const char *ic_last_error(void);
+
+/* comprehensive_stats (iterative_cleaner.py:181-226) alone, on the GPU, for
+ * the data the reference hands it (:111-117): data [nsub][nchan][nbin] f32 and
+ * weights [nsub][nchan] f32; the kernel forms X = f32(data * w), masked where
+ * w == 0, computes the four diagnostics (:206-217), their channel / subint
+ * median-MAD scaling (:219-224) and test [nsub*nchan] f64 = the median of the
+ * four (:225).  std/mean/ptp/fftmax outputs may be NULL.  Synchronous. */
+int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const float *data, const float *weights,
+                           double chanthresh, double subintthresh, double *test_out, double *std_out,
+                           double *mean_out, float *ptp_out, double *fftmax_out);
 
 /* ------------------------------------------------------------------------
  * Channel-sharded cleaning of ONE archive across `world` shards (config C3,

@@ -13,7 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # IC_LIBRARY: an alternative build of the same library (A/B measurements)
 LIB_PATH = os.environ.get("IC_LIBRARY") or os.path.join(HERE, "libicgpu.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # symbols exported by libicgpu.so, as declared in include/iterative_cleaner.h
 EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session_destroy",
@@ -22,7 +22,10 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_set_timing", "ic_get_run_stats", "ic_set_fit_tail", "ic_last_error",
            "ic_shard_layout", "ic_session_create_shard", "ic_group_create", "ic_group_destroy",
            "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free",
-           "ic_upload_pols")
+           "ic_upload_pols", "ic_comprehensive_stats")
+
+FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)
+FIT_CLOSED = 1   # IC_FIT_CLOSED: closed-form amplitude fused with the diagnostics (fast mode)
 
 
 class NativeError(RuntimeError):
@@ -128,6 +131,8 @@ def load_library(path: str = LIB_PATH):
     lib.ic_group_destroy.argtypes = [vp]
     lib.ic_group_destroy.restype = None
     lib.ic_session_create_grouped.argtypes = [C.POINTER(Params), C.c_int, vp, C.c_int, C.POINTER(vp)]
+    lib.ic_comprehensive_stats.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_double, C.c_double,
+                                           vp, vp, vp, vp, vp]
     if lib.ic_abi_version() != ABI_VERSION:
         raise NativeError("libicgpu ABI %d != expected %d" % (lib.ic_abi_version(), ABI_VERSION))
     _lib = lib
@@ -162,13 +167,14 @@ class GpuSession:
     """One cleaning session on one GPU (wraps ic_session_*)."""
 
     def __init__(self, nsub, nchan, nbin, max_iter=5, chanthresh=5.0, subintthresh=5.0,
-                 pulse_region=(0, 0, 1), baseline_duty=0.15, device=0):
+                 pulse_region=(0, 0, 1), baseline_duty=0.15, device=0, fit_mode=FIT_EXACT):
         self.lib = load_library()
         self.shape = (int(nsub), int(nchan), int(nbin))
         self.max_iter = int(max_iter)
+        self.fit_mode = int(fit_mode)
         on, fac, a, b = normalise_pulse_region(list(pulse_region), int(nbin))
         self.params = Params(int(nsub), int(nchan), int(nbin), int(max_iter), float(chanthresh),
-                             float(subintthresh), on, fac, a, b, float(baseline_duty), 0)
+                             float(subintthresh), on, fac, a, b, float(baseline_duty), self.fit_mode)
         h = C.c_void_p()
         rc = self._create(int(device), h)
         if rc != 0:
@@ -302,6 +308,26 @@ class GpuSession:
             name = self.lib.ic_kernel_name(buf[q].kernel).decode()
             out[name] = dict(ms=buf[q].ms, launches=buf[q].launches)
         return out
+
+
+def comprehensive_stats(data, weights, chanthresh=5.0, subintthresh=5.0, device=0, diagnostics=False):
+    """comprehensive_stats (iterative_cleaner.py:181-226) on the GPU for the
+    (nsub, nchan, nbin) data and (nsub, nchan) weights the reference masks and
+    weights at :111-117; returns test [, (std, mean, ptp, fftmax)]."""
+    lib = load_library()
+    data = np.ascontiguousarray(data, dtype=np.float32)
+    if data.ndim != 3:
+        raise ValueError("comprehensive_stats: data must be (nsub, nchan, nbin)")
+    nsub, nchan, nbin = data.shape
+    w = np.ascontiguousarray(weights, dtype=np.float32).reshape(nsub, nchan)
+    test = np.empty((nsub, nchan), np.float64)
+    sd, mn, ff = (np.empty((nsub, nchan), np.float64) for _ in range(3)) if diagnostics else (None,) * 3
+    pt = np.empty((nsub, nchan), np.float32) if diagnostics else None
+    rc = lib.ic_comprehensive_stats(int(device), nsub, nchan, nbin, _ptr(data), _ptr(w), float(chanthresh),
+                                    float(subintthresh), _ptr(test), _ptr(sd), _ptr(mn), _ptr(pt), _ptr(ff))
+    if rc != 0:
+        raise NativeError("ic_comprehensive_stats: %s (rc=%d)" % (_err(lib), rc))
+    return (test, (sd, mn, pt, ff)) if diagnostics else test
 
 
 class PinnedArray:

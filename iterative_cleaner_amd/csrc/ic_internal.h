@@ -62,6 +62,7 @@ enum KernelId {
     K_SB_TREE,
     K_SHARD_PACK,     // pack / assemble / unpack of shard exchanges
     K_EXCHANGE,       // the collectives themselves (host transport or peer copies)
+    K_TNORM,          // fit_mode 1: sum(T*T)
     K_COUNT
 };
 
@@ -96,6 +97,8 @@ hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, cons
 // gathered shard roots)
 hipError_t launch_window(hipStream_t st, const double *part, long ss, long sl, const SbPlan &plan, int nsub,
                          int nbin, int width, int32_t *win, int32_t *flags);
+// dynamic LDS of k_window (nbin doubles + per-thread partials)
+size_t window_lds_bytes(int nbin);
 // flags != nullptr: only subints with flags[s] != 0
 hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, const int32_t *win,
                        const int32_t *flags, int nsub, int nchan, int nbin, int width, float *base);
@@ -143,12 +146,37 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
                            double *amp, int32_t *info, unsigned long long *sweeps);
+// Diagnostics kernels (k_diag_p2<N> for power-of-two nbin 64..4096, k_diag
+// otherwise).  mode: DIAG_EXACT = residual from the exact fit's amp/info and
+// the fit cube D (row stride ldD); DIAG_CLOSED = fit_mode 1, the closed-form
+// amplitude sum(T*p)/TT from raw + base (written to amp/info), then the same
+// residual; DIAG_STATS = comprehensive_stats of the rows of D alone (no shift).
 // tw: exp(-2 pi i q/nbin), q < nbin; tw_p2 (power-of-two nbin only): see p2_twiddles()
-hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const double *amp,
-                       const int32_t *info, const float *w0, const int32_t *shift, const double2 *tw,
-                       const double2 *tw_p2, const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
-                       int pr_start, int pr_end, double *std_o, double *mean_o, float *ptp_o,
-                       double *fft_o);
+enum DiagMode { DIAG_EXACT = 0, DIAG_CLOSED = 1, DIAG_STATS = 2 };
+struct DiagArgs {
+    int mode;
+    const float *D;
+    int ldD;
+    const float *raw, *base;
+    const double *T64, *TT;
+    double *amp;
+    int32_t *info;
+    const float *w0;
+    const int32_t *shift;
+    const double2 *tw, *tw_p2;
+    const PwPlan *plan;
+    int nsub, nchan, nbin;
+    int pr_on;
+    double pr_factor;
+    int pr_start, pr_end;
+    double *std_o, *mean_o, *fft_o;
+    float *ptp_o;
+};
+hipError_t launch_diag(hipStream_t st, const DiagArgs &a);
+// dynamic LDS the generic k_diag needs for one wave (0 for the power-of-two kernels)
+size_t diag_lds_bytes(int nbin);
+// *TT = numpy pairwise sum of T64[i]^2 over nbin (plan), nleaf_ub >= plan leaves/ops
+hipError_t launch_tnorm(hipStream_t st, const double *T64, const PwPlan *plan, int nleaf_ub, double *TT);
 // which: bit 0 = column lines (length nsub), bit 1 = row lines (length nchan)
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which = 3);
 hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const float *w0,
@@ -157,8 +185,9 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
                           const double *row_med, const double *row_mad, double chanthresh,
                           double subintthresh, double *test, float *W, float *hist, int iter,
                           int32_t *counters);
-hipError_t launch_residual(hipStream_t st, const float *D, const double *T64, const double *amp,
-                           const int32_t *info, const int32_t *shift, int nsub, int nchan, int nbin, int ldD,
-                           int pr_on, double pr_factor, int pr_start, int pr_end, float *R);
+// D == nullptr: fit-cube rows formed from raw and base (fit_mode 1)
+hipError_t launch_residual(hipStream_t st, const float *D, const float *raw, const float *base, const double *T64,
+                           const double *amp, const int32_t *info, const int32_t *shift, int nsub, int nchan,
+                           int nbin, int ldD, int pr_on, double pr_factor, int pr_start, int pr_end, float *R);
 
 }  // namespace icgpu

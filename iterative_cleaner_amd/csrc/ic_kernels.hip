@@ -1593,7 +1593,7 @@ __device__ __forceinline__ void stockham_stage(Get get, double2 *dst, int m, int
 
 struct DiagLayout {
     int ntw;          // twiddles in LDS
-    size_t cw_off, x_off, scr_off, per_wave;
+    size_t cw_off, x_off, p_off, scr_off, per_wave;
 };
 
 __host__ __device__ inline DiagLayout diag_layout(int n, int nleaf, int nops)
@@ -1605,58 +1605,86 @@ __host__ __device__ inline DiagLayout diag_layout(int n, int nleaf, int nops)
     const size_t cwb = (size_t)(pow2 ? n / 2 : 1) * 16;
     L.x_off = cwb;                                           // buffer B (n/2 complex) aliases X (n f32)
     const size_t xb = ((size_t)n * 4 + 15) & ~(size_t)15;
-    L.scr_off = L.x_off + (pow2 ? (cwb > xb ? cwb : xb) : xb);
+    L.p_off = L.x_off + (pow2 ? (cwb > xb ? cwb : xb) : xb);  // DIAG_CLOSED: the fit-cube row
+    L.scr_off = L.p_off + xb;
     L.per_wave = L.scr_off + (size_t)(nleaf * 9 + nops + 8) * 8;
     L.per_wave = (L.per_wave + 15) & ~(size_t)15;
     return L;
 }
 
-__global__ __launch_bounds__(256) void k_diag(
-    const float *__restrict__ D, const double *__restrict__ T64, const double *__restrict__ amp,
-    const int32_t *__restrict__ info, const float *__restrict__ w0, const int32_t *__restrict__ shift,
-    const double2 *__restrict__ tw_g, const PwPlan *__restrict__ plan_g, int nsub, int nchan, int nbin, int ldD,
-    int pr_on, double pr_factor, int pr_start, int pr_end, double *__restrict__ std_o,
-    double *__restrict__ mean_o, float *__restrict__ ptp_o, double *__restrict__ fft_o)
+__global__ __launch_bounds__(256) void k_diag(DiagArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ PwPlan pl;
-    const int n = nbin;
+    const int n = a.nbin;
     const int wpb = blockDim.x >> 6;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     {
-        const int32_t *src = (const int32_t *)plan_g;
+        const int32_t *src = (const int32_t *)a.plan;
         int32_t *dst = (int32_t *)&pl;
         for (int q = threadIdx.x; q < (int)(sizeof(PwPlan) / 4); q += blockDim.x) dst[q] = src[q];
     }
-    const DiagLayout lay = diag_layout(n, plan_g->nleaf, plan_g->nops);
+    const DiagLayout lay = diag_layout(n, a.plan->nleaf, a.plan->nops);
     double2 *tw = (double2 *)smem;
-    for (int q = threadIdx.x; q < lay.ntw; q += blockDim.x) tw[q] = tw_g[q];
+    for (int q = threadIdx.x; q < lay.ntw; q += blockDim.x) tw[q] = a.tw[q];
     __syncthreads();
     unsigned char *wb = smem + (size_t)lay.ntw * 16 + (size_t)wave * lay.per_wave;
     double2 *cw = (double2 *)(wb + lay.cw_off);
     float *X = (float *)(wb + lay.x_off);
+    float *Pr = (float *)(wb + lay.p_off);
     double *scr = (double *)(wb + lay.scr_off);
     const bool pow2 = (n & (n - 1)) == 0 && n >= 4;
-    const size_t P = (size_t)nsub * nchan;
+    const size_t P = (size_t)a.nsub * a.nchan;
+    const double *T64 = a.T64;
+    const int mode = a.mode;
 
     for (size_t k = (size_t)blockIdx.x * wpb + wave; k < P; k += (size_t)gridDim.x * wpb) {
-        const int c = (int)((unsigned)k % (unsigned)nchan);
-        const double x = amp[k];
-        const int stt = info[k];
-        const bool ok = stt >= 1 && stt <= 4;
-        const float w = w0[k];
+        const int c = (int)((unsigned)k % (unsigned)a.nchan);
+        const float w = a.w0[k];
         const bool valid = (w != 0.0f);
-        const int sh = shift[c];
-        const float *p = D + k * (size_t)ldD;
+        const int sh = mode == DIAG_STATS ? 0 : a.shift[c];
         wave_sync();   // previous profile's LDS reads are done
+        double x = 0.0;
+        int stt = 0;
+        const float *p;
+        if (mode == DIAG_CLOSED) {
+            // the fit-cube row f32(ded - base0), dedispersed order, then the
+            // closed-form amplitude from numpy pairwise sums
+            const float *row = a.raw + k * (size_t)n;
+            const float b = a.base[k];
+            for (int j = lane; j < n; j += 64) {
+                int i = j - sh;
+                if (i < 0) i += n;
+                Pr[i] = row[j] - b;
+            }
+            wave_sync();
+            const double dot = wave_pairwise<double>(pl, [&](int q) { return T64[q] * (double)Pr[q]; }, scr, lane);
+            const double TT = *a.TT;
+            x = TT != 0.0 ? dot / TT : 0.0;
+            stt = isfinite(x) ? 1 : 5;
+            if (lane == 0) {
+                a.amp[k] = x;
+                a.info[k] = stt;
+            }
+            p = Pr;
+        } else {
+            if (mode == DIAG_EXACT) {
+                x = a.amp[k];
+                stt = a.info[k];
+            }
+            p = a.D + k * (size_t)a.ldD;
+        }
+        const bool ok = stt >= 1 && stt <= 4;
         // residual -> X (dispersed frame): X[j] = f32(f32(r[i]) * w), j = (i + sh) mod n
         for (int i = lane; i < n; i += 64) {
             float R = 0.0f;
-            if (ok) {
+            if (mode == DIAG_STATS) {
+                R = p[i];
+            } else if (ok) {
                 const double u = x * T64[i];
                 double e = u - (double)p[i];
-                if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
+                if (a.pr_on && i >= a.pr_start && i < a.pr_end) e = e * a.pr_factor;
                 R = (float)e;
             }
             int j = i + sh;
@@ -1742,9 +1770,9 @@ __global__ __launch_bounds__(256) void k_diag(
                 }
                 const double re = er + (orr * wr - oi * wi);
                 const double im = ei + (orr * wi + oi * wr);
-                const double a = hypot(re, im);
-                if (isnan(a)) nanf = 1;
-                best = fmax(best, a);
+                const double mag = hypot(re, im);
+                if (isnan(mag)) nanf = 1;
+                best = fmax(best, mag);
             }
         } else {
             for (int kk = lane; kk <= n / 2; kk += 64) {
@@ -1758,9 +1786,9 @@ __global__ __launch_bounds__(256) void k_diag(
                     q += kk;
                     if (q >= n) q -= n;
                 }
-                const double a = hypot(sr, si);
-                if (isnan(a)) nanf = 1;
-                best = fmax(best, a);
+                const double mag = hypot(sr, si);
+                if (isnan(mag)) nanf = 1;
+                best = fmax(best, mag);
             }
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -1768,42 +1796,60 @@ __global__ __launch_bounds__(256) void k_diag(
             nanf |= __shfl_xor(nanf, off);
         }
         if (lane == 0) {
-            std_o[k] = valid ? sd : 0.0;
-            mean_o[k] = valid ? mean : 0.0;
-            ptp_o[k] = valid ? ptp : 1e20f;
-            fft_o[k] = nanf ? NAN : best;
+            a.std_o[k] = valid ? sd : 0.0;
+            a.mean_o[k] = valid ? mean : 0.0;
+            a.ptp_o[k] = valid ? ptp : 1e20f;
+            a.fft_o[k] = nanf ? NAN : best;
         }
     }
 }
 
 // ---------------------------------------------------------------------------
 // k_diag_p2<N>: the same diagnostics for power-of-two nbin = N (64..4096).
+// A profile group of TPP = 64*WPP threads cleans one profile: one wave for
+// N <= 1024, N/1024 waves for N = 2048/4096, so every thread holds the same
+// 16 samples and one pairwise chain at every N >= 1024 (at N = 4096 one wave
+// per profile needed a 32-KiB work array per wave: 1.25 waves/SIMD).
 // numpy's pairwise sum for N = 2^k is a balanced tree over leaves of
 // min(N,128) samples, each leaf 8 strided chains of min(N,128)/8 samples:
-// chain c = (leaf c/8, accumulator c%8) lives in lane c%64, slot c/64, and the
-// tree is reproduced exactly by xor-shuffles (IEEE add is commutative) and a
-// balanced in-register add of the slots.  X sits in LDS at idx + 8*(idx>>7)
-// so the chain reads are bank-conflict free.  The rFFT is an in-place
-// mixed-radix Stockham FFT of N/2 complex points (all of a stage's inputs are
-// in registers before it writes), twiddle powers by recurrence.
+// chain c = (leaf c/8, accumulator c%8) lives in thread c%TPP, slot c/TPP, and
+// the tree is reproduced exactly by xor-shuffles within a wave (IEEE add is
+// commutative), a balanced add of the group's waves and a balanced in-register
+// add of the slots.  X sits in LDS at idx + 8*(idx>>7) so the chain reads are
+// bank-conflict free.  The rFFT is an in-place mixed-radix Stockham FFT of
+// N/2 complex points (all of a stage's inputs are in registers before it
+// writes).
+// Modes (DiagArgs.mode):
+//   DIAG_EXACT   residual from the exact fit's amplitude / status (ic.py:279-288)
+//   DIAG_CLOSED  fit_mode 1: closed-form amplitude a = sum(T*p) / sum(T*T)
+//                (numpy pairwise f64 sums over the dedispersed profile, the
+//                fit cube row p = f32(ded - base0) formed from the raw cube),
+//                then the same residual; writes amp / info
+//   DIAG_STATS   comprehensive_stats alone (ic.py:181-226): X = f32(row * w)
 template <int N>
 struct P2 {
+    static constexpr int WPP = N >= 2048 ? N / 1024 : 1;   // waves per profile
+    static constexpr int TPP = 64 * WPP;                    // threads per profile
     static constexpr int M = N / 2;
     static constexpr int LEAF = N < 128 ? N : 128;
     static constexpr int NL = N / LEAF;
     static constexpr int CL = LEAF / 8;
     static constexpr int CH = 8 * NL;
-    static constexpr int CPL = CH > 64 ? CH / 64 : 1;
-    static constexpr int ACT = CH < 64 ? CH : 64;
+    static constexpr int CPL = CH > TPP ? CH / TPP : 1;     // chains per thread
+    static constexpr int ACT = CH < TPP ? CH : TPP;         // threads holding a chain
+    static constexpr int WACT = ACT < 64 ? ACT : 64;        // ... per wave
+    static constexpr int NPT = N / TPP;                     // samples per thread
     static constexpr int XPAD = N + 8 * NL;
     static constexpr int XBYTES = ((XPAD * 4 + 15) / 16) * 16;
     static constexpr int CBYTES = M * 16;   // complex points at cidx(q)
-    static constexpr int WAVE_BYTES = XBYTES > CBYTES ? XBYTES : CBYTES;
+    static constexpr int WORK_BYTES = XBYTES > CBYTES ? XBYTES : CBYTES;
+    static constexpr int RED_BYTES = WPP > 1 ? 512 : 0;     // cross-wave partials
+    static constexpr int GROUP_BYTES = WORK_BYTES + RED_BYTES;
     static constexpr int LG = __builtin_ctz(M);
     static constexpr int TW = 2 * M;   // twiddle entries: M post-processing + <= M stage tables
-    // N >= 4096: the 64-KiB table would cut a CU to two waves; read it through
-    // L1/L2 instead and keep the LDS for the per-wave work arrays (32 KiB each)
-    static constexpr bool TWG = N >= 4096;
+    // multi-wave groups: the table (up to 64 KiB) would cost blocks; it is read
+    // through L1/L2 and the LDS holds only the groups' work arrays
+    static constexpr bool TWG = WPP > 1;
     static constexpr int TW_LDS = TWG ? 0 : TW;
 };
 
@@ -1814,10 +1860,12 @@ __device__ __forceinline__ int xaddr(int idx) { return idx + 8 * (idx >> 7); }
 // the contiguous / reversed gathers (ds_read_b128, 16-lane groups over 64 banks).
 __device__ __forceinline__ int cidx(int q) { return q ^ ((q >> 3) & 7); }
 
-template <typename T, int ACT>
-__device__ __forceinline__ T tree_lanes(T v)
+// barrier of a profile group: one wave needs only ordering of its LDS ops
+template <int WPP>
+__device__ __forceinline__ void gsync()
 {
-    return wave_tree<ACT>(v, OpAdd());
+    if constexpr (WPP > 1) __syncthreads();
+    else wave_sync();
 }
 
 template <typename T, int CPL>
@@ -1829,21 +1877,54 @@ __device__ __forceinline__ T tree_slots(const T (&v)[CPL])
     else return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));   // CPL == 8
 }
 
+// Group-uniform reduction of a per-thread value: the wave tree over its WACT
+// active lanes, then (WPP > 1) a balanced tree over the group's waves through
+// `red` (WPP slots of 8 B, one slot array per call site; both barriers keep the
+// slots reusable on the next profile).
+template <int WPP, int WACT, typename T, typename Op>
+__device__ __forceinline__ T group_tree(T v, Op op, T *red, int wave, int lane)
+{
+    T w = wave_tree<WACT>(v, op);
+    if constexpr (WPP == 1) {
+        return w;
+    } else {
+        if (lane == 0) red[wave] = w;
+        __syncthreads();
+        T r;
+        if constexpr (WPP == 2) r = op(red[0], red[1]);
+        else r = op(op(red[0], red[1]), op(red[2], red[3]));   // WPP == 4
+        __syncthreads();
+        return r;
+    }
+}
+
+// chain sums (one per slot) -> the pairwise total over the group, balanced
+// over threads, then over slots
+template <int N, typename T>
+__device__ __forceinline__ T chain_total(const T (&cs)[P2<N>::CPL], T *red, int wave, int lane)
+{
+    using C = P2<N>;
+    T fs[C::CPL];
+#pragma unroll
+    for (int sl = 0; sl < C::CPL; ++sl) fs[sl] = group_tree<C::WPP, C::WACT>(cs[sl], OpAdd(), red + 8 * sl, wave, lane);
+    return tree_slots<T, C::CPL>(fs);
+}
+
 // One radix-R Stockham stage (compile-time R, NS = product of earlier radices),
 // in place: every input of the stage is in registers before it writes.
 // stw: this stage's twiddles w^(r k), w = exp(-2 pi i/(R NS)), as [k][r-1]
 // (host-built in long double; no recurrences).  FIRST: the input is the real
 // signal X (f32, padded addresses) minus mu, read as complex pairs.
-template <int R, int NS, bool FIRST, int M>
-__device__ __forceinline__ void p2_stage(double2 *C, const float *X, double mu, const double2 *stw, int lane)
+template <int R, int NS, bool FIRST, int M, int TPP>
+__device__ __forceinline__ void p2_stage(double2 *C, const float *X, double mu, const double2 *stw, int t)
 {
     constexpr int NB = M / R;
-    constexpr int BPL = (NB + 63) / 64;
+    constexpr int BPL = (NB + TPP - 1) / TPP;
     double2 v[BPL][R];
 #pragma unroll
     for (int u = 0; u < BPL; ++u) {
-        const int b = lane + 64 * u;
-        if (NB % 64 == 0 || b < NB) {
+        const int b = t + TPP * u;
+        if (NB % TPP == 0 || b < NB) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int q = b + r * NB;
@@ -1856,16 +1937,16 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, double mu, 
             }
         }
     }
-    wave_sync();
+    gsync<TPP / 64>();
 #pragma unroll
     for (int u = 0; u < BPL; ++u) {
-        const int b = lane + 64 * u;
-        if (NB % 64 == 0 || b < NB) {
+        const int b = t + TPP * u;
+        if (NB % TPP == 0 || b < NB) {
             const int k = b & (NS - 1);
             if (NS > 1) {
-                const double2 *t = stw + k * (R - 1);
+                const double2 *tk = stw + k * (R - 1);
 #pragma unroll
-                for (int r = 1; r < R; ++r) v[u][r] = cmul_f(v[u][r], t[r - 1]);
+                for (int r = 1; r < R; ++r) v[u][r] = cmul_f(v[u][r], tk[r - 1]);
             }
             dft_small<R>(v[u]);
             const int idx = (b - k) * R + k;
@@ -1873,133 +1954,203 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, double mu, 
             for (int r = 0; r < R; ++r) C[cidx(idx + r * NS)] = v[u][r];
         }
     }
-    wave_sync();
+    gsync<TPP / 64>();
 }
 
 // the whole N/2-point FFT as a compile-time chain of stages (radix 8 while >= 3
 // levels remain, then 4 or 2); OFF = offset of the next stage table in tw
-template <int M, int LG, int DONE, int NS, int OFF>
-__device__ __forceinline__ void p2_fft(double2 *C, const float *X, double mu, const double2 *tw, int lane)
+template <int M, int TPP, int LG, int DONE, int NS, int OFF>
+__device__ __forceinline__ void p2_fft(double2 *C, const float *X, double mu, const double2 *tw, int t)
 {
     if constexpr (DONE < LG) {
         constexpr int REM = LG - DONE;
         constexpr int R = REM >= 3 ? 8 : (REM == 2 ? 4 : 2);
         constexpr int LR = R == 8 ? 3 : (R == 4 ? 2 : 1);
-        p2_stage<R, NS, DONE == 0, M>(C, X, mu, tw + OFF, lane);
-        p2_fft<M, LG, DONE + LR, NS * R, (NS > 1 ? OFF + NS * (R - 1) : OFF)>(C, X, mu, tw, lane);
+        p2_stage<R, NS, DONE == 0, M, TPP>(C, X, mu, tw + OFF, t);
+        p2_fft<M, TPP, LG, DONE + LR, NS * R, (NS > 1 ? OFF + NS * (R - 1) : OFF)>(C, X, mu, tw, t);
     }
 }
 
+// occupancy floors (waves per SIMD, <= 128 VGPRs): 4 for the multi-wave groups
+// (the LDS allows 4 blocks of 4096 per CU) and for N = 1024 (the LDS allows 4
+// waves/SIMD with 8-wave blocks), where the template is then read from L1
+// instead of being held in 32 VGPRs.  Measured on C2 (k_diag ms per clean):
+// 3 waves + template in registers 8.63, 4 waves + registers 8.10 (spills),
+// 4 waves + L1 template 7.95 (profiles/r02_c2_diag_ab.txt).
+// IC_P2_MINW_1024 / IC_P2_TREG_1024: A/B build knobs for the N = 1024 kernel.
+#ifndef IC_P2_MINW_1024
+#define IC_P2_MINW_1024 4
+#endif
+#ifndef IC_P2_TREG_1024
+#define IC_P2_TREG_1024 0
+#endif
 template <int N>
-__global__ __launch_bounds__(N >= 4096 ? 256 : 512) void k_diag_p2(
-    const float *__restrict__ D, const double *__restrict__ T64g, const double *__restrict__ amp,
-    const int32_t *__restrict__ info, const float *__restrict__ w0, const int32_t *__restrict__ shift,
-    const double2 *__restrict__ tw_g, int nsub, int nchan, int ldD, int pr_on, double pr_factor,
-    int pr_start, int pr_end, double *__restrict__ std_o, double *__restrict__ mean_o,
-    float *__restrict__ ptp_o, double *__restrict__ fft_o)
+constexpr int p2_min_waves() { return N >= 2048 ? 4 : (N == 1024 ? IC_P2_MINW_1024 : 1); }
+
+template <int N, int MODE>
+__global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) void k_diag_p2(DiagArgs a)
 {
     using C = P2<N>;
+    constexpr int WPP = C::WPP, TPP = C::TPP, NPT = C::NPT;
+    // one-wave groups keep the template and the next row in registers; the
+    // multi-wave groups (N >= 2048) read both when needed and rely on occupancy
+    constexpr bool TREG = WPP == 1 && (N != 1024 || IC_P2_TREG_1024), PREFETCH = WPP == 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // [M] post-processing twiddles, then the stage tables (LDS copy unless TWG)
-    const double2 *tw = C::TWG ? tw_g : (const double2 *)smem;
-    const double *T = T64g;          // L1/L2-resident, read coalesced
-    const int wpb = blockDim.x >> 6;
-    const int wave = threadIdx.x >> 6;
+    const double2 *tw = C::TWG ? a.tw_p2 : (const double2 *)smem;
+    const double *T = a.T64;          // L1/L2-resident, read coalesced
+    constexpr int mode = MODE;
     const int lane = threadIdx.x & 63;
+    // WPP == 1: independent waves (groups) per block; WPP > 1: the block is one group
+    const int group = WPP == 1 ? (int)(threadIdx.x >> 6) : 0;
+    const int gpb = WPP == 1 ? (int)(blockDim.x >> 6) : 1;
+    const int wave = WPP == 1 ? 0 : (int)(threadIdx.x >> 6);   // wave within the group
+    int t = WPP == 1 ? lane : (int)threadIdx.x;               // thread within the group
     if (!C::TWG) {
-        for (int q = threadIdx.x; q < C::TW; q += blockDim.x) ((double2 *)smem)[q] = tw_g[q];
+        for (int q = threadIdx.x; q < C::TW; q += blockDim.x) ((double2 *)smem)[q] = a.tw_p2[q];
         __syncthreads();
     }
-    unsigned char *wb = smem + (size_t)C::TW_LDS * 16 + (size_t)wave * C::WAVE_BYTES;
-    float *X = (float *)wb;
-    double2 *Cb = (double2 *)wb;   // aliases X after the first FFT stage has read it
-    const unsigned P = (unsigned)nsub * (unsigned)nchan;
-    const unsigned stride = gridDim.x * wpb;
-    // the template stays in registers (N <= 1024), and each wave loads the
-    // next profile's row while it works on the current one: every global load
-    // of the loop is issued ahead of its use (software pipelining)
-    constexpr int NPL = N / 64;
-    constexpr bool TREG = N <= 1024;
-    constexpr bool PREFETCH = N <= 1024;
-    double tv[TREG ? NPL : 1];
+    unsigned char *gb = smem + (size_t)C::TW_LDS * 16 + (size_t)group * C::GROUP_BYTES;
+    float *X = (float *)gb;
+    double2 *Cb = (double2 *)gb;   // aliases X after the first FFT stage has read it
+    double *red = (double *)(gb + C::WORK_BYTES);   // 64 slots of 8 B (WPP > 1)
+    const unsigned P = (unsigned)a.nsub * (unsigned)a.nchan;
+    const unsigned stride = gridDim.x * gpb;
+    const int nchan = a.nchan;
+    // the template stays in registers, and each group loads the next profile's
+    // row while it works on the current one: every global load of the loop is
+    // issued ahead of its use (software pipelining)
+    double tv[TREG ? NPT : 1];
     if (TREG) {
 #pragma unroll
-        for (int u = 0; u < NPL; ++u) tv[u] = T[lane + 64 * u];
+        for (int u = 0; u < NPT; ++u) tv[u] = T[t + TPP * u];
     }
-    float pv[NPL];
-    unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + wave);
+    const double TT = mode == DIAG_CLOSED ? *a.TT : 0.0;
+    constexpr bool closed = mode == DIAG_CLOSED;
+    const float *rows = closed ? a.raw : a.D;
+    const size_t ld = closed ? (size_t)N : (size_t)a.ldD;
+    float pv[NPT];
+    unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group);
     // per-profile scalars, loaded one profile ahead as well
     double nx = 0.0;
     int nst = 0, nsh = 0;
-    float nw = 0.0f;
+    float nw = 0.0f, nb = 0.0f;
     if (k < P) {
         if (PREFETCH) {
 #pragma unroll
-            for (int u = 0; u < NPL; ++u) pv[u] = D[(size_t)k * ldD + lane + 64 * u];
+            for (int u = 0; u < NPT; ++u) pv[u] = rows[(size_t)k * ld + t + TPP * u];
         }
-        nx = amp[k];
-        nst = info[k];
-        nw = w0[k];
-        nsh = shift[k % (unsigned)nchan];
+        if (mode == DIAG_EXACT) {
+            nx = a.amp[k];
+            nst = a.info[k];
+        }
+        if (closed) nb = a.base[k];
+        nw = a.w0[k];
+        nsh = mode == DIAG_STATS ? 0 : a.shift[k % (unsigned)nchan];
     }
     for (; k < P; k += stride) {
-        const double x = nx;
-        const bool ok = nst >= 1 && nst <= 4;
+        // opaque to the optimiser: the LDS addresses of the FFT stages derive
+        // from t, and hoisting all of them out of the loop costs ~100 VGPRs
+        // (spills at N >= 2048); recomputing them is a few VALU ops each
+        asm volatile("" : "+v"(t));
+        double x = nx;
+        int st = nst;
         const float w = nw;
         const bool valid = (w != 0.0f);
         const int sh = nsh;
+        const float bk = nb;
         if (!PREFETCH) {
 #pragma unroll
-            for (int u = 0; u < NPL; ++u) pv[u] = D[(size_t)k * ldD + lane + 64 * u];
+            for (int u = 0; u < NPT; ++u) pv[u] = rows[(size_t)k * ld + t + TPP * u];
         }
-        wave_sync();
-        // residual -> X (dispersed frame, padded addresses)
-        if (pr_on) {
+        gsync<WPP>();
+        if (closed) {
+            // fit cube row p_i = f32(ded_i - base0), i = (j - sh) mod N: to LDS in
+            // the dedispersed order, then a = sum(T*p)/sum(T*T) over the chains
 #pragma unroll
-            for (int u = 0; u < NPL; ++u) {
-                const int i = lane + 64 * u;
-                const double t = TREG ? tv[u] : T[i];
-                const double uu = x * t;
+            for (int u = 0; u < NPT; ++u) {
+                const int j = t + TPP * u;
+                X[xaddr((j - sh) & (N - 1))] = pv[u] - bk;
+            }
+            gsync<WPP>();
+            double cs[C::CPL];
+            const bool act = t < C::ACT;
+#pragma unroll
+            for (int sl = 0; sl < C::CPL; ++sl) {
+                const int ch = t + TPP * sl;
+                const int base = (ch >> 3) * C::LEAF + (ch & 7);
+                double r = 0.0;
+                if (act) {
+                    r = T[base] * (double)X[xaddr(base)];
+#pragma unroll
+                    for (int q = 1; q < C::CL; ++q) {
+                        const double pr = T[base + 8 * q] * (double)X[xaddr(base + 8 * q)];
+                        r = r + pr;
+                    }
+                }
+                cs[sl] = r;
+            }
+            const double dot = 0.0 + chain_total<N, double>(cs, red, wave, lane);
+            x = TT != 0.0 ? dot / TT : 0.0;
+            st = isfinite(x) ? 1 : 5;
+#pragma unroll
+            for (int u = 0; u < NPT; ++u) pv[u] = X[xaddr(t + TPP * u)];
+            if (t == 0) {
+                a.amp[k] = x;
+                a.info[k] = st;
+            }
+            gsync<WPP>();
+        }
+        const bool ok = st >= 1 && st <= 4;
+        // residual -> X (dispersed frame, padded addresses)
+        if (mode == DIAG_STATS) {
+#pragma unroll
+            for (int u = 0; u < NPT; ++u) X[xaddr(t + TPP * u)] = pv[u] * w;
+        } else if (a.pr_on) {
+#pragma unroll
+            for (int u = 0; u < NPT; ++u) {
+                const int i = t + TPP * u;
+                const double uu = x * (TREG ? tv[u] : T[i]);
                 double e = uu - (double)pv[u];
-                if (i >= pr_start && i < pr_end) e = e * pr_factor;
+                if (i >= a.pr_start && i < a.pr_end) e = e * a.pr_factor;
                 const float R = ok ? (float)e : 0.0f;
-                const int j = (i + sh) & (N - 1);
-                X[xaddr(j)] = R * w;
+                X[xaddr((i + sh) & (N - 1))] = R * w;
             }
         } else {
 #pragma unroll
-            for (int u = 0; u < NPL; ++u) {
-                const int i = lane + 64 * u;
-                const double t = TREG ? tv[u] : T[i];
-                const double uu = x * t;
+            for (int u = 0; u < NPT; ++u) {
+                const int i = t + TPP * u;
+                const double uu = x * (TREG ? tv[u] : T[i]);
                 const double e = uu - (double)pv[u];
                 const float R = ok ? (float)e : 0.0f;
-                const int j = (i + sh) & (N - 1);
-                X[xaddr(j)] = R * w;
+                X[xaddr((i + sh) & (N - 1))] = R * w;
             }
         }
         if (k + stride < P) {
             const unsigned kn = k + stride;
             if (PREFETCH) {
-                const float *pn = D + (size_t)kn * ldD;
+                const float *pn = rows + (size_t)kn * ld;
 #pragma unroll
-                for (int u = 0; u < NPL; ++u) pv[u] = pn[lane + 64 * u];
+                for (int u = 0; u < NPT; ++u) pv[u] = pn[t + TPP * u];
             }
-            nx = amp[kn];
-            nst = info[kn];
-            nw = w0[kn];
-            nsh = shift[kn % (unsigned)nchan];
+            if (mode == DIAG_EXACT) {
+                nx = a.amp[kn];
+                nst = a.info[kn];
+            }
+            if (closed) nb = a.base[kn];
+            nw = a.w0[kn];
+            nsh = mode == DIAG_STATS ? 0 : a.shift[kn % (unsigned)nchan];
         }
-        wave_sync();
+        gsync<WPP>();
         double mean = 0.0, sd = 0.0, fftv = 0.0;
         float ptp = 1e20f;
         if (valid) {
             // chain values -> registers
             float v[C::CPL][C::CL];
-            const bool act = lane < C::ACT;
+            const bool act = t < C::ACT;
 #pragma unroll
             for (int sl = 0; sl < C::CPL; ++sl) {
-                const int ch = lane + 64 * sl;
+                const int ch = t + TPP * sl;
                 const int base = (ch >> 3) * C::LEAF + (ch & 7);
 #pragma unroll
                 for (int q = 0; q < C::CL; ++q) v[sl][q] = act ? X[xaddr(base + 8 * q)] : 0.0f;
@@ -2011,9 +2162,9 @@ __global__ __launch_bounds__(N >= 4096 ? 256 : 512) void k_diag_p2(
                 float r = v[sl][0];
 #pragma unroll
                 for (int q = 1; q < C::CL; ++q) r = r + v[sl][q];
-                fs[sl] = tree_lanes<float, C::ACT>(r);
+                fs[sl] = r;
             }
-            const float s32 = 0.0f + tree_slots<float, C::CPL>(fs);
+            const float s32 = 0.0f + chain_total<N, float>(fs, (float *)(red + 16), wave, lane);
             mean = (double)s32 / (double)N;
             // var: f64 pairwise sum of (f64(X) - mean)^2
             double ds[C::CPL];
@@ -2027,9 +2178,9 @@ __global__ __launch_bounds__(N >= 4096 ? 256 : 512) void k_diag_p2(
                     const double sq = d * d;
                     r = r + sq;
                 }
-                ds[sl] = tree_lanes<double, C::ACT>(r);
+                ds[sl] = r;
             }
-            const double ss = 0.0 + tree_slots<double, C::CPL>(ds);
+            const double ss = 0.0 + chain_total<N, double>(ds, red + 24, wave, lane);
             sd = sqrt(ss / (double)N);
             // ptp (NaN-propagating)
             float mx = -INFINITY, mn = INFINITY;
@@ -2039,28 +2190,28 @@ __global__ __launch_bounds__(N >= 4096 ? 256 : 512) void k_diag_p2(
                 for (int sl = 0; sl < C::CPL; ++sl)
 #pragma unroll
                     for (int q = 0; q < C::CL; ++q) {
-                        const float t = v[sl][q];
-                        nan |= isnan(t);
-                        mx = fmaxf(mx, t);
-                        mn = fminf(mn, t);
+                        const float tq = v[sl][q];
+                        nan |= isnan(tq);
+                        mx = fmaxf(mx, tq);
+                        mn = fminf(mn, tq);
                     }
             }
-            mx = wave_tree<64>(mx, OpMaxF());
-            mn = wave_tree<64>(mn, OpMinF());
-            nan = wave_tree<64>(nan, OpOr());
+            mx = group_tree<WPP, 64>(mx, OpMaxF(), (float *)(red + 32), wave, lane);
+            mn = group_tree<WPP, 64>(mn, OpMinF(), (float *)(red + 36), wave, lane);
+            nan = group_tree<WPP, 64>(nan, OpOr(), (int *)(red + 40), wave, lane);
             ptp = nan ? NAN : (mx - mn);
             // rFFT of f64(X) - mean: N/2-point complex Stockham, in place
-            p2_fft<C::M, C::LG, 0, 1, C::M>(Cb, X, mean, tw, lane);
+            p2_fft<C::M, TPP, C::LG, 0, 1, C::M>(Cb, X, mean, tw, t);
             // X_k = E_k + w^k O_k, computed as 2 X_k (the 1/2 factors are exact
             // powers of two, applied once to the maximum)
-            // k = 0 .. M-1 on all lanes; the Nyquist term k = M (w = -1, Z_M = Z_0)
-            // reduces to (Re 2Z_0 - Im 2Z_0)^2 and is added by lane 0 from k = 0
+            // k = 0 .. M-1 on all threads; the Nyquist term k = M (w = -1, Z_M = Z_0)
+            // reduces to (Re 2Z_0 - Im 2Z_0)^2 and is added by thread 0 from k = 0
             double best2 = 0.0;
             int nanf = 0;
 #pragma unroll 2
-            for (int j = 0; j < (C::M + 63) / 64; ++j) {
-                const int kk = lane + 64 * j;
-                if (C::M % 64 != 0 && kk >= C::M) continue;   // M = 32 (N = 64)
+            for (int j = 0; j < (C::M + TPP - 1) / TPP; ++j) {
+                const int kk = t + TPP * j;
+                if (C::M % TPP != 0 && kk >= C::M) continue;   // M = 32 (N = 64)
                 const double2 zk = Cb[cidx(kk)];
                 const double2 zm = Cb[cidx(kk == 0 ? 0 : C::M - kk)];
                 const double er = zk.x + zm.x, ei = zk.y - zm.y;
@@ -2071,34 +2222,37 @@ __global__ __launch_bounds__(N >= 4096 ? 256 : 512) void k_diag_p2(
                 const double a2 = __builtin_fma(re, re, im * im);
                 nanf |= isnan(a2);
                 best2 = fmax(best2, a2);
-                if (j == 0 && lane == 0) {
+                if (j == 0 && t == 0) {
                     const double rn = er - orr;
                     const double an = rn * rn;
                     nanf |= isnan(an);
                     best2 = fmax(best2, an);
                 }
             }
-            best2 = wave_tree<64>(best2, OpMaxF());
-            nanf = wave_tree<64>(nanf, OpOr());
+            best2 = group_tree<WPP, 64>(best2, OpMaxF(), red + 44, wave, lane);
+            nanf = group_tree<WPP, 64>(nanf, OpOr(), (int *)(red + 48), wave, lane);
             fftv = nanf ? NAN : 0.5 * sqrt(best2);
         } else {
             // invalid: rfft of f64(X) = +-0 -> 0, unless R was non-finite (X NaN)
             int nanx = 0;
-            for (int i = lane; i < N; i += 64) nanx |= isnan(X[xaddr(i)]);
-            nanx = wave_tree<64>(nanx, OpOr());
+            for (int i = t; i < N; i += TPP) nanx |= isnan(X[xaddr(i)]);
+            nanx = group_tree<WPP, 64>(nanx, OpOr(), (int *)(red + 52), wave, lane);
             fftv = nanx ? NAN : 0.0;
         }
-        if (lane == 0) {
-            std_o[k] = valid ? sd : 0.0;
-            mean_o[k] = valid ? mean : 0.0;
-            ptp_o[k] = valid ? ptp : 1e20f;
-            fft_o[k] = fftv;
+        if (t == 0) {
+            a.std_o[k] = valid ? sd : 0.0;
+            a.mean_o[k] = valid ? mean : 0.0;
+            a.ptp_o[k] = valid ? ptp : 1e20f;
+            a.fft_o[k] = fftv;
         }
     }
 }
 
-// residual cube on request (ic_get_residual): R (dispersed frame, unweighted)
-__global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, const double *__restrict__ T64,
+// residual cube on request (ic_get_residual): R (dispersed frame, unweighted).
+// D == nullptr (fit_mode 1 keeps no fit cube): the fit-cube row is formed from
+// raw and the w0 baseline as in k_chan_partials mode 3, f32(ded - base).
+__global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, const float *__restrict__ raw,
+                                                  const float *__restrict__ base, const double *__restrict__ T64,
                                                   const double *__restrict__ amp, const int32_t *__restrict__ info,
                                                   const int32_t *__restrict__ shift, size_t P, int nchan, int nbin,
                                                   int ldD, int pr_on, double pr_factor, int pr_start, int pr_end,
@@ -2110,19 +2264,31 @@ __global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, c
         const int st = info[k];
         const bool ok = st >= 1 && st <= 4;
         const double a = amp[k];
+        const float b = D ? 0.0f : base[k];
         for (int i = lane; i < nbin; i += 64) {
+            int j = i + sh;
+            if (j >= nbin) j -= nbin;
             float v = 0.0f;
             if (ok) {
+                const float p = D ? D[k * ldD + i] : raw[k * nbin + j] - b;
                 const double u = a * T64[i];
-                double e = u - (double)D[k * ldD + i];
+                double e = u - (double)p;
                 if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
                 v = (float)e;
             }
-            int j = i + sh;
-            if (j >= nbin) j -= nbin;
             R[k * nbin + j] = v;
         }
     }
+}
+
+// TT = numpy pairwise sum of T64[i]^2 (fit_mode 1's denominator), one wave
+__global__ __launch_bounds__(64) void k_tnorm(const double *__restrict__ T64, const PwPlan *__restrict__ plan,
+                                              double *__restrict__ TT)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char tsm[];
+    const int lane = threadIdx.x & 63;
+    const double v = wave_pairwise<double>(*plan, [&](int q) { return T64[q] * T64[q]; }, (double *)tsm, lane);
+    if (lane == 0) *TT = v;
 }
 
 // ============================================================ medians
@@ -2606,11 +2772,14 @@ hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, cons
     return hipGetLastError();
 }
 
+size_t window_lds_bytes(int nbin) { return (size_t)nbin * 8 + kWindowThreads * (8 + 4); }
+
 hipError_t launch_window(hipStream_t st, const double *part, long ss, long sl, const SbPlan &plan, int nsub,
                          int nbin, int width, int32_t *win, int32_t *flags)
 {
     if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
-    const size_t shm = (size_t)nbin * 8 + kWindowThreads * (8 + 4);
+    const size_t shm = window_lds_bytes(nbin);
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_window, dim3(nsub), dim3(kWindowThreads), shm, st, part, ss, sl, plan, nbin, width, win, flags);
     return hipGetLastError();
 }
@@ -2747,23 +2916,28 @@ hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, lo
     return hipGetLastError();
 }
 
-hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const double *amp,
-                       const int32_t *info, const float *w0, const int32_t *shift, const double2 *tw,
-                       const double2 *tw_p2, const PwPlan *plan, int nsub, int nchan, int nbin, int ldD, int pr_on, double pr_factor,
-                       int pr_start, int pr_end, double *std_o, double *mean_o, float *ptp_o,
-                       double *fft_o)
+hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
 {
+    const int nbin = a.nbin;
+    const size_t P = (size_t)a.nsub * a.nchan;
+    if (P == 0) return hipSuccess;
+    if (a.mode == DIAG_CLOSED ? (!a.raw || !a.base || !a.TT || !a.amp || !a.info)
+                              : (!a.D || a.ldD < nbin || (a.mode == DIAG_EXACT && (!a.amp || !a.info))))
+        return hipErrorInvalidValue;
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
-        const size_t fixed = (size_t)P2<NN>::TW_LDS * 16;                                           \
-        int wpb = NN >= 4096 ? 4 : 8;                                                              \
-        while (wpb > 1 && fixed + wpb * (size_t)P2<NN>::WAVE_BYTES > 150 * 1024) --wpb;            \
-        const size_t shm = fixed + wpb * (size_t)P2<NN>::WAVE_BYTES;                               \
-        const size_t P = (size_t)nsub * nchan;                                                     \
-        const unsigned grid = (unsigned)std::min<size_t>((P + wpb - 1) / wpb, 4096);               \
-        hipLaunchKernelGGL(k_diag_p2<NN>, dim3(grid), dim3(64 * wpb), shm, st, D, T64, amp, info, w0, \
-                           shift, tw_p2, nsub, nchan, ldD, pr_on, pr_factor, pr_start, pr_end, std_o, \
-                           mean_o, ptp_o, fft_o);                                                  \
+        using C = P2<NN>;                                                                          \
+        const size_t fixed = (size_t)C::TW_LDS * 16;                                               \
+        int gpb = C::WPP > 1 ? 1 : 8;                                                              \
+        while (gpb > 1 && fixed + gpb * (size_t)C::GROUP_BYTES > 150 * 1024) --gpb;                \
+        const size_t shm = fixed + gpb * (size_t)C::GROUP_BYTES;                                   \
+        const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);               \
+        if (a.mode == DIAG_EXACT)                                                                  \
+            hipLaunchKernelGGL((k_diag_p2<NN, DIAG_EXACT>), dim3(grid), dim3(C::TPP * gpb), shm, st, a); \
+        else if (a.mode == DIAG_CLOSED)                                                            \
+            hipLaunchKernelGGL((k_diag_p2<NN, DIAG_CLOSED>), dim3(grid), dim3(C::TPP * gpb), shm, st, a); \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_diag_p2<NN, DIAG_STATS>), dim3(grid), dim3(C::TPP * gpb), shm, st, a); \
         return hipGetLastError();                                                                  \
     }
     IC_P2(64) IC_P2(128) IC_P2(256) IC_P2(512) IC_P2(1024) IC_P2(2048) IC_P2(4096)
@@ -2776,13 +2950,28 @@ hipError_t launch_diag(hipStream_t st, const float *D, const double *T64, const 
     while (wpb > 1 && fixed + wpb * lay.per_wave > 150 * 1024) --wpb;
     const size_t shm = fixed + wpb * lay.per_wave;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>((P + wpb - 1) / wpb, 8192);
-    hipLaunchKernelGGL(k_diag, dim3(grid), dim3(64 * wpb), shm, st, D, T64, amp, info, w0, shift, tw, plan,
-                       nsub, nchan, nbin, ldD, pr_on, pr_factor, pr_start, pr_end, std_o, mean_o, ptp_o, fft_o);
+    hipLaunchKernelGGL(k_diag, dim3(grid), dim3(64 * wpb), shm, st, a);
     return hipGetLastError();
 }
 
+size_t diag_lds_bytes(int nbin)
+{
+    switch (nbin) {
+    case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096: return 0;
+    default: break;
+    }
+    const int nleaf_ub = nbin <= 128 ? 1 : (nbin / 64 + 1);
+    const DiagLayout lay = diag_layout(nbin, nleaf_ub, nleaf_ub);
+    return (size_t)lay.ntw * 16 + lay.per_wave;
+}
+
+hipError_t launch_tnorm(hipStream_t st, const double *T64, const PwPlan *plan, int nleaf_ub, double *TT)
+{
+    const size_t shm = (size_t)(nleaf_ub * 9 + nleaf_ub + 8) * 8;
+    hipLaunchKernelGGL(k_tnorm, dim3(1), dim3(64), shm, st, T64, plan, TT);
+    return hipGetLastError();
+}
 
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
 {
@@ -2821,14 +3010,15 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
     return hipGetLastError();
 }
 
-hipError_t launch_residual(hipStream_t st, const float *D, const double *T64, const double *amp,
-                           const int32_t *info, const int32_t *shift, int nsub, int nchan, int nbin, int ldD,
-                           int pr_on, double pr_factor, int pr_start, int pr_end, float *R)
+hipError_t launch_residual(hipStream_t st, const float *D, const float *raw, const float *base, const double *T64,
+                           const double *amp, const int32_t *info, const int32_t *shift, int nsub, int nchan,
+                           int nbin, int ldD, int pr_on, double pr_factor, int pr_start, int pr_end, float *R)
 {
     const size_t P = (size_t)nsub * nchan;
+    if (!D && (!raw || !base)) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
-    hipLaunchKernelGGL(k_residual, dim3(grid), dim3(256), 0, st, D, T64, amp, info, shift, P, nchan, nbin, ldD,
-                       pr_on, pr_factor, pr_start, pr_end, R);
+    hipLaunchKernelGGL(k_residual, dim3(grid), dim3(256), 0, st, D, raw, base, T64, amp, info, shift, P, nchan, nbin,
+                       ldD, pr_on, pr_factor, pr_start, pr_end, R);
     return hipGetLastError();
 }
 

@@ -46,7 +46,8 @@ int fail(int code, const char *fmt, ...)
 const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",
                                      "k_fscrunch",      "k_tscrunch",  "k_fit_pass", "k_fit_state",
                                      "k_diag",          "k_linestats", "k_combine",  "k_residual",
-                                     "k_fit_tail",      "k_sb_tree",   "k_shard_pack", "exchange"};
+                                     "k_fit_tail",      "k_sb_tree",   "k_shard_pack", "exchange",
+                                     "k_tnorm"};
 
 constexpr int kMaxRounds = 1024;      // lmdif rounds per fit (maxfev = 400 bounds it far below)
 constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
@@ -101,7 +102,7 @@ struct Session {
     uint8_t *valid = nullptr;
     int32_t *shift = nullptr, *win = nullptr, *wflag = nullptr, *info = nullptr, *counters = nullptr;
     double *part = nullptr, *part2 = nullptr, *wpart = nullptr, *T64 = nullptr, *amp = nullptr, *std_ = nullptr,
-           *mean = nullptr, *fft = nullptr, *test = nullptr, *lstat = nullptr;
+           *mean = nullptr, *fft = nullptr, *test = nullptr, *lstat = nullptr, *TT = nullptr;
     double2 *tw = nullptr, *tw_p2 = nullptr;
     PwPlan *plan = nullptr;
     FitStateArrays fs{};
@@ -112,6 +113,7 @@ struct Session {
     hipEvent_t rev[2] = {nullptr, nullptr};
     void *fs_block = nullptr;   // one allocation backing fs
     int fit_rounds = 0;
+    int plan_ub = 0;            // max(leaves, ops) of the pairwise plan (k_tnorm scratch)
     long tail_threshold = kTailProfiles;
     ic_run_stats stats{};
     // timing
@@ -240,7 +242,7 @@ void free_all(Session *s)
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
-                    s->wflag};
+                    s->wflag, s->TT};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     void *rbufs[] = {s->std_r, s->mean_r, s->fft_r, s->ptp_r, s->valid_r};
@@ -430,10 +432,10 @@ int prepare(Session *s)
 int iteration_template(Session *s, int iter)
 {
     const int nsub = s->p.nsub, nchan = s->nchan, nbin = s->p.nbin;
-    if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s; also writes D
+    if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s; also writes D (exact fit)
         LAUNCH(s, K_CHAN_PARTIALS,
-               launch_chan_partials(s->stream, 3, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
-                                    nullptr, s->part2, s->wpart, s->D, s->ldD));
+               launch_chan_partials(s->stream, s->D ? 3 : 1, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan,
+                                    nbin, nullptr, s->part2, s->wpart, s->D, s->ldD));
     } else {
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, 2, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
@@ -581,7 +583,14 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (p.nsub > 16384 || p.nchan > 16384)
         return fail(IC_EINVAL, "line length > 16384 unsupported (nsub=%d nchan=%d)", p.nsub, p.nchan);
     if (p.max_iter < 0) return fail(IC_EINVAL, "max_iter < 0");
-    if (p.fit_mode != 0) return fail(IC_EINVAL, "fit_mode %d unsupported", p.fit_mode);
+    if (p.fit_mode != IC_FIT_EXACT && p.fit_mode != IC_FIT_CLOSED)
+        return fail(IC_EINVAL, "fit_mode %d unsupported", p.fit_mode);
+    if (diag_lds_bytes(p.nbin) > 160 * 1024)
+        return fail(IC_EINVAL, "nbin=%d needs %zu bytes of LDS for the diagnostics (> 160 KiB)", p.nbin,
+                    diag_lds_bytes(p.nbin));
+    if (window_lds_bytes(p.nbin) > 160 * 1024)
+        return fail(IC_EINVAL, "nbin=%d needs %zu bytes of LDS for the baseline window (> 160 KiB)", p.nbin,
+                    window_lds_bytes(p.nbin));
     if (world < 1 || rank < 0 || rank >= world) return fail(IC_EINVAL, "bad rank %d / world %d", rank, world);
     std::vector<int32_t> cr(2 * world), rr(2 * world);
     if (const char *e = shard_layout(p.nsub, p.nchan, world, cr.data(), rr.data()))
@@ -635,11 +644,15 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         return bail(fail(IC_EHIP, "hipStreamCreate failed"));
     const size_t P = s->P, N = s->N;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
+    const bool exact = p.fit_mode == IC_FIT_EXACT;
     AL(s->slot_raw[0], N);
     s->raw = s->slot_raw[0];
-    AL(s->D, s->Ppad * (size_t)s->ldD);
-    if (hipMemset(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD) != hipSuccess)
-        return bail(fail(IC_EHIP, "hipMemset(D) failed"));
+    if (exact) {   // the closed-form fit reads the raw cube; no fit cube, no lmdif state
+        AL(s->D, s->Ppad * (size_t)s->ldD);
+        if (hipMemset(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD) != hipSuccess)
+            return bail(fail(IC_EHIP, "hipMemset(D) failed"));
+    }
+    AL(s->TT, 1);
     AL(s->slot_w0[0], P);
     s->w0 = s->slot_w0[0];
     AL(s->W, P);
@@ -671,7 +684,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw, (size_t)nbin);
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
-    AL(s->lists, 2 * P);
+    if (exact) AL(s->lists, 2 * P);
     AL(s->rcount, (size_t)2 * kMaxRounds + 2);
     if (sharded) {
         const char *cerr = nullptr;
@@ -735,7 +748,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     for (auto &e : s->rev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
             return bail(fail(IC_EHIP, "hipEventCreate failed"));
-    {
+    if (exact) {
         // fit state: 23 double arrays + 5 int arrays, each padded to 256 B
         const size_t dstride = ((P * 8 + 255) / 256) * 256, istride = ((P * 4 + 255) / 256) * 256;
         if (hipMalloc(&s->fs_block, 23 * dstride + 5 * istride) != hipSuccess)
@@ -758,6 +771,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     const std::vector<double2> tw2 = p2_twiddles(nbin);
     PwPlan plan;
     if (make_plan(nbin, &plan) != 0) return bail(fail(IC_EINVAL, "pairwise plan too large for nbin=%d", nbin));
+    s->plan_ub = std::max(plan.nleaf, plan.nops);
     if (hipMemcpy(s->tw, tw.data(), sizeof(double2) * nbin, hipMemcpyHostToDevice) != hipSuccess ||
         (!tw2.empty() &&
          hipMemcpy(s->tw_p2, tw2.data(), sizeof(double2) * tw2.size(), hipMemcpyHostToDevice) != hipSuccess) ||
@@ -850,13 +864,23 @@ int ic_upload_pols(void *session, const float *data, int npol, const float *w0, 
         if (shift[c] < 0 || shift[c] >= s->p.nbin) return fail(IC_EINVAL, "shift[%d]=%d out of [0,nbin)", c, shift[c]);
     s->ever_uploaded = true;
     const size_t row = sizeof(float) * (size_t)s->nchan * s->p.nbin;   // one subint of one polarisation
-    // pol 0 -> raw; pol 1 -> the fit-cube buffer as scratch (rebuilt, and re-zeroed, below)
+    // pol 0 -> raw; pol 1 -> the fit-cube buffer as scratch (rebuilt, and re-zeroed, below),
+    // or a temporary buffer when the session keeps no fit cube (fit_mode 1)
     CK(hipMemcpy2DAsync(s->raw, row, data, row * npol, row, s->p.nsub, hipMemcpyHostToDevice, s->stream));
     if (npol >= 2) {
-        CK(hipMemcpy2DAsync(s->D, row, (const char *)data + row, row * npol, row, s->p.nsub,
-                            hipMemcpyHostToDevice, s->stream));
-        CK(launch_pscrunch(s->stream, s->raw, s->D, s->N));
-        CK(hipMemsetAsync(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD, s->stream));
+        float *pol1 = s->D;
+        if (!pol1 && hipMalloc((void **)&pol1, sizeof(float) * s->N) != hipSuccess)
+            return fail(IC_ENOMEM, "hipMalloc(pol1 scratch, %zu floats) failed", s->N);
+        hipError_t e = hipMemcpy2DAsync(pol1, row, (const char *)data + row, row * npol, row, s->p.nsub,
+                                        hipMemcpyHostToDevice, s->stream);
+        if (e == hipSuccess) e = launch_pscrunch(s->stream, s->raw, pol1, s->N);
+        if (e == hipSuccess && s->D)
+            e = hipMemsetAsync(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD, s->stream);
+        if (!s->D) {
+            if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+            (void)hipFree(pol1);
+        }
+        if (e != hipSuccess) return fail(IC_EHIP, "ic_upload_pols: %s", hipGetErrorString(e));
     }
     CK(hipMemcpyAsync(s->w0, w0, sizeof(float) * s->P, hipMemcpyHostToDevice, s->stream));
     CK(hipMemcpyAsync(s->shift, shift, sizeof(int32_t) * s->nchan, hipMemcpyHostToDevice, s->stream));
@@ -953,6 +977,40 @@ int ic_get_kernel_times(void *session, ic_kernel_time *out, int n)
 
 namespace {
 
+// the diagnostics launch of one iteration: exact fit (amp/info from run_fit,
+// fit cube D) or closed form (k_diag computes amp/info from raw and base0)
+DiagArgs diag_args(Session *s, int pr_start, int pr_end)
+{
+    const ic_params &p = s->p;
+    DiagArgs a{};
+    a.mode = p.fit_mode == IC_FIT_EXACT ? DIAG_EXACT : DIAG_CLOSED;
+    a.D = s->D;
+    a.ldD = s->ldD;
+    a.raw = s->raw;
+    a.base = s->base0;
+    a.T64 = s->T64;
+    a.TT = s->TT;
+    a.amp = s->amp;
+    a.info = s->info;
+    a.w0 = s->w0;
+    a.shift = s->shift;
+    a.tw = s->tw;
+    a.tw_p2 = s->tw_p2;
+    a.plan = s->plan;
+    a.nsub = p.nsub;
+    a.nchan = s->nchan;
+    a.nbin = p.nbin;
+    a.pr_on = p.pr_on;
+    a.pr_factor = p.pr_factor;
+    a.pr_start = pr_start;
+    a.pr_end = pr_end;
+    a.std_o = s->std_;
+    a.mean_o = s->mean;
+    a.fft_o = s->fft;
+    a.ptp_o = s->ptp;
+    return a;
+}
+
 int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_out, int32_t *changed_out,
              int32_t *nzero_out, int32_t *n_iter_out, int32_t *converged_out)
 {
@@ -997,11 +1055,13 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         x += 1;
         ++n_iter;
         if (int rc = iteration_template(s, n_iter)) return rc;
-        if (int rc = run_fit(s)) return rc;
-        LAUNCH(s, K_DIAG,
-               launch_diag(s->stream, s->D, s->T64, s->amp, s->info, s->w0, s->shift, s->tw, s->tw_p2, s->plan, nsub,
-                           nchan, nbin, s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, s->std_, s->mean, s->ptp,
-                           s->fft));
+        DiagArgs da = diag_args(s, pr_start, pr_end);
+        if (p.fit_mode == IC_FIT_EXACT) {
+            if (int rc = run_fit(s)) return rc;
+        } else {
+            LAUNCH(s, K_TNORM, launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
+        }
+        LAUNCH(s, K_DIAG, launch_diag(s->stream, da));
         // channel medians are local to a shard; row medians need whole rows
         LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, la, s->comm ? 1 : 3));
         if (s->comm)
@@ -1075,8 +1135,8 @@ int ic_get_residual(void *session, float *out)
     // temporary output buffer
     float *R = nullptr;
     CK(hipMalloc((void **)&R, sizeof(float) * s->N));
-    hipError_t e = launch_residual(s->stream, s->D, s->T64, s->amp, s->info, s->shift, p.nsub, s->nchan, p.nbin,
-                                   s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, R);
+    hipError_t e = launch_residual(s->stream, s->D, s->raw, s->base0, s->T64, s->amp, s->info, s->shift, p.nsub,
+                                   s->nchan, p.nbin, s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, R);
     if (e == hipSuccess) e = hipMemcpyAsync(out, R, sizeof(float) * s->N, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(R);
@@ -1132,6 +1192,103 @@ int ic_get_diagnostics(void *session, double *std_o, double *mean_o, float *ptp_
     if (ptp_o) CK(hipMemcpyAsync(ptp_o, s->ptp, sizeof(float) * s->P, hipMemcpyDeviceToHost, s->stream));
     if (fftmax_o) CK(hipMemcpyAsync(fftmax_o, s->fft, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
     CK(hipStreamSynchronize(s->stream));
+    return IC_OK;
+}
+
+// comprehensive_stats alone (iterative_cleaner.py:181-226 on the data of
+// :111-117): one-shot device buffers, the diagnostics kernel in DIAG_STATS mode,
+// the line medians and the combine of one "iteration" (weights/history unused).
+int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const float *data, const float *weights,
+                           double chanthresh, double subintthresh, double *test_out, double *std_o, double *mean_o,
+                           float *ptp_o, double *fftmax_o)
+{
+    if (!data || !weights || !test_out) return fail(IC_EINVAL, "null argument");
+    if (nsub <= 0 || nchan <= 0 || nbin <= 0 || nsub > 16384 || nchan > 16384 || nbin > 32768)
+        return fail(IC_EINVAL, "bad shape nsub=%d nchan=%d nbin=%d", nsub, nchan, nbin);
+    if (diag_lds_bytes(nbin) > 160 * 1024) return fail(IC_EINVAL, "nbin=%d unsupported", nbin);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(IC_EHIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
+    CK(hipSetDevice(device));
+    const size_t P = (size_t)nsub * nchan, N = P * (size_t)nbin;
+    PwPlan plan;
+    if (make_plan(nbin, &plan) != 0) return fail(IC_EINVAL, "pairwise plan too large for nbin=%d", nbin);
+    std::vector<double2> tw(nbin);
+    for (int q = 0; q < nbin; ++q) {
+        const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)q / (long double)nbin;
+        tw[q] = make_double2((double)cosl(ang), (double)sinl(ang));
+    }
+    const std::vector<double2> tw2 = p2_twiddles(nbin);
+    struct Buf {
+        void *p = nullptr;
+        ~Buf() { if (p) (void)hipFree(p); }
+    } bD, bw, bvalid, bW, bhist, bstd, bmean, bfft, bptp, btest, blstat, bcnt, btw, btw2, bplan;
+    hipStream_t st = nullptr;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    struct StreamGuard {
+        hipStream_t s;
+        ~StreamGuard() { (void)hipStreamDestroy(s); }
+    } sg{st};
+    struct {
+        Buf *b;
+        size_t bytes;
+    } al[] = {{&bD, 4 * N},       {&bw, 4 * P},      {&bvalid, P},      {&bW, 4 * P},
+              {&bhist, 8 * P},    {&bstd, 8 * P},    {&bmean, 8 * P},   {&bfft, 8 * P},
+              {&bptp, 4 * P},     {&btest, 8 * P},   {&blstat, 8 * 16 * ((size_t)nsub + nchan)},
+              {&bcnt, 4 * 8},     {&btw, 16 * (size_t)nbin}, {&btw2, 16 * (size_t)nbin + 16}, {&bplan, sizeof plan}};
+    for (auto &x : al)
+        if (hipMalloc(&x.b->p, x.bytes + 16) != hipSuccess) return fail(IC_ENOMEM, "hipMalloc(%zu) failed", x.bytes);
+    float *D = (float *)bD.p, *w0 = (float *)bw.p, *W = (float *)bW.p, *hist = (float *)bhist.p;
+    uint8_t *valid = (uint8_t *)bvalid.p;
+    double *sd = (double *)bstd.p, *mn = (double *)bmean.p, *ff = (double *)bfft.p, *test = (double *)btest.p;
+    float *pt = (float *)bptp.p;
+    double *lstat = (double *)blstat.p;
+    int32_t *cnt = (int32_t *)bcnt.p;
+    CK(hipMemcpyAsync(D, data, 4 * N, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(w0, weights, 4 * P, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(btw.p, tw.data(), 16 * (size_t)nbin, hipMemcpyHostToDevice, st));
+    if (!tw2.empty()) CK(hipMemcpyAsync(btw2.p, tw2.data(), 16 * tw2.size(), hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(bplan.p, &plan, sizeof plan, hipMemcpyHostToDevice, st));
+    CK(hipMemsetAsync(cnt, 0, 4 * 8, st));
+    hipLaunchKernelGGL(k_valid, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, w0, valid, W, hist, P);
+    CK(hipGetLastError());
+    DiagArgs a{};
+    a.mode = DIAG_STATS;
+    a.D = D;
+    a.ldD = nbin;
+    a.w0 = w0;
+    a.tw = (const double2 *)btw.p;
+    a.tw_p2 = (const double2 *)btw2.p;
+    a.plan = (const PwPlan *)bplan.p;
+    a.nsub = nsub;
+    a.nchan = nchan;
+    a.nbin = nbin;
+    a.std_o = sd;
+    a.mean_o = mn;
+    a.fft_o = ff;
+    a.ptp_o = pt;
+    CK(launch_diag(st, a));
+    LineStatsArgs la;
+    la.nsub = nsub;
+    la.nchan = nchan;
+    la.valid = valid;
+    la.std_d = sd;
+    la.mean_d = mn;
+    la.fft_d = ff;
+    la.ptp_d = pt;
+    la.col_med = lstat;
+    la.col_mad = lstat + 4 * nchan;
+    la.row_med = lstat + 8 * nchan;
+    la.row_mad = lstat + 8 * nchan + 4 * nsub;
+    CK(launch_linestats(st, la, 3));
+    CK(launch_combine(st, nsub, nchan, valid, w0, sd, mn, pt, ff, la.col_med, la.col_mad, la.row_med, la.row_mad,
+                      chanthresh, subintthresh, test, W, hist, 1, cnt));
+    CK(hipMemcpyAsync(test_out, test, 8 * P, hipMemcpyDeviceToHost, st));
+    if (std_o) CK(hipMemcpyAsync(std_o, sd, 8 * P, hipMemcpyDeviceToHost, st));
+    if (mean_o) CK(hipMemcpyAsync(mean_o, mn, 8 * P, hipMemcpyDeviceToHost, st));
+    if (ptp_o) CK(hipMemcpyAsync(ptp_o, pt, 4 * P, hipMemcpyDeviceToHost, st));
+    if (fftmax_o) CK(hipMemcpyAsync(fftmax_o, ff, 8 * P, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
     return IC_OK;
 }
 

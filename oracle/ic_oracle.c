@@ -506,6 +506,41 @@ static double pw_f64(const double *a, int n)
 float orc_sum_f32(const float *a, int n) { return 0.0f + pw_f32(a, n, 1); }
 double orc_sum_f64(const double *a, int n) { return 0.0 + pw_f64(a, n); }
 
+/* ------------------------------------------------- closed-form fit (fast mode) */
+/* fit_mode 1 (IC_FIT_CLOSED, include/iterative_cleaner.h): NOT the reference's
+ * arithmetic (which is leastsq, iterative_cleaner.py:277-278) but its closed-form
+ * least-squares solution, stated in numpy terms as
+ *     TT = np.sum(T64 * T64);  a = np.sum(T64 * p64) / TT   (pairwise f64 sums)
+ * with a = 0 when TT == 0 and status 1 (5 when a is not finite: residual zeroed,
+ * like a failed leastsq, :284-286).  The residual follows :279-283 as in the
+ * exact mode.  D: fit cube (P, m), dedispersed. */
+void orc_fit_closed(int P, int m, const float *T, const float *D,
+                    int pr_on, double pr_factor, int pr_start, int pr_end,
+                    double *amp, int32_t *info, float *R)
+{
+    double *prod = (double *)malloc(sizeof(double) * (size_t)m);
+    for (int i = 0; i < m; ++i) prod[i] = (double)T[i] * (double)T[i];
+    const double TT = orc_sum_f64(prod, m);
+    for (int k = 0; k < P; ++k) {
+        const float *p = D + (size_t)k * m;
+        for (int i = 0; i < m; ++i) prod[i] = (double)T[i] * (double)p[i];
+        const double dot = orc_sum_f64(prod, m);
+        const double x = TT != 0.0 ? dot / TT : 0.0;
+        const int st = isfinite(x) ? 1 : 5;
+        amp[k] = x;
+        info[k] = st;
+        float *o = R + (size_t)k * m;
+        for (int i = 0; i < m; ++i) {
+            if (st != 1) { o[i] = 0.0f; continue; }
+            double t = x * (double)T[i];
+            double e = t - (double)p[i];
+            if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
+            o[i] = (float)e;
+        }
+    }
+    free(prod);
+}
+
 /* ------------------------------------------------------------ fft max */
 /* max_k |DFT(x)_k| for k = 0..n/2 (np.fft.rfft magnitude; tolerance-level
  * agreement with pocketfft).  Radix-2 iterative for powers of two, direct
@@ -817,6 +852,7 @@ typedef struct {
     double pr_factor;
     int32_t pr_start, pr_end;
     double baseline_duty;
+    int32_t fit_mode;   /* 0: exact leastsq (orc_fit_residual), 1: closed form (orc_fit_closed) */
 } orc_params;
 
 /* One full clean loop (iterative_cleaner.py:83-146).
@@ -855,7 +891,10 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
         x += 1;
         orc_template(nsub, nchan, n, raw, Wcur, shift, pp->baseline_duty, T);
         if (T_all) memcpy(T_all + (size_t)(x - 1) * n, T, sizeof(float) * (size_t)n);
-        orc_fit_residual((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
+        if (pp->fit_mode == 1)
+            orc_fit_closed((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
+        else
+            orc_fit_residual((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
         /* dededisperse + apply_weights */
         for (int s = 0; s < nsub; ++s)
             for (int c = 0; c < nchan; ++c) {

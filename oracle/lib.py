@@ -24,7 +24,7 @@ class OrcParams(C.Structure):
                 ("max_iter", C.c_int32), ("chanthresh", C.c_double),
                 ("subintthresh", C.c_double), ("pr_on", C.c_int32),
                 ("pr_factor", C.c_double), ("pr_start", C.c_int32), ("pr_end", C.c_int32),
-                ("baseline_duty", C.c_double)]
+                ("baseline_duty", C.c_double), ("fit_mode", C.c_int32)]
 
 
 def _p(a):
@@ -42,6 +42,7 @@ def lib():
         _lib.orc_fit_residual.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                           C.c_double, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                           C.c_void_p]
+        _lib.orc_fit_closed.argtypes = _lib.orc_fit_residual.argtypes
         _lib.orc_baseline.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_double, C.c_void_p, C.c_void_p]
         _lib.orc_fit_cube.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_double, C.c_void_p]
         _lib.orc_template.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_double, C.c_void_p]
@@ -78,6 +79,19 @@ def fit_residual(D, T, pr=None):
     R = np.empty((P, n), np.float32)
     on, fac, a, b = (0, 1.0, 0, 0) if pr is None else (1, float(pr[0]), int(pr[1]), int(pr[2]))
     lib().orc_fit_residual(P, n, _p(T), _p(D), on, fac, a, b, _p(amp), _p(info), _p(R))
+    return amp, info, R
+
+
+def fit_closed(D, T, pr=None):
+    """fit_mode 1 (closed form): (amp, info, R f32 dedispersed) of the (P, nbin) fit cube."""
+    D = f32(D).reshape(-1, np.shape(D)[-1])
+    T = f32(T)
+    P, n = D.shape
+    amp = np.empty(P, np.float64)
+    info = np.empty(P, np.int32)
+    R = np.empty((P, n), np.float32)
+    on, fac, a, b = (0, 1.0, 0, 0) if pr is None else (1, float(pr[0]), int(pr[1]), int(pr[2]))
+    lib().orc_fit_closed(P, n, _p(T), _p(D), on, fac, a, b, _p(amp), _p(info), _p(R))
     return amp, info, R
 
 
@@ -128,7 +142,7 @@ def test_values(valid, std, mean, ptp, fft, ct, st):
 
 
 def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pulse_region=None,
-               duty=0.15, want_residual=False, want_details=False):
+               duty=0.15, want_residual=False, want_details=False, fit_mode=0):
     """Whole loop; returns dict(test, weights, loops, changed, nzero, [...])."""
     raw = f32(raw)
     nsub, nchan, n = raw.shape
@@ -136,7 +150,8 @@ def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pul
     pr_on, fac, a, b = 0, 1.0, 0, 0
     if pulse_region is not None:
         pr_on, fac, a, b = 1, float(pulse_region[0]), int(pulse_region[1]), int(pulse_region[2])
-    prm = OrcParams(nsub, nchan, n, max_iter, float(chanthresh), float(subintthresh), pr_on, fac, a, b, duty)
+    prm = OrcParams(nsub, nchan, n, max_iter, float(chanthresh), float(subintthresh), pr_on, fac, a, b, duty,
+                    int(fit_mode))
     test = np.empty((nsub, nchan), np.float64)
     weights = np.empty((nsub, nchan), np.float32)
     loops = np.zeros(1, np.int32)

@@ -180,3 +180,22 @@ def comprehensive_stats(X: np.ndarray, w0: np.ndarray, chanthresh, subintthresh,
 def weighted_cube(R: np.ndarray, w0: np.ndarray) -> np.ndarray:
     """apply_weights (iterative_cleaner.py:291-297): f32(R * w0)."""
     return (np.asarray(R, np.float32) * np.asarray(w0, np.float32)[..., None]).astype(np.float32)
+
+
+# --------------------------------------------------------------------------
+# fit_mode 1 (IC_FIT_CLOSED): the closed-form amplitude, stated in numpy
+# --------------------------------------------------------------------------
+def closed_form_fit(D: np.ndarray, T: np.ndarray):
+    """a = np.sum(T*p) / np.sum(T*T) per fit-cube row (numpy pairwise f64 sums
+    along the contiguous bin axis); a = 0 for an all-zero template; status 1, or
+    5 (residual zeroed) when a is not finite.  Returns (amp, info, R f32)."""
+    T64 = np.asarray(T, np.float32).astype(np.float64)
+    D64 = np.asarray(D, np.float32).astype(np.float64).reshape(-1, T64.size)
+    TT = np.sum(T64 * T64)
+    with np.errstate(all="ignore"):
+        dot = np.sum(D64 * T64[None, :], axis=-1)
+        amp = dot / TT if TT != 0.0 else np.zeros_like(dot)
+        info = np.where(np.isfinite(amp), 1, 5).astype(np.int32)
+        R = np.where(info[:, None] == 1, amp[:, None] * T64[None, :] - D64, 0.0).astype(np.float32)
+    return amp, info, R
+

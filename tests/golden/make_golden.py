@@ -143,7 +143,7 @@ class Recorder:
 
 
 def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
-                   keep_cubes=True, npol=1, workdir=None, out_dir=HERE):
+                   keep_cubes=True, npol=1, workdir=None, out_dir=HERE, residual_full=True):
     data, weights, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi, npol=npol)
     path = os.path.join(workdir, "%s.ar" % name)
     ar = ica.Archive(data, weights, shift, filename=path)
@@ -195,6 +195,17 @@ def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
         else:
             arrays["residual_ded_sha_%d" % k] = np.array(sha(it["residual_ded"]))
             arrays["X_sha_%d" % k] = np.array(sha(it["X"]))
+    if "-u" in extra_args:
+        # the residual archive the reference unloads (iterative_cleaner.py:106-108, :161-162)
+        res = ica.Archive_load("%s_residual_%s.ar" % (path, loops))
+        rdata = res.get_data()
+        arrays["residual_sha256"] = np.array(sha(rdata))
+        arrays["residual_weights"] = res.get_weights()
+        arrays["residual_shape"] = np.array(rdata.shape)
+        if residual_full:
+            arrays["residual_data"] = rdata
+        else:
+            arrays["residual_subint0"] = rdata[0]
     fn = os.path.join(out_dir, "clean_%s.npz" % name)
     np.savez_compressed(fn, **arrays)
     print("wrote %s  iters=%d loops=%s" % (fn, len(rec.iters), loops))
@@ -254,6 +265,87 @@ def run_stats_cases(ic, out_dir=HERE):
     fn = os.path.join(out_dir, "stats_cases.npz")
     np.savez_compressed(fn, **arrays)
     print("wrote", fn)
+
+
+LONG_NBINS = (512, 1024, 2048, 4096)
+
+
+def long_stats_cases():
+    """comprehensive_stats inputs at the bench profile lengths (nbin 512..4096):
+    regenerated from this seeded generator by the tests (the fixture keeps the
+    input hashes and the reference's outputs, not the 0.1-1 MB inputs)."""
+    cases = []
+    for ni, nbin in enumerate(LONG_NBINS):
+        for kind in range(5):
+            rng = np.random.default_rng(9000 + 10 * ni + kind)
+            nsub = int(rng.integers(3, 8))
+            nchan = int(rng.integers(4, 12))
+            X = rng.standard_normal((nsub, nchan, nbin)).astype(np.float32)
+            X *= np.float32(10.0 ** rng.uniform(-2, 2))
+            w = np.ones((nsub, nchan), np.float32)
+            if kind == 1:      # zero-weight channel + subint, fractional weights
+                w[:, rng.integers(0, nchan)] = 0
+                w[rng.integers(0, nsub), :] = 0
+                w[rng.integers(0, nsub), rng.integers(0, nchan)] = 0.5
+            if kind == 2:      # narrowband sinusoid (FFT maximum off DC), dead channel
+                ph = (np.arange(nbin) + 0.5) / nbin
+                X[:, 1, :] += (30 * np.sin(2 * np.pi * 17.0 * ph)).astype(np.float32)
+                X[:, 2, :] = 0
+            if kind == 3:      # impulsive spikes (ptp / mean outliers)
+                X[rng.integers(0, nsub), :, rng.integers(0, nbin, 9)] += 200
+            if kind == 4:      # quantised (ties in medians, exact sums)
+                X = (np.round(X * 4) / 4).astype(np.float32)
+            thr = [(5, 5), (3.0, 3.0), (1.5, 4.0), (5, 2.5), (5, 5)][kind]
+            cases.append((X, w, thr))
+    return cases
+
+
+def run_long_stats_cases(ic, out_dir=HERE):
+    arrays = {}
+    cases = long_stats_cases()
+    for i, (X, w, (ct, st)) in enumerate(cases):
+        args = argparse.Namespace(chanthresh=ct, subintthresh=st)
+        data = ic.apply_weights(X.copy(), w)
+        mask = np.bitwise_not(np.expand_dims(w, 2).astype(bool)).repeat(X.shape[2], axis=2)
+        mdata = np.ma.masked_array(data, mask=mask)
+        with np.errstate(all="ignore"):
+            test = ic.comprehensive_stats(mdata, args, axis=2)
+            diags = [np.ma.std(mdata, axis=2), np.ma.mean(mdata, axis=2), np.ma.ptp(mdata, axis=2),
+                     np.max(np.abs(np.fft.rfft(
+                         mdata - np.expand_dims(mdata.mean(axis=2), axis=2), axis=2)), axis=2)]
+        arrays["X_sha256_%d" % i] = np.array(sha(X))
+        arrays["w_%d" % i] = w
+        arrays["thr_%d" % i] = np.array([ct, st], dtype=np.float64)
+        arrays["thr_is_int_%d" % i] = np.array([isinstance(ct, int), isinstance(st, int)])
+        arrays["test_%d" % i] = np.asarray(test)
+        for nm, d in zip(("std", "mean", "ptp", "fft"), diags):
+            arrays["diag_%s_%d" % (nm, i)] = np.ma.getdata(d).copy()
+    arrays["n"] = np.array(len(cases))
+    fn = os.path.join(out_dir, "stats_cases_long.npz")
+    np.savez_compressed(fn, **arrays)
+    print("wrote", fn)
+
+
+def run_zap_plot_case(ic, out_dir=HERE):
+    """clean() with -z: the reference's zap PNG (iterative_cleaner.py:164-171)."""
+    import matplotlib.pyplot as plt
+    with tempfile.TemporaryDirectory() as wd:
+        data, weights, shift = synth.make_cube(8, 24, 64, 61, 0.2)
+        path = "zap.ar"                      # relative: the plot title carries the name
+        args = ref_args(ic, ["-l", "-q", "-z"])
+        cwd = os.getcwd()
+        os.chdir(wd)
+        plt.close("all")
+        try:
+            ica.Archive(data, weights, shift, filename=path).unload(path)
+            ic.clean(ica.Archive_load(path), args, path)
+            img = plt.imread("%s_%s_%s.png" % (path, args.chanthresh, args.subintthresh))
+        finally:
+            os.chdir(cwd)
+        plt.close("all")
+        np.savez_compressed(os.path.join(out_dir, "zap_plot_case.npz"), image=img,
+                            input_sha256=np.array(sha(data)))
+        print("wrote zap_plot_case.npz", img.shape)
 
 
 def leastsq_cases(rng):
@@ -362,8 +454,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--skip-big", action="store_true")
+    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap (round-2 fixtures only)")
     a = ap.parse_args()
     ic = import_reference()
+    only = set(filter(None, a.only.split(",")))
+    if only:
+        if "long" in only:
+            run_long_cases(ic, a.out)
+        if "stats_long" in only:
+            run_long_stats_cases(ic, a.out)
+        if "zap" in only:
+            run_zap_plot_case(ic, a.out)
+        return
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s12x48x128", 12, 48, 128, 3, 0.05, workdir=wd, out_dir=a.out)
         run_clean_case(ic, "s16x64x256_rfi30", 16, 64, 256, 4, 0.30, workdir=wd, out_dir=a.out)
@@ -382,6 +484,26 @@ def main():
     run_leastsq_cases(ic, a.out)
     run_pulse_region_case(ic, a.out)
     run_cli_case(ic, a.out)
+    run_long_cases(ic, a.out)
+    run_long_stats_cases(ic, a.out)
+    run_zap_plot_case(ic, a.out)
+
+
+def run_long_cases(ic, out_dir=HERE):
+    """clean() at the bench profile lengths (C4's 512, C2/C3's 1024, C5's 4096)."""
+    with tempfile.TemporaryDirectory() as wd:
+        run_clean_case(ic, "s6x48x512_u", 6, 48, 512, 44, 0.05, extra_args=("-u",),
+                       keep_cubes=False, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s6x48x1024", 6, 48, 1024, 43, 0.05, keep_cubes=False,
+                       workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s16x128x1024", 16, 128, 1024, 41, 0.05, keep_cubes=False,
+                       workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s4x32x2048_rfi30", 4, 32, 2048, 45, 0.30, keep_cubes=False,
+                       workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s4x32x4096_rfi30", 4, 32, 4096, 47, 0.30, keep_cubes=False,
+                       workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s4x32x4096_rfi30_m3u", 4, 32, 4096, 40, 0.30, extra_args=("-u", "-m", "3"),
+                       keep_cubes=False, workdir=wd, out_dir=out_dir, residual_full=False)
 
 
 if __name__ == "__main__":

@@ -35,3 +35,25 @@ def bits_equal(a, b):
 
 def nan_equal(a, b):
     return bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+
+
+def long_stats_cases():
+    """The seeded comprehensive_stats inputs of tests/golden/stats_cases_long.npz
+    (generator in make_golden.py; the fixture pins their hashes)."""
+    import importlib
+    import sys
+    if GOLDEN not in sys.path:
+        sys.path.insert(0, GOLDEN)
+    mg = importlib.import_module("make_golden")
+    z = np.load(os.path.join(GOLDEN, "stats_cases_long.npz"))
+    cases = mg.long_stats_cases()
+    for i, (X, w, _) in enumerate(cases):
+        assert hashlib.sha256(np.ascontiguousarray(X).tobytes()).hexdigest() == str(z["X_sha256_%d" % i]), \
+            "long stats generator drifted from the golden fixture (case %d)" % i
+    return z, cases
+
+
+def thresholds(z, i):
+    """(chanthresh, subintthresh) of a stats fixture case, int where the reference had an int."""
+    thr, isint = z["thr_%d" % i], z["thr_is_int_%d" % i]
+    return (int(thr[0]) if isint[0] else float(thr[0]), int(thr[1]) if isint[1] else float(thr[1]))

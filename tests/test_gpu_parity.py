@@ -95,6 +95,18 @@ def test_clean_stdout_matches_reference(path, tmp_path, monkeypatch, capsys):
     printed = capsys.readouterr().out
     assert printed == str(z["stdout"])
     assert bits_equal(out_ar.get_weights(), z["final_weights"])
+    if "-u" in meta["extra_args"]:
+        # the residual archive (iterative_cleaner.py:106-108, :161-162) equals the reference's
+        import hashlib
+        res = ica.Archive_load("%s_residual_%s.ar" % (arpath, int(z["loops"])))
+        rdata = res.get_data()
+        assert rdata.shape == tuple(z["residual_shape"])
+        assert bits_equal(res.get_weights(), z["residual_weights"])
+        if "residual_data" in z.files:
+            assert bits_equal(rdata, z["residual_data"])
+        else:
+            assert bits_equal(rdata[0], z["residual_subint0"])
+        assert hashlib.sha256(rdata.tobytes()).hexdigest() == str(z["residual_sha256"])
 
 
 CASES = [

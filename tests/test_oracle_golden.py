@@ -6,7 +6,8 @@ import os
 import numpy as np
 import pytest
 
-from helpers import GOLDEN, bits_equal, clean_fixtures, load_clean_case, nan_equal
+from helpers import (GOLDEN, bits_equal, clean_fixtures, load_clean_case, long_stats_cases, nan_equal,
+                     thresholds)
 
 
 def test_leastsq_cases_bit_exact(oracle_lib):
@@ -69,6 +70,50 @@ def test_stats_cases_c_oracle(oracle_lib):
         assert np.array_equal(np.isnan(t), np.isnan(ref))
         assert np.all(np.abs(t[fin] - ref[fin]) <= 1e-9 * np.maximum(1, np.abs(ref[fin])))
         assert np.array_equal((t >= 1), (ref >= 1))
+
+
+def test_long_stats_cases_restated_and_c_oracle(oracle_lib):
+    """nbin 512..4096 (the bench profile lengths): the numpy restatement and the
+    C oracle reproduce the reference's comprehensive_stats — std/mean/ptp and
+    the test values' zap decisions bit for bit, fftmax within 1e-9 relative."""
+    from oracle import restated as R
+    z, cases = long_stats_cases()
+    for i, (X, w, _) in enumerate(cases):
+        ct, st = thresholds(z, i)
+        Xw = R.weighted_cube(X, w)
+        valid = w != 0
+        t = R.comprehensive_stats(Xw, w, ct, st)
+        ref = z["test_%d" % i]
+        assert bits_equal(np.where(np.isnan(t), 0, t), np.where(np.isnan(ref), 0, ref)), i
+        sd, mn, pt, ff = oracle_lib.diagnostics(Xw, valid)
+        for got, nm in ((sd, "std"), (mn, "mean"), (pt, "ptp")):
+            want = z["diag_%s_%d" % (nm, i)]
+            assert bits_equal(np.where(valid, got, 0), np.where(valid, want, 0).astype(got.dtype)), (i, nm)
+        assert np.allclose(ff, z["diag_fft_%d" % i], rtol=1e-9, atol=0), i
+        tc = oracle_lib.test_values(valid, sd, mn, pt, ff, ct, st)
+        fin = np.isfinite(ref)
+        assert np.array_equal(np.isnan(tc), np.isnan(ref))
+        assert np.all(np.abs(tc[fin] - ref[fin]) <= 1e-9 * np.maximum(1, np.abs(ref[fin])))
+        assert np.array_equal(tc >= 1, ref >= 1), i
+
+
+def test_zap_plot_matches_reference(oracle_lib, tmp_path, monkeypatch):
+    """-z (iterative_cleaner.py:164-171): the host plot of the oracle's test
+    values is pixel-identical to the PNG the reference wrote."""
+    import argparse
+
+    import matplotlib.pyplot as plt
+
+    from iterative_cleaner_amd import cleaner, synth
+    z = np.load(os.path.join(GOLDEN, "zap_plot_case.npz"))
+    data, w0, shift = synth.make_cube(8, 24, 64, 61, 0.2)
+    out = oracle_lib.clean_loop(data[:, 0], w0, shift)
+    monkeypatch.chdir(tmp_path)
+    plt.close("all")
+    cleaner._plot_zap(out["test"], "zap.ar", argparse.Namespace(chanthresh=5, subintthresh=5))
+    img = plt.imread("zap.ar_5_5.png")
+    plt.close("all")
+    assert img.shape == z["image"].shape and np.array_equal(img, z["image"])
 
 
 @pytest.mark.parametrize("path", clean_fixtures(), ids=lambda p: os.path.basename(p)[6:-4])
@@ -148,3 +193,26 @@ def test_reference_like_cpu_baseline(name):
     assert loops == int(z["loops"])
     assert bits_equal(weights, z["weights_%d" % nit])
     assert nan_equal(test, z["test_%d" % nit])
+
+
+@pytest.mark.parametrize("nbin", [64, 100, 1024, 4096])
+def test_closed_form_c_oracle_matches_numpy_statement(nbin, oracle_lib):
+    """fit_mode 1's definition (oracle/restated.py closed_form_fit: numpy
+    pairwise sums) and the C oracle agree bit for bit, including an all-zero
+    template (a = 0), a zero profile and a NaN profile (status 5)."""
+    from oracle import restated as R
+
+    from iterative_cleaner_amd import synth
+    data, w0, shift = synth.make_cube(4, 24, nbin, 5, 0.2)
+    D = oracle_lib.fit_cube(data[:, 0], w0, shift).reshape(-1, nbin)
+    D[3] = 0.0
+    D[5, 7] = np.nan
+    T = oracle_lib.template(data[:, 0], w0, shift)
+    for k, TT in enumerate((T, np.zeros_like(T))):
+        a1, i1, R1 = oracle_lib.fit_closed(D, TT)
+        a2, i2, R2 = R.closed_form_fit(D, TT)
+        assert bits_equal(a1, a2) and bits_equal(i1, i2) and bits_equal(R1, R2)
+        if k == 0:
+            assert i1[5] == 5 and not R1[5].any()
+        else:
+            assert not a1.any() and np.array_equal(R1, -D, equal_nan=True)
