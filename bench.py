@@ -253,6 +253,31 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def fast_mode_summary(_native, cube, w0, shift, shape, device, steps, torch):
+    """fit_mode 1 (closed-form amplitude fused with the diagnostics) on the same
+    archive: profiles/s, the loop's SURVEY §8(d) HBM fraction, and (filled in by
+    the caller) the zap-mask flips against the exact mode.  Not the reference's
+    arithmetic; the headline value stays the exact mode's."""
+    nsub, nchan, nbin = shape
+    with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=device, fit_mode=_native.FIT_CLOSED) as s:
+        s.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
+        s.run(fetch=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = s.run(fetch=False)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        weights = s.run()["weights"]
+    P = nsub * nchan
+    loop_gbs = (8 * P * nbin + 64 * P) * out["n_iter"] / dt / 1e9
+    return {"fit_mode": "closed", "value": round(P / dt, 1), "unit": "profiles/s", "ms_per_step": round(1e3 * dt, 3),
+            "loops": out["loops"], "loop_hbm_gbs": round(loop_gbs, 1),
+            "loop_hbm_frac": round(loop_gbs / HBM_PEAK_GBS, 4), "weights": weights,
+            "note": "closed-form amplitude sum(T*p)/sum(T*T) (IC_FIT_CLOSED): the north star's HBM-bound fast "
+                    "mode, not the reference's leastsq arithmetic"}
+
+
 def batch_main(a, workload, rank, world, local, dev):
     """C4: every rank cleans `--batch` archives per step from page-locked host
     memory through the batch pipeline (iterative_cleaner_amd/batch.py); three
@@ -343,6 +368,11 @@ def main():
                     help="exact: scipy leastsq emulated bit for bit (the reference's arithmetic, default); "
                          "closed: the closed-form amplitude fused with the diagnostics (fit_mode 1, fast mode; "
                          "also reports the zap-mask flips against the exact mode on the same archive)")
+    ap.add_argument("--no-fast-summary", action="store_true",
+                    help="exact mode at N=1: skip the closed-form (fit_mode 1) summary added to the line")
+    ap.add_argument("--no-flip-check", action="store_true",
+                    help="closed mode: skip the (untimed) exact run that counts zap-mask flips "
+                         "(profiling passes, whose kernel tallies it would mix in)")
     a = ap.parse_args()
 
     import torch
@@ -395,15 +425,19 @@ def main():
             P_total = P_total * world          # replicas: every rank cleans its own archive
     torch.cuda.synchronize()
     sess.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
+    fast = None
+    if fit_mode == _native.FIT_EXACT and not sharded and world == 1 and not a.no_fast_summary:
+        # the north star's fast mode on the same archive, beside the exact line
+        fast = fast_mode_summary(_native, cube, w0, shift, (nsub, nchan, nbin), local, a.steps, torch)
     flips = None
-    if fit_mode == _native.FIT_CLOSED and not sharded:
+    if fit_mode == _native.FIT_CLOSED and not sharded and not a.no_flip_check:
         # zap-mask flips of the fast mode against the exact fit on this archive (untimed)
-        fast = sess.run()
+        fres = sess.run()
         with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local) as ex:
             ex.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
             exact = ex.run()
-        flips = {"profiles": int(np.count_nonzero(fast["weights"] != exact["weights"])),
-                 "loops_fast": fast["loops"], "loops_exact": exact["loops"]}
+        flips = {"profiles": int(np.count_nonzero(fres["weights"] != exact["weights"])),
+                 "loops_fast": fres["loops"], "loops_exact": exact["loops"]}
     del cube
     torch.cuda.empty_cache()
     for _ in range(a.warmup):
@@ -428,6 +462,7 @@ def main():
     ktimes = sess.kernel_times()
     stats = sess.run_stats()
     n_iter = out["n_iter"]
+    exact_weights = sess.run()["weights"] if fast is not None else None
     sess.close()
 
     if rank == 0:
@@ -522,6 +557,9 @@ def main():
         }
         if flips is not None:
             rec["config"]["mask_flips_vs_exact"] = flips
+        if fast is not None:
+            fast["mask_flips_vs_exact"] = int(np.count_nonzero(fast.pop("weights") != exact_weights))
+            rec["fast_mode"] = fast
         if "exchange" in ktimes and ktimes["exchange"]["launches"]:
             rec["config"]["exchange_ms_per_step"] = round(ktimes["exchange"]["ms"] / a.steps, 3)
         if world == 1 and not a.no_cpu_baseline:

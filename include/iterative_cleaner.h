@@ -126,6 +126,12 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
  * f32 [nsub][nchan][nbin] — what --unload_res writes (:161-162). */
 int ic_get_residual(void *session, float *out);
 
+/* Profiles whose fit status was not 1-4 in each iteration of the last ic_run
+ * (the reference prints "Bad status for least squares fit when removing
+ * profile." once per such profile and loop, iterative_cleaner.py:284-285, and
+ * zeroes its residual).  Fills up to n entries; returns the iteration count. */
+int ic_get_bad_fits(void *session, int32_t *per_iter, int n);
+
 /* Last iteration's internals for parity checks (any may be NULL):
  * template T [nbin], fit amplitude/status [P] (:278), diagnostics [P] (:206-217). */
 int ic_get_template(void *session, float *T);
@@ -163,6 +169,14 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
 int ic_set_fit_tail(void *session, int64_t threshold);
 
 const char *ic_last_error(void);
+
+/* remove_profile1d (iterative_cleaner.py:275-288) on the GPU for nprof given
+ * profiles [nprof][nbin] f32 against the template T [nbin] f32: the amplitude
+ * (:278; fit_mode as ic_params.fit_mode) and status per profile, and the f32
+ * residual a*T - p (zeros for a status outside 1-4, :284-286).  Outputs may be
+ * NULL (not all).  Synchronous. */
+int ic_fit_profiles(int device, int nprof, int nbin, const float *T, const float *profiles, int fit_mode,
+                    double *amp_out, int32_t *info_out, float *resid_out);
 
 /* comprehensive_stats (iterative_cleaner.py:181-226) alone, on the GPU, for
  * the data the reference hands it (:111-117): data [nsub][nchan][nbin] f32 and

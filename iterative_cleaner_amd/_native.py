@@ -22,7 +22,8 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_set_timing", "ic_get_run_stats", "ic_set_fit_tail", "ic_last_error",
            "ic_shard_layout", "ic_session_create_shard", "ic_group_create", "ic_group_destroy",
            "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free",
-           "ic_upload_pols", "ic_comprehensive_stats")
+           "ic_upload_pols", "ic_comprehensive_stats", "ic_get_bad_fits",
+           "ic_fit_profiles")
 
 FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)
 FIT_CLOSED = 1   # IC_FIT_CLOSED: closed-form amplitude fused with the diagnostics (fast mode)
@@ -131,6 +132,8 @@ def load_library(path: str = LIB_PATH):
     lib.ic_group_destroy.argtypes = [vp]
     lib.ic_group_destroy.restype = None
     lib.ic_session_create_grouped.argtypes = [C.POINTER(Params), C.c_int, vp, C.c_int, C.POINTER(vp)]
+    lib.ic_get_bad_fits.argtypes = [vp, vp, C.c_int]
+    lib.ic_fit_profiles.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp]
     lib.ic_comprehensive_stats.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_double, C.c_double,
                                            vp, vp, vp, vp, vp]
     if lib.ic_abi_version() != ABI_VERSION:
@@ -257,8 +260,11 @@ class GpuSession:
         self._check(self.lib.ic_run(self.h, _ptr(test), _ptr(weights), _ptr(loops), _ptr(changed),
                                     _ptr(nzero), _ptr(n_iter), _ptr(conv)), "ic_run")
         k = int(n_iter[0])
+        bad = np.zeros(m, np.int32)
+        self._check(self.lib.ic_get_bad_fits(self.h, _ptr(bad), m), "ic_get_bad_fits")
         return dict(test=test, weights=weights, loops=int(loops[0]), n_iter=k,
-                    converged=bool(conv[0]), changed=changed[:k].copy(), nzero=nzero[:k].copy())
+                    converged=bool(conv[0]), changed=changed[:k].copy(), nzero=nzero[:k].copy(),
+                    bad_fits=bad[:k].copy())
 
     def residual(self):
         out = np.empty(self.shape, np.float32)
@@ -308,6 +314,24 @@ class GpuSession:
             name = self.lib.ic_kernel_name(buf[q].kernel).decode()
             out[name] = dict(ms=buf[q].ms, launches=buf[q].launches)
         return out
+
+
+def fit_profiles(profiles, template, fit_mode=FIT_EXACT, device=0):
+    """remove_profile1d (iterative_cleaner.py:275-288) on the GPU for the
+    (nprof, nbin) profiles: (amp f64, info i32, residual f32 a*T - p)."""
+    lib = load_library()
+    P = np.ascontiguousarray(profiles, dtype=np.float32)
+    if P.ndim != 2:
+        raise ValueError("fit_profiles: profiles must be (nprof, nbin)")
+    T = np.ascontiguousarray(template, dtype=np.float32).reshape(P.shape[1])
+    amp = np.empty(P.shape[0], np.float64)
+    info = np.empty(P.shape[0], np.int32)
+    R = np.empty(P.shape, np.float32)
+    rc = lib.ic_fit_profiles(int(device), P.shape[0], P.shape[1], _ptr(T), _ptr(P), int(fit_mode), _ptr(amp),
+                             _ptr(info), _ptr(R))
+    if rc != 0:
+        raise NativeError("ic_fit_profiles: %s (rc=%d)" % (_err(lib), rc))
+    return amp, info, R
 
 
 def comprehensive_stats(data, weights, chanthresh=5.0, subintthresh=5.0, device=0, diagnostics=False):

@@ -9,7 +9,11 @@ order so that the HIP kernels can reproduce it bit-for-bit:
 
 * samples and weights are float32 (``get_data``/``get_weights`` return f32
   copies);
-* ``pscrunch``: total intensity = f32(pol0 + pol1);
+* ``get_state``: psrchive's polarisation state names - "Intensity" (one
+  polarisation), "PPQQ" (AA, BB), "Coherence" (AA, BB, CR, CI) or "Stokes"
+  (I, Q, U, V);
+* ``pscrunch``: total intensity = f32(pol0 + pol1) for PPQQ / Coherence data,
+  pol 0 (= I) for Stokes data; the state becomes "Intensity";
 * ``dedisperse``/``dededisperse``: integer per-channel rotation by
   ``dm_shift[c]`` bins, ``ded[i] = raw[(i + shift) % nbin]``;
 * channel sums (baseline total, fscrunch) use the CANONICAL CHANNEL ORDER
@@ -37,7 +41,15 @@ SUPER_BLOCK = 256          # channels per canonical-order super-block
 BASELINE_DUTY = 0.15       # psrchive BaselineWindow default duty cycle
 
 __all__ = ["Archive", "Archive_load", "Profile", "Integration", "chan_sum", "sb_tree",
-           "baseline_width", "window_argmin", "SUPER_BLOCK", "BASELINE_DUTY"]
+           "baseline_width", "window_argmin", "SUPER_BLOCK", "BASELINE_DUTY", "STATES", "default_state",
+           "load_channels"]
+
+
+STATES = ("Intensity", "PPQQ", "Coherence", "Stokes")
+
+
+def default_state(npol: int) -> str:
+    return {1: "Intensity", 2: "PPQQ", 4: "Coherence"}.get(int(npol), "PPQQ")
 
 
 def sb_tree(parts):
@@ -136,12 +148,17 @@ class Archive:
     def __init__(self, data, weights=None, dm_shift=None, dedispersed=False,
                  filename="synthetic.ar", source="J0000+0000",
                  centre_frequency=1400.0, mjd_start=60000.0, mjd_end=60000.01,
-                 baseline_duty=BASELINE_DUTY):
+                 baseline_duty=BASELINE_DUTY, state=None):
         data = np.asarray(data, dtype=np.float32)
         if data.ndim != 4:
             raise ValueError("data must be (nsub, npol, nchan, nbin)")
         self._data = np.ascontiguousarray(data)
-        nsub, _, nchan, nbin = data.shape
+        nsub, npol, nchan, nbin = data.shape
+        if state is None:
+            state = default_state(npol)
+        if state not in STATES or (state == "Intensity") != (npol == 1):
+            raise ValueError("bad polarisation state %r for npol=%d" % (state, npol))
+        self._state = state
         if weights is None:
             weights = np.ones((nsub, nchan), dtype=np.float32)
         self._weights = np.array(weights, dtype=np.float32).reshape(nsub, nchan)
@@ -198,6 +215,9 @@ class Archive:
     def get_baseline_duty(self) -> float:
         return self._duty
 
+    def get_state(self) -> str:
+        return self._state
+
     def __str__(self) -> str:
         # "<format>:<name>"; the CLI (iterative_cleaner.py:49) splits on the first ':'
         return "NumPyArchive:%s" % os.path.splitext(self._filename)[0]
@@ -208,7 +228,11 @@ class Archive:
     # ---------------------------------------------------------------- transforms
     def pscrunch(self) -> None:
         if self.get_npol() > 1:
-            self._data = np.ascontiguousarray(self._data[:, 0:1] + self._data[:, 1:2])
+            if self._state == "Stokes":
+                self._data = np.ascontiguousarray(self._data[:, 0:1])
+            else:
+                self._data = np.ascontiguousarray(self._data[:, 0:1] + self._data[:, 1:2])
+            self._state = "Intensity"
 
     def _ded_view(self) -> np.ndarray:
         """Samples in the dedispersed frame (a copy if currently dispersed)."""
@@ -288,3 +312,11 @@ class Archive:
 def Archive_load(path: str) -> Archive:
     from . import archive_io
     return archive_io.load(path)
+
+
+def load_channels(path: str, c0: int, c1: int) -> Archive:
+    """Channels [c0, c1) of the archive at `path`, read without loading the rest
+    (channel-sharded cleaning: each rank holds its slice only).  The returned
+    archive carries ``_chan_range = (c0, c1)`` and ``_nchan_total``."""
+    from . import archive_io
+    return archive_io.load(path, channels=(c0, c1))

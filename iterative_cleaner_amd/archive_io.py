@@ -39,6 +39,7 @@ def save(ar: Archive, path: str) -> None:
         "mjd_start": ar.start_time().in_days(),
         "mjd_end": ar.end_time().in_days(),
         "baseline_duty": ar.get_baseline_duty(),
+        "state": ar.get_state(),
     }
     with open(path, "wb") as fh:
         np.savez(fh, data=ar._data, weights=ar._weights, dm_shift=ar._shift,
@@ -46,15 +47,67 @@ def save(ar: Archive, path: str) -> None:
                  meta=np.array(json.dumps(meta)))
 
 
-def load(path: str) -> Archive:
+def _npz_member(path: str, name: str, channels):
+    """Member `name` of an uncompressed .npz; with `channels` = (c0, c1), only
+    those channels (axis -2 of the (..., nchan, nbin) data array), read through a
+    memory map of the stored .npy so the other channels are never loaded."""
+    import zipfile
+    with zipfile.ZipFile(path) as zf:
+        info = zf.getinfo(name + ".npy")
+        if info.compress_type != zipfile.ZIP_STORED:
+            with zf.open(info) as f:
+                a = np.lib.format.read_array(f, allow_pickle=False)
+            return a[..., channels[0]:channels[1], :] if channels else a
+        with open(path, "rb") as fh:
+            fh.seek(info.header_offset)
+            local = fh.read(30)
+            nlen, xlen = int.from_bytes(local[26:28], "little"), int.from_bytes(local[28:30], "little")
+            fh.seek(info.header_offset + 30 + nlen + xlen)
+            version = np.lib.format.read_magic(fh)
+            shape, fortran, dtype = np.lib.format._read_array_header(fh, version)
+            offset = fh.tell()
+    if fortran:
+        raise ValueError("%s: Fortran-ordered %s" % (path, name))
+    mm = np.memmap(path, dtype=dtype, mode="r", offset=offset, shape=shape)
+    return np.array(mm[..., channels[0]:channels[1], :] if channels else mm)
+
+
+def probe_shape(path: str):
+    """(nsub, npol, nchan, nbin) of the archive at `path` from its headers alone."""
     if psrfits.is_psrfits(path):
-        return psrfits.load(path)
+        return psrfits.probe_shape(path)
+    import zipfile
+    with zipfile.ZipFile(path) as zf, zf.open("data.npy") as f:
+        version = np.lib.format.read_magic(f)
+        shape, _, _ = np.lib.format._read_array_header(f, version)
+    return tuple(int(x) for x in shape)
+
+
+def load(path: str, channels=None) -> Archive:
+    """The archive at `path`; channels = (c0, c1): only those channels (see
+    archive.load_channels)."""
+    if psrfits.is_psrfits(path):
+        return psrfits.load(path, channels=channels)
     with np.load(path, allow_pickle=False) as z:
         meta = json.loads(str(z["meta"]))
-        return Archive(z["data"], z["weights"], z["dm_shift"],
-                       dedispersed=bool(z["dedispersed"]), filename=path,
-                       source=meta.get("source", "J0000+0000"),
-                       centre_frequency=meta.get("centre_frequency", 1400.0),
-                       mjd_start=meta.get("mjd_start", 60000.0),
-                       mjd_end=meta.get("mjd_end", 60000.01),
-                       baseline_duty=meta.get("baseline_duty", 0.15))
+        weights, shift = z["weights"], z["dm_shift"]
+        dedispersed = bool(z["dedispersed"])
+        data = z["data"] if channels is None else None
+    nchan_total = weights.shape[1]
+    if channels is not None:
+        c0, c1 = int(channels[0]), int(channels[1])
+        if not 0 <= c0 < c1 <= nchan_total:
+            raise ValueError("%s: channel range %s outside [0, %d)" % (path, (c0, c1), nchan_total))
+        data = _npz_member(path, "data", (c0, c1))
+        weights, shift = weights[:, c0:c1], shift[c0:c1]
+    ar = Archive(data, weights, shift, dedispersed=dedispersed, filename=path,
+                 source=meta.get("source", "J0000+0000"),
+                 centre_frequency=meta.get("centre_frequency", 1400.0),
+                 mjd_start=meta.get("mjd_start", 60000.0),
+                 mjd_end=meta.get("mjd_end", 60000.01),
+                 baseline_duty=meta.get("baseline_duty", 0.15),
+                 state=meta.get("state"))
+    if channels is not None:
+        ar._chan_range = (int(channels[0]), int(channels[1]))
+        ar._nchan_total = int(nchan_total)
+    return ar

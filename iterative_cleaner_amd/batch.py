@@ -42,22 +42,29 @@ def pipeline(session, items, fetch=True):
     yield session.run(fetch)
 
 
-def run_lanes(sessions, items, fetch=True):
+def run_lanes(sessions, items, fetch=True, stop=None):
     """Clean every (cube, w0, shift) of `items` on `len(sessions)` sessions of one
     shape concurrently (one host thread per session, shared work queue; each
     session overlaps its next upload with its current run).  The arrays must
     stay valid until their result is yielded.  Yields the ic_run dicts in input
-    order.  One session: exactly `pipeline`."""
+    order.  One session: exactly `pipeline`.
+
+    On a worker error, or when the consumer stops early (generator closed), the
+    lanes stop: the `stop` event (created here if not given) is set, queued work
+    is dropped, and the generator returns only after every worker thread has
+    exited - a worker finishes at most the run it is in, so no thread is inside
+    ic_run when the caller closes the sessions."""
     if len(sessions) == 1:
         yield from pipeline(sessions[0], items, fetch)
         return
+    stop = stop if stop is not None else threading.Event()
     work = queue.Queue(maxsize=2 * len(sessions))
     done = queue.Queue()
 
     def worker(sess):
         pending = None   # index uploaded to this session, not yet run
         try:
-            while True:
+            while not stop.is_set():
                 try:
                     item = work.get_nowait()
                 except queue.Empty:
@@ -66,16 +73,17 @@ def run_lanes(sessions, items, fetch=True):
                         pending = None
                         continue
                     item = work.get()
-                if item is None:
+                if item is None or stop.is_set():
                     break
                 idx, arrays = item
                 sess.upload_async(*arrays)
                 if pending is not None:
                     done.put((pending, sess.run(fetch)))
                 pending = idx
-            if pending is not None:
+            if pending is not None and not stop.is_set():
                 done.put((pending, sess.run(fetch)))
         except BaseException as e:  # noqa: BLE001 - re-raised by the consumer
+            stop.set()
             done.put((-1, e))
 
     threads = [threading.Thread(target=worker, args=(sess,), daemon=True) for sess in sessions]
@@ -84,17 +92,29 @@ def run_lanes(sessions, items, fetch=True):
     n = 0
     feed_error = []
 
+    def put(item):
+        while not stop.is_set():
+            try:
+                work.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
     def feed():
         nonlocal n
         try:
             for arrays in items:
-                work.put((n, arrays))
+                if not put((n, arrays)):
+                    return
                 n += 1
         except BaseException as e:  # noqa: BLE001
             feed_error.append(e)
+            stop.set()
         finally:
             for _ in threads:
-                work.put(None)
+                if not put(None):
+                    break
 
     feeder = threading.Thread(target=feed, daemon=True)
     feeder.start()
@@ -120,9 +140,20 @@ def run_lanes(sessions, items, fetch=True):
         if ready or nxt != n:
             raise RuntimeError("batch lanes lost archives %d..%d" % (nxt, n - 1))
     finally:
-        feeder.join(timeout=60)
+        stop.set()
+        while True:                       # drop queued work; wake blocked workers
+            try:
+                work.get_nowait()
+            except queue.Empty:
+                break
+        for _ in threads:
+            try:
+                work.put_nowait(None)
+            except queue.Full:
+                break
         for th in threads:
-            th.join(timeout=60)
+            th.join()                     # at most the run a worker is in
+        feeder.join(timeout=5.0)          # may wait in `items`: the caller's stop ends that
 
 
 class _Ring:
@@ -194,20 +225,24 @@ def clean_batch(loader, shape, device=0, ring=None, max_iter=5, chanthresh=5.0, 
 
     order = []
     sessions = []
+    lanes_gen = None
     try:
         for _ in range(lanes):
             sessions.append(_native.GpuSession(nsub, nchan, nbin, max_iter, chanthresh, subintthresh,
                                                pulse_region, baseline_duty, device=device))
-        for k, out in enumerate(run_lanes(sessions, staged())):
+        lanes_gen = run_lanes(sessions, staged(), stop=stop)
+        for k, out in enumerate(lanes_gen):
             free.put(order[k])          # archive k's slot is free once its result is yielded
             yield out
         if error:
             raise error[0]
     finally:
+        stop.set()                      # loader and lanes stop taking archives
+        for _ in range(ring):
+            free.put(0)                 # a loader waiting for a slot wakes up and returns
+        if lanes_gen is not None:
+            lanes_gen.close()           # returns once no worker thread is inside ic_run
+        th.join(timeout=60)
         for sess in sessions:
             sess.close()
-        stop.set()
-        for _ in range(ring):
-            free.put(0)
-        th.join(timeout=60)
         rg.close()

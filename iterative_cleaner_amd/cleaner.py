@@ -84,14 +84,14 @@ def main(args):
     """CLI driver (iterative_cleaner.py:59-62).  Under torchrun each rank cleans
     its round-robin share of the archive list on its own GPU (batch mode,
     SURVEY.md §8(e): no collective).  With IC_CHANNEL_SHARDS=1 the ranks instead
-    clean every archive together, each on its channel shard (config C3), and
-    rank 0 writes the outputs."""
+    clean every archive together, each on its channel shard (config C3): a rank
+    reads only its channel slice of the file, and rank 0 writes the outputs."""
     from .dist import channel_sharding, rank_world, shard
     rank, world, _ = rank_world()
     backend = archive_backend()
     together = channel_sharding()
     for arch in (args.archive if together else shard(args.archive, rank, world)):
-        ar = backend.Archive_load(arch)
+        ar = _load_shard(backend, arch, rank, world) if together else backend.Archive_load(arch)
         o_name = _output_name(ar, args)
         ar = clean(ar, args, arch)
         if together and rank != 0:
@@ -99,6 +99,19 @@ def main(args):
         ar.unload(o_name)
         if not args.quiet:
             print("Cleaned archive: %s" % o_name)
+
+
+def _load_shard(backend, arch, rank, world):
+    """This rank's channel slice of the archive (channel-sharded CLI).  The
+    stand-in formats (npz, PSRFITS) are read slice-only from their headers and a
+    memory map; an archive backend that cannot do that (real psrchive) is loaded
+    whole and sliced in memory (run_loop)."""
+    if backend.__name__.endswith("archive") and hasattr(backend, "load_channels"):
+        from . import archive_io
+        nsub, _, nchan, _ = archive_io.probe_shape(arch)
+        chans, _ = _native.shard_layout(nsub, nchan, world)
+        return backend.load_channels(arch, *chans[rank])
+    return backend.Archive_load(arch)
 
 
 def _dm_shift(ar) -> np.ndarray:
@@ -118,12 +131,22 @@ def _dm_shift(ar) -> np.ndarray:
     return out
 
 
+def _state(ar) -> str:
+    """psrchive polarisation state name ("Intensity", "PPQQ", "Coherence",
+    "Stokes"); archives without get_state are taken by their npol."""
+    if hasattr(ar, "get_state"):
+        return str(ar.get_state())
+    return {1: "Intensity", 2: "PPQQ", 4: "Coherence"}.get(ar.get_npol(), "PPQQ")
+
+
 def _loop_input(ar) -> np.ndarray:
-    """What the loop cleans: (nsub, nchan, nbin) f32 when the archive holds one
-    polarisation, else the full-pol (nsub, npol, nchan, nbin) f32 data, which
+    """What the loop cleans (the pscrunched data of iterative_cleaner.py:70,
+    :89, :98): (nsub, nchan, nbin) f32 when the archive holds one polarisation
+    or is in the Stokes state (total intensity = I = pol 0, psrchive pscrunch),
+    else the full-pol (nsub, npol, nchan, nbin) f32 AA, BB(, CR, CI) data, which
     the GPU pscrunches (ic_upload_pols: total intensity f32(pol0 + pol1))."""
     data = ar.get_data()
-    if data.shape[1] == 1:
+    if data.shape[1] == 1 or _state(ar) == "Stokes":
         return np.ascontiguousarray(data[:, 0], dtype=np.float32)
     return np.ascontiguousarray(data, dtype=np.float32)
 
@@ -135,11 +158,13 @@ def _device() -> int:
     return 0
 
 
-def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15):
+def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15, nchan_total=None):
     """Run the GPU loop on a (nsub, nchan, nbin) f32 cube, or on full-polarisation
     data (nsub, npol, nchan, nbin) that the GPU pscrunches; returns the ic_run dict
     (+ ``residual`` when requested).  Under channel sharding (dist.channel_sharding)
-    every rank runs its channel shard and gets the merged result."""
+    every rank runs its channel shard and gets the merged result: `cube` is then
+    either the whole archive (sliced here) or, with ``nchan_total`` set, already
+    this rank's channel slice (read slice-only from the file)."""
     pols = cube.ndim == 4
     nsub, nchan, nbin = (cube.shape[0], cube.shape[2], cube.shape[3]) if pols else cube.shape
     from .dist import channel_sharding
@@ -149,15 +174,20 @@ def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_d
         from . import sharded
         from .dist import rank_world
         rank, world, local = rank_world()
-        chans, _ = _native.shard_layout(nsub, nchan, world)
-        c0, c1 = chans[rank]
         dev = torch.device("cuda", _device() if device is None else device)
-        part = cube[:, :, c0:c1] if pols else cube[:, c0:c1]
+        if nchan_total is None:
+            chans, _ = _native.shard_layout(nsub, nchan, world)
+            c0, c1 = chans[rank]
+            cube = cube[:, :, c0:c1] if pols else cube[:, c0:c1]
+            w0, shift = np.asarray(w0)[:, c0:c1], np.asarray(shift)[c0:c1]
+            nchan_total = nchan
         return sharded.clean_cube_dist(
-            np.ascontiguousarray(part), np.ascontiguousarray(np.asarray(w0)[:, c0:c1]),
-            np.asarray(shift)[c0:c1], (nsub, nchan, nbin), dev, want_residual=want_residual,
+            np.ascontiguousarray(cube), np.ascontiguousarray(w0), np.asarray(shift), (nsub, nchan_total, nbin),
+            dev, want_residual=want_residual,
             max_iter=args.max_iter, chanthresh=args.chanthresh, subintthresh=args.subintthresh,
             pulse_region=args.pulse_region, baseline_duty=baseline_duty)
+    if nchan_total is not None and nchan_total != nchan:
+        raise ValueError("a channel slice of an archive needs channel sharding")
     with _native.GpuSession(nsub, nchan, nbin, args.max_iter, args.chanthresh, args.subintthresh,
                             args.pulse_region, baseline_duty,
                             device=_device() if device is None else device) as s:
@@ -214,41 +244,56 @@ def _plot_zap(test, ar_name, args):
     plt.savefig("%s_%s_%s.png" % (ar_name, args.chanthresh, args.subintthresh), bbox_inches="tight")
 
 
+BAD_STATUS = "Bad status for least squares fit when removing profile."
+
+
 def clean(ar, args, arch):
     """Surgical cleaning of one archive (iterative_cleaner.py:65-178).  Under
-    channel sharding only rank 0 prints and writes files."""
+    channel sharding only rank 0 prints and writes files; `ar` may then be this
+    rank's channel slice (main() reads slice-only) and rank 0 loads the whole
+    archive for the output."""
     from .dist import channel_sharding, rank_world
-    if channel_sharding() and rank_world()[0] != 0:
+    sharding = channel_sharding()
+    if sharding and rank_world()[0] != 0:
         args = argparse.Namespace(**dict(vars(args), quiet=True, no_log=True, print_zap=False))
         _side_effects = False
     else:
         _side_effects = True
     backend = archive_backend()
+    chan_slice = getattr(ar, "_chan_range", None) is not None
+    nchan_total = ar._nchan_total if chan_slice else None
     orig_weights = ar.get_weights()
     # The reference pscrunches the archive in memory unless --memory without -p
     # (iterative_cleaner.py:67-70).  Only -p keeps that pscrunched copy as the
     # output; otherwise the archive is reloaded (or kept full-pol with --memory),
     # so its data go to the GPU full-pol and are pscrunched there.
-    if args.pscrunch:
+    if args.pscrunch and not chan_slice:
         ar.pscrunch()
     ar_name = ar.get_filename().split()[-1]
     max_iterations = args.max_iter
+    size = orig_weights.shape[0] * nchan_total if chan_slice else orig_weights.size
     if not args.quiet:
-        print("Total number of profiles: %s" % orig_weights.size)
+        print("Total number of profiles: %s" % size)
 
     cube = _loop_input(ar)
     shift = _dm_shift(ar)
     duty = ar.get_baseline_duty() if hasattr(ar, "get_baseline_duty") else 0.15
-    out = run_loop(cube, orig_weights, shift, args, want_residual=args.unload_res,
-                   baseline_duty=duty)
+    out = run_loop(cube, orig_weights, shift, args, want_residual=args.unload_res, baseline_duty=duty,
+                   nchan_total=nchan_total)
+    del cube
 
-    size = orig_weights.size
     x = 0
     loops = None
+    bad = out.get("bad_fits", [0] * out["n_iter"])
     for k in range(out["n_iter"]):
         x = k + 1
         if not args.quiet:
             print("Loop: %s" % x)
+        if _side_effects:
+            # printed by remove_profile1d for every failed fit, -q or not (:284-285)
+            for _ in range(int(bad[k])):
+                print(BAD_STATUS)
+        if not args.quiet:
             rfi_frac = out["nzero"][k] / float(size)
             print("Differences to previous weights: %s  RFI fraction: %s"
                   % (int(out["changed"][k]), rfi_frac))
@@ -265,7 +310,17 @@ def clean(ar, args, arch):
         raise NameError("name 'avg_test_results' is not defined")
     avg_test_results = out["test"]
 
-    if not args.pscrunch and not args.memory:
+    if chan_slice:
+        if not _side_effects:
+            return ar              # outputs are rank 0's
+        # the whole archive for the output: what the reference holds at :150-153
+        # (reloaded; or the in-memory archive, pscrunched with -p)
+        ar = backend.Archive_load(arch)
+        orig_weights = ar.get_weights()      # the residual archive's weights (pscrunch keeps them)
+        if args.pscrunch:
+            ar.pscrunch()
+        shift = _dm_shift(ar)
+    elif not args.pscrunch and not args.memory:
         ar = backend.Archive_load(arch)
     set_weights_archive(ar, avg_test_results)
     if args.bad_chan != 1 or args.bad_subint != 1:

@@ -179,7 +179,10 @@ size_t diag_lds_bytes(int nbin);
 hipError_t launch_tnorm(hipStream_t st, const double *T64, const PwPlan *plan, int nleaf_ub, double *TT);
 // which: bit 0 = column lines (length nsub), bit 1 = row lines (length nchan)
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which = 3);
-hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const float *w0,
+// counters: [0] changed, [1] zero weights, [2] fit statuses outside 1-4 (info
+// may be null), [3+h] new weights != history h (iterative_cleaner.py:127-141)
+hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const int32_t *info,
+                          const float *w0,
                           const double *std_d, const double *mean_d, const float *ptp_d,
                           const double *fft_d, const double *col_med, const double *col_mad,
                           const double *row_med, const double *row_mad, double chanthresh,

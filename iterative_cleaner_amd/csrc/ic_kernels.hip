@@ -595,7 +595,11 @@ __device__ int lm_after_qtf(LmState &L)
     if (L.fnorm != 0.0 && L.acnorm != 0.0) {
         double sum = 0.0;
         sum += L.r * (L.qtf / L.fnorm);
-        L.gnorm = dmax_(L.gnorm, fabs(sum / L.acnorm));
+        // scipy's MINPACK keeps gnorm = 0 when the term is NaN (a non-finite
+        // profile): info 4 at once, x = 1 (probed against scipy 1.15.3;
+        // tests/golden/leastsq_nonfinite.npz)
+        const double g = fabs(sum / L.acnorm);
+        if (g > L.gnorm) L.gnorm = g;
     }
     if (L.gnorm <= 0.0) {  // gtol = 0
         L.info = 4;
@@ -2526,9 +2530,11 @@ __device__ __forceinline__ double nanmax2(double a, double b)
     return a > b ? a : b;
 }
 
-// counters: [0] changed vs hist[iter-1], [1] zero weights, [2+h] != hist[h]
+// counters: [0] changed vs hist[iter-1], [1] zero weights, [2] profiles whose
+// fit status is not 1-4 (info may be null: 0), [3+h] != hist[h]
 __global__ __launch_bounds__(256) void k_combine(
-    int nsub, int nchan, const uint8_t *__restrict__ valid, const float *__restrict__ w0,
+    int nsub, int nchan, const uint8_t *__restrict__ valid, const int32_t *__restrict__ info,
+    const float *__restrict__ w0,
     const double *__restrict__ std_d, const double *__restrict__ mean_d, const float *__restrict__ ptp_d,
     const double *__restrict__ fft_d, const double *__restrict__ col_med, const double *__restrict__ col_mad,
     const double *__restrict__ row_med, const double *__restrict__ row_mad, double cth, double sth,
@@ -2537,10 +2543,10 @@ __global__ __launch_bounds__(256) void k_combine(
 {
     // grid-stride; the convergence counters are reduced per block (one atomic
     // per counter per block: same-address atomics serialise at the memory side)
-    __shared__ int red[2][4];
+    __shared__ int red[3][4];
     __shared__ unsigned long long dred[4];
     const size_t P = (size_t)nsub * nchan;
-    int changed = 0, zero = 0;
+    int changed = 0, zero = 0, bad = 0;
     unsigned long long diff = 0ull;   // bit h: W != hist[h] somewhere (h < 64)
     const int hmax = iter < 64 ? iter : 64;
     for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < P; k += (size_t)gridDim.x * blockDim.x) {
@@ -2575,37 +2581,45 @@ __global__ __launch_bounds__(256) void k_combine(
         hist[(size_t)iter * P + k] = wn;
         changed += !(wn == hist[(size_t)(iter - 1) * P + k]);
         zero += (wn == 0.0f);
+        if (info) {   // "Bad status for least squares fit" (iterative_cleaner.py:284-285)
+            const int st = info[k];
+            bad += (st < 1 || st > 4);
+        }
         // history equality (iterative_cleaner.py:135-136)
         for (int h = 0; h < hmax; ++h)
             if (!(wn == hist[(size_t)h * P + k])) diff |= 1ull << h;
         for (int h = 64; h < iter; ++h)
-            if (!(wn == hist[(size_t)h * P + k])) atomicOr(&counters[2 + h], 1);
+            if (!(wn == hist[(size_t)h * P + k])) atomicOr(&counters[3 + h], 1);
     }
     for (int off = 32; off > 0; off >>= 1) {
         changed += __shfl_xor(changed, off);
         zero += __shfl_xor(zero, off);
+        bad += __shfl_xor(bad, off);
         diff |= __shfl_xor(diff, off);
     }
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         red[0][wave] = changed;
         red[1][wave] = zero;
+        red[2][wave] = bad;
         dred[wave] = diff;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int ch = 0, ze = 0;
+        int ch = 0, ze = 0, bd = 0;
         unsigned long long df = 0ull;
         for (int w = 0; w < nw; ++w) {
             ch += red[0][w];
             ze += red[1][w];
+            bd += red[2][w];
             df |= dred[w];
         }
         // counters[0..1] (changed, zero) as one u64 add: both < 2^32, no carry
         if (ch || ze)
             atomicAdd((unsigned long long *)counters, ((unsigned long long)(unsigned)ze << 32) | (unsigned)ch);
+        if (bd) atomicAdd(&counters[2], bd);
         for (int h = 0; h < hmax; ++h)
-            if ((df >> h) & 1ull) atomicOr(&counters[2 + h], 1);
+            if ((df >> h) & 1ull) atomicOr(&counters[3 + h], 1);
     }
 }
 
@@ -2995,7 +3009,8 @@ hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
     return hipSuccess;
 }
 
-hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const float *w0,
+hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const int32_t *info,
+                          const float *w0,
                           const double *std_d, const double *mean_d, const float *ptp_d,
                           const double *fft_d, const double *col_med, const double *col_mad,
                           const double *row_med, const double *row_mad, double chanthresh,
@@ -3004,7 +3019,7 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
 {
     const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 256), 1024);
-    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(256), 0, st, nsub, nchan, valid, w0, std_d,
+    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(256), 0, st, nsub, nchan, valid, info, w0, std_d,
                        mean_d, ptp_d, fft_d, col_med, col_mad, row_med, row_mad, chanthresh, subintthresh,
                        test, W, hist, iter, counters);
     return hipGetLastError();

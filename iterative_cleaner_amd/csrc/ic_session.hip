@@ -116,6 +116,7 @@ struct Session {
     int plan_ub = 0;            // max(leaves, ops) of the pairwise plan (k_tnorm scratch)
     long tail_threshold = kTailProfiles;
     ic_run_stats stats{};
+    std::vector<int32_t> bad_fits;   // per iteration of the last run: fit statuses outside 1-4
     // timing
     bool timing = false;
     std::vector<Timed> events;
@@ -733,12 +734,12 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
                   {(void **)&s->xd_recv, drecv, "diagnostics receive"},
                   {(void **)&s->xr_send, sizeof(double) * 8 * s->rows_pad, "row statistics"},
                   {(void **)&s->xr_recv, sizeof(double) * 8 * s->rows_pad * world, "gathered row statistics"},
-                  {(void **)&s->counters, sizeof(int32_t) * (p.max_iter + 4), "counters"}};
+                  {(void **)&s->counters, sizeof(int32_t) * (p.max_iter + 5), "counters"}};
         for (auto &b : xb)
             if (s->comm->alloc(b.ptr, b.bytes + 16) != 0 || !*b.ptr)
                 return bail(fail(IC_ENOMEM, "exchange buffer (%s, %zu bytes) failed", b.name, b.bytes));
     } else {
-        AL(s->counters, (size_t)(p.max_iter + 4));
+        AL(s->counters, (size_t)(p.max_iter + 5));
     }
 #undef AL
     if (hipHostMalloc((void **)&s->h_rcount, sizeof(int32_t) * kMaxRounds,
@@ -1047,7 +1048,8 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     la.col_mad = s->lstat + 4 * nchan;
     la.row_med = s->lstat + 8 * nchan;
     la.row_mad = s->lstat + 8 * nchan + 4 * nsub;
-    std::vector<int32_t> cnt(p.max_iter + 4);
+    std::vector<int32_t> cnt(p.max_iter + 5);
+    s->bad_fits.clear();
     int x = 0, loops = -1, n_iter = 0, converged = 0;
     // k_fit_tail's sweep counter (after the per-round counters): one run's total
     CK(hipMemsetAsync((unsigned long long *)s->rcount + kMaxRounds, 0, sizeof(unsigned long long), s->stream));
@@ -1066,20 +1068,21 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, la, s->comm ? 1 : 3));
         if (s->comm)
             if (int rc = shard_rowstats(s, la)) return rc;
-        CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t) * (p.max_iter + 4), s->stream));
+        CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t) * (p.max_iter + 5), s->stream));
         LAUNCH(s, K_COMBINE,
-               launch_combine(s->stream, nsub, nchan, s->valid, s->w0, s->std_, s->mean, s->ptp, s->fft,
+               launch_combine(s->stream, nsub, nchan, s->valid, s->info, s->w0, s->std_, s->mean, s->ptp, s->fft,
                               la.col_med, la.col_mad, la.row_med, la.row_mad, p.chanthresh, p.subintthresh,
                               s->test, s->W, s->hist, n_iter, s->counters));
         if (s->comm)
-            CM(s, s->comm->allreduce_sum_i32(s->counters, (size_t)(n_iter + 2), s->stream), "convergence counters");
-        CK(hipMemcpyAsync(cnt.data(), s->counters, sizeof(int32_t) * (n_iter + 2), hipMemcpyDeviceToHost,
+            CM(s, s->comm->allreduce_sum_i32(s->counters, (size_t)(n_iter + 3), s->stream), "convergence counters");
+        CK(hipMemcpyAsync(cnt.data(), s->counters, sizeof(int32_t) * (n_iter + 3), hipMemcpyDeviceToHost,
                           s->stream));
         CK(hipStreamSynchronize(s->stream));
         if (changed_out) changed_out[n_iter - 1] = cnt[0];
         if (nzero_out) nzero_out[n_iter - 1] = cnt[1];
+        s->bad_fits.push_back(cnt[2]);
         for (int h = 0; h < n_iter; ++h)
-            if (cnt[2 + h] == 0) {
+            if (cnt[3 + h] == 0) {
                 loops = x;
                 converged = 1;
                 x = 1000000;
@@ -1142,6 +1145,15 @@ int ic_get_residual(void *session, float *out)
     (void)hipFree(R);
     if (e != hipSuccess) return fail(IC_EHIP, "residual: %s", hipGetErrorString(e));
     return IC_OK;
+}
+
+int ic_get_bad_fits(void *session, int32_t *per_iter, int n)
+{
+    Session *s = (Session *)session;
+    if (!s || (!per_iter && n > 0)) return fail(IC_EINVAL, "null argument");
+    const int m = (int)s->bad_fits.size();
+    for (int q = 0; q < m && q < n; ++q) per_iter[q] = s->bad_fits[q];
+    return m;
 }
 
 int ic_set_fit_tail(void *session, int64_t threshold)
@@ -1281,7 +1293,7 @@ int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const floa
     la.row_med = lstat + 8 * nchan;
     la.row_mad = lstat + 8 * nchan + 4 * nsub;
     CK(launch_linestats(st, la, 3));
-    CK(launch_combine(st, nsub, nchan, valid, w0, sd, mn, pt, ff, la.col_med, la.col_mad, la.row_med, la.row_mad,
+    CK(launch_combine(st, nsub, nchan, valid, nullptr, w0, sd, mn, pt, ff, la.col_med, la.col_mad, la.row_med, la.row_mad,
                       chanthresh, subintthresh, test, W, hist, 1, cnt));
     CK(hipMemcpyAsync(test_out, test, 8 * P, hipMemcpyDeviceToHost, st));
     if (std_o) CK(hipMemcpyAsync(std_o, sd, 8 * P, hipMemcpyDeviceToHost, st));
@@ -1289,6 +1301,69 @@ int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const floa
     if (ptp_o) CK(hipMemcpyAsync(ptp_o, pt, 4 * P, hipMemcpyDeviceToHost, st));
     if (fftmax_o) CK(hipMemcpyAsync(fftmax_o, ff, 8 * P, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
+    return IC_OK;
+}
+
+// remove_profile1d (iterative_cleaner.py:275-288) over caller-given profiles:
+// a one-shot session of nsub x nchan >= nprof profiles (zero rows pad the last
+// subint) whose fit cube is the profiles themselves, then the session's fit
+// (exact: run_fit; closed form: the fused kernel on raw rows with a zero
+// baseline) and k_residual with no dispersion shift.
+int ic_fit_profiles(int device, int nprof, int nbin, const float *T, const float *profiles, int fit_mode,
+                    double *amp_out, int32_t *info_out, float *resid_out)
+{
+    if (!T || !profiles || (!amp_out && !info_out && !resid_out)) return fail(IC_EINVAL, "null argument");
+    if (nprof <= 0 || nbin <= 0) return fail(IC_EINVAL, "bad shape nprof=%d nbin=%d", nprof, nbin);
+    ic_params p{};
+    p.nchan = nprof < 4096 ? nprof : 4096;
+    p.nsub = (nprof + p.nchan - 1) / p.nchan;
+    p.nbin = nbin;
+    p.max_iter = 1;
+    p.chanthresh = p.subintthresh = 5.0;
+    p.baseline_duty = 0.15;
+    p.fit_mode = fit_mode;
+    void *h = nullptr;
+    int rc = create_session(&p, device, 0, 1, false, [](const char **) -> Comm * { return nullptr; }, &h);
+    if (rc) return rc;
+    Session *s = (Session *)h;
+    struct Guard {
+        Session *s;
+        ~Guard() { ic_session_destroy(s); }
+    } guard{s};
+    const size_t P = s->P, row = sizeof(float) * (size_t)nbin;
+    std::vector<double> t64(s->ldD, 0.0);
+    for (int i = 0; i < nbin; ++i) t64[i] = (double)T[i];
+    CK(hipMemcpyAsync(s->T64, t64.data(), sizeof(double) * s->ldD, hipMemcpyHostToDevice, s->stream));
+    CK(hipMemsetAsync(s->shift, 0, sizeof(int32_t) * s->nchan, s->stream));
+    CK(hipMemsetAsync(s->base0, 0, sizeof(float) * P, s->stream));
+    {
+        std::vector<float> ones(P, 1.0f);
+        CK(hipMemcpyAsync(s->w0, ones.data(), sizeof(float) * P, hipMemcpyHostToDevice, s->stream));
+        CK(hipStreamSynchronize(s->stream));
+    }
+    CK(hipMemsetAsync(s->raw, 0, sizeof(float) * s->N, s->stream));
+    CK(hipMemcpyAsync(s->raw, profiles, row * nprof, hipMemcpyHostToDevice, s->stream));
+    if (fit_mode == IC_FIT_EXACT) {
+        CK(hipMemcpy2DAsync(s->D, sizeof(float) * s->ldD, s->raw, row, row, P, hipMemcpyDeviceToDevice, s->stream));
+        if (int r = run_fit(s)) return r;
+    } else {
+        CK(launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
+        DiagArgs da = diag_args(s, 0, 0);
+        CK(launch_diag(s->stream, da));
+    }
+    if (amp_out) CK(hipMemcpyAsync(amp_out, s->amp, sizeof(double) * nprof, hipMemcpyDeviceToHost, s->stream));
+    if (info_out) CK(hipMemcpyAsync(info_out, s->info, sizeof(int32_t) * nprof, hipMemcpyDeviceToHost, s->stream));
+    if (resid_out) {
+        float *R = nullptr;
+        CK(hipMalloc((void **)&R, sizeof(float) * s->N));
+        hipError_t e = launch_residual(s->stream, s->D, s->raw, s->base0, s->T64, s->amp, s->info, s->shift, p.nsub,
+                                       s->nchan, nbin, s->ldD, 0, 1.0, 0, 0, R);
+        if (e == hipSuccess) e = hipMemcpyAsync(resid_out, R, row * nprof, hipMemcpyDeviceToHost, s->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+        (void)hipFree(R);
+        if (e != hipSuccess) return fail(IC_EHIP, "ic_fit_profiles residual: %s", hipGetErrorString(e));
+    }
+    CK(hipStreamSynchronize(s->stream));
     return IC_OK;
 }
 

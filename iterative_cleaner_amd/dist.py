@@ -47,10 +47,18 @@ def channel_sharding() -> bool:
         backend = os.environ.get("IC_SHARD_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout())
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout())
     return True
+
+
+def pg_timeout():
+    """Process-group timeout of the channel-shard exchanges (IC_PG_TIMEOUT
+    seconds, default 300): a peer that stops taking part makes the others'
+    collectives fail after this long instead of blocking for ever."""
+    import datetime
+    return datetime.timedelta(seconds=float(os.environ.get("IC_PG_TIMEOUT", "300")))
 
 
 def shard(items: Sequence[T], rank: int, world: int) -> list[T]:
@@ -85,7 +93,7 @@ class TorchComm:
     the C++ side as a non-zero return code (the session then fails loudly).
     """
 
-    def __init__(self, device, group=None):
+    def __init__(self, device, group=None, fail_at=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -97,6 +105,36 @@ class TorchComm:
         self.bufs = {}
         self.error = None
         self._ops = None
+        # fault injection (tests): the fail_at-th collective of this rank raises
+        self.fail_at = fail_at
+        self.calls = 0
+        self.aborted = False
+
+    def _count(self):
+        self.calls += 1
+        if self.fail_at is not None and self.calls == self.fail_at:
+            raise RuntimeError("injected transport failure at collective %d (rank %d)" % (self.calls, self.rank))
+
+    def abort(self):
+        """Called when this rank's session failed: tear the process group down so
+        that peers blocked in a collective with this rank get an error (gloo:
+        connection closed at once; RCCL: the communicator is aborted, or the
+        peers' collectives fail at the process-group timeout)."""
+        if self.aborted:
+            return
+        self.aborted = True
+        dist = self.dist
+        try:
+            from torch.distributed import distributed_c10d as c10d
+            if hasattr(c10d, "_abort_process_group"):
+                c10d._abort_process_group(self.group)
+                return
+        except Exception:  # noqa: BLE001 - fall back to destroying the group
+            pass
+        try:
+            dist.destroy_process_group(self.group)
+        except Exception:  # noqa: BLE001
+            pass
 
     # ------------------------------------------------------------ buffers
     def alloc(self, nbytes):
@@ -124,6 +162,7 @@ class TorchComm:
 
     def allgather(self, send, recv, stream=None):
         dist = self.dist
+        self._count()
         with self._stream_ctx(stream):
             if self._staged():
                 self.torch.cuda.current_stream(self.device).synchronize()
@@ -137,6 +176,7 @@ class TorchComm:
 
     def alltoallv(self, send, send_sizes, recv, recv_sizes, stream=None):
         dist = self.dist
+        self._count()
         with self._stream_ctx(stream):
             if self._staged():
                 self.torch.cuda.current_stream(self.device).synchronize()
@@ -148,6 +188,7 @@ class TorchComm:
 
     def allreduce_sum(self, t, stream=None):
         dist = self.dist
+        self._count()
         with self._stream_ctx(stream):
             if self._staged():
                 self.torch.cuda.current_stream(self.device).synchronize()

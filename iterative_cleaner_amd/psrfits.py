@@ -130,6 +130,12 @@ def quantise(data: np.ndarray):
     return q, scl, offs
 
 
+# psrchive state <-> PSRFITS POL_TYPE (fold-mode SUBINT keyword)
+STATE_POL_TYPE = {"Intensity": "AA+BB", "PPQQ": "AABB", "Coherence": "AABBCRCI", "Stokes": "IQUV"}
+POL_TYPE_STATE = {"AA+BB": "Intensity", "INTEN": "Intensity", "I": "Intensity", "AABB": "PPQQ",
+                  "AABBCRCI": "Coherence", "IQUV": "Stokes"}
+
+
 def decode(q: np.ndarray, scl: np.ndarray, offs: np.ndarray) -> np.ndarray:
     return (q.astype(np.float32) * scl[..., None] + offs[..., None]).astype(np.float32)
 
@@ -174,7 +180,7 @@ def save(ar, path: str, stand_in_meta: bool = True) -> None:
     mjd0 = float(ar.start_time().in_days())
     imjd = int(np.floor(mjd0))
     smjd = (mjd0 - imjd) * 86400.0
-    pol_type = {1: "AA+BB", 2: "AABB", 4: "AABBCRCI"}.get(npol, "AABB")
+    pol_type = STATE_POL_TYPE.get(ar.get_state(), "AABB")
     primary = [("SIMPLE", True), ("BITPIX", 8), ("NAXIS", 0), ("EXTEND", True),
                ("FITSTYPE", "PSRFITS"), ("HDRVER", "6.1"), ("OBS_MODE", "PSR"),
                ("TELESCOP", "SYNTH"), ("SRC_NAME", ar.get_source()), ("OBSFREQ", cfreq),
@@ -221,7 +227,27 @@ def _columns(hdr: dict):
     return np.dtype(fields), tdims
 
 
-def load(path: str):
+def probe_shape(path: str):
+    """(nsub, npol, nchan, nbin) from the SUBINT header alone."""
+    with open(path, "rb") as fh:
+        primary = _read_header(fh)
+        if not primary or primary.get("SIMPLE") is not True:
+            raise ValueError("%s: not a FITS file" % path)
+        fh.seek(_data_bytes(primary) + (-_data_bytes(primary) % BLOCK), 1)
+        while True:
+            hdr = _read_header(fh)
+            if hdr is None:
+                raise ValueError("%s: no SUBINT table" % path)
+            if hdr.get("EXTNAME") == "SUBINT":
+                return int(hdr["NAXIS2"]), int(hdr["NPOL"]), int(hdr["NCHAN"]), int(hdr["NBIN"])
+            n = _data_bytes(hdr)
+            fh.seek(n + (-n % BLOCK), 1)
+
+
+def load(path: str, channels=None):
+    """Read a fold-mode PSRFITS archive.  channels = (c0, c1): only those
+    channels; the SUBINT table is memory-mapped, so the other channels' samples
+    are never read (channel-sharded cleaning)."""
     from .archive import Archive
     with open(path, "rb") as fh:
         primary = _read_header(fh)
@@ -234,26 +260,30 @@ def load(path: str):
                 raise ValueError("%s: no SUBINT table" % path)
             n = _data_bytes(hdr)
             if hdr.get("EXTNAME") == "SUBINT":
-                raw = fh.read(n)
+                table_offset = fh.tell()
                 break
             fh.seek(n + (-n % BLOCK), 1)
     dt, tdims = _columns(hdr)
     if dt.itemsize != int(hdr["NAXIS1"]):
         raise ValueError("%s: row size %d != NAXIS1 %d" % (path, dt.itemsize, hdr["NAXIS1"]))
     nsub = int(hdr["NAXIS2"])
-    rows = np.frombuffer(raw[:dt.itemsize * nsub], dtype=dt, count=nsub)
-    npol, nchan, nbin = int(hdr["NPOL"]), int(hdr["NCHAN"]), int(hdr["NBIN"])
-    q = np.asarray(rows["DATA"], np.int16).reshape(nsub, npol, nchan, nbin)
-    scl = np.asarray(rows["DAT_SCL"], np.float32).reshape(nsub, npol, nchan)
-    offs = np.asarray(rows["DAT_OFFS"], np.float32).reshape(nsub, npol, nchan)
-    weights = np.asarray(rows["DAT_WTS"], np.float32).reshape(nsub, nchan)
-    freqs = np.asarray(rows["DAT_FREQ"], np.float64).reshape(nsub, nchan)[0] if "DAT_FREQ" in dt.names \
-        else None
+    rows = np.memmap(path, dtype=dt, mode="r", offset=table_offset, shape=(nsub,))
+    npol, nchan_total, nbin = int(hdr["NPOL"]), int(hdr["NCHAN"]), int(hdr["NBIN"])
+    c0, c1 = (0, nchan_total) if channels is None else (int(channels[0]), int(channels[1]))
+    if not 0 <= c0 < c1 <= nchan_total:
+        raise ValueError("%s: channel range %s outside [0, %d)" % (path, (c0, c1), nchan_total))
+    nchan = c1 - c0
+    q = np.array(rows["DATA"].reshape(nsub, npol, nchan_total, nbin)[:, :, c0:c1], np.int16)
+    scl = np.array(rows["DAT_SCL"].reshape(nsub, npol, nchan_total)[:, :, c0:c1], np.float32)
+    offs = np.array(rows["DAT_OFFS"].reshape(nsub, npol, nchan_total)[:, :, c0:c1], np.float32)
+    weights = np.array(rows["DAT_WTS"].reshape(nsub, nchan_total)[:, c0:c1], np.float32)
+    freqs = np.array(rows["DAT_FREQ"].reshape(nsub, nchan_total)[0, c0:c1], np.float64) \
+        if "DAT_FREQ" in dt.names else None
     period = float(np.asarray(rows["PERIOD"]).reshape(-1)[0]) if "PERIOD" in dt.names else 1.0
     cfreq = float(primary.get("OBSFREQ", 1400.0))
     dm = float(hdr.get("DM", 0.0))
     if "IC_SHIFT" in dt.names:
-        shift = np.asarray(rows["IC_SHIFT"], np.int64).reshape(nsub, nchan)[0]
+        shift = np.array(rows["IC_SHIFT"].reshape(nsub, nchan_total)[0, c0:c1], np.int64)
     elif freqs is not None and dm != 0.0:
         delay = 4.148808e3 * dm * (freqs ** -2 - cfreq ** -2)
         shift = np.rint(delay / period * nbin).astype(np.int64) % nbin
@@ -261,11 +291,19 @@ def load(path: str):
         shift = np.zeros(nchan, np.int64)
     mjd0 = float(primary.get("STT_IMJD", 60000)) + (float(primary.get("STT_SMJD", 0))
                                                      + float(primary.get("STT_OFFS", 0.0))) / 86400.0
+    pol_type = str(hdr.get("POL_TYPE", "")).strip().upper()
+    state = POL_TYPE_STATE.get(pol_type) if pol_type else None
+    if state is not None and (state == "Intensity") != (npol == 1):
+        state = None          # inconsistent header: fall back on the npol default
+    del rows
     ar = Archive(decode(q, scl, offs), weights, shift, dedispersed=bool(hdr.get("IC_DEDSP", False)),
                  filename=path, source=str(primary.get("SRC_NAME", "J0000+0000")),
                  centre_frequency=cfreq, mjd_start=mjd0,
                  mjd_end=float(hdr.get("IC_MJDE", mjd0 + 0.01)),
-                 baseline_duty=float(hdr.get("IC_DUTY", 0.15)))
+                 baseline_duty=float(hdr.get("IC_DUTY", 0.15)), state=state)
+    if channels is not None:
+        ar._chan_range = (c0, c1)
+        ar._nchan_total = nchan_total
     ar._psrfits_q = (q, scl, offs)
     ar._format = "PSRFITS"
     ar._chan_freqs = freqs

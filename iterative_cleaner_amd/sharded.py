@@ -30,7 +30,7 @@ def _loop_kwargs(args):
     return dict(max_iter=args.get("max_iter", 5), chanthresh=args.get("chanthresh", 5.0),
                 subintthresh=args.get("subintthresh", 5.0),
                 pulse_region=args.get("pulse_region", (0, 0, 1)),
-                baseline_duty=args.get("baseline_duty", 0.15))
+                baseline_duty=args.get("baseline_duty", 0.15), fit_mode=args.get("fit_mode", 0))
 
 
 def clean_cube_local(cube, w0, shift, world, devices=None, want_details=False, fit_tail=None, **args):
@@ -104,7 +104,7 @@ def _merge(results, chans, shape2, want_details):
 
 
 def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, group=None,
-                    want_residual=False, **args):
+                    want_residual=False, fail_at=None, **args):
     """This rank's channel shard of one archive under torch.distributed.
     `cube_slice` etc. are the rank's channel range (``_native.shard_layout``);
     returns the merged full-archive dict on every rank (with want_residual, the
@@ -113,27 +113,68 @@ def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, gro
 
     from .dist import TorchComm
     nsub, nchan, nbin = global_shape
-    comm = TorchComm(device, group)
+    comm = TorchComm(device, group, fail_at=fail_at)
     world, rank = comm.world, comm.rank
     chans, _ = _native.shard_layout(nsub, nchan, world)
-    with _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm,
-                              device=_device_index(device), **_loop_kwargs(args)) as s:
-        if np.ndim(cube_slice) == 4:   # full-pol: pscrunched on the GPU
-            s.upload_pols(cube_slice, w0_slice, shift_slice)
-        else:
-            s.upload(cube_slice, w0_slice, shift_slice)
-        out = s.run()
-        res = s.residual() if want_residual and out["n_iter"] > 0 else None
+    try:
+        with _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm,
+                                  device=_device_index(device), **_loop_kwargs(args)) as s:
+            if np.ndim(cube_slice) == 4:   # full-pol: pscrunched on the GPU
+                s.upload_pols(cube_slice, w0_slice, shift_slice)
+            else:
+                s.upload(cube_slice, w0_slice, shift_slice)
+            out = s.run()
+            res = s.residual() if want_residual and out["n_iter"] > 0 else None
+    except _native.NativeError:
+        comm.abort()          # peers waiting in a collective with this rank must not block
+        raise
+    return _merge_dist(out, res, chans, (nsub, nchan, nbin), comm, group, want_residual)
+
+
+def _merge_dist(out, res, chans, shape, comm, group, want_residual):
+    """Every rank's (nsub, nchan_r) test / weights slices -> the full arrays on
+    every rank, and the residual slices -> the full cube on rank 0, through
+    tensor collectives (padded to the widest slice; RCCL on "nccl", host
+    tensors on "gloo").  The scalar loop results are checked for agreement."""
+    import torch
+    import torch.distributed as dist
+    nsub, nchan, nbin = shape
+    world, rank = comm.world, comm.rank
+    dev = comm.device if comm.backend != "gloo" else torch.device("cpu")
+    wmax = max(c1 - c0 for c0, c1 in chans)
+    nc = chans[rank][1] - chans[rank][0]
+    scalars = {k: out[k] for k in ("loops", "n_iter", "converged")}
+    scalars.update(changed=list(map(int, out["changed"])), nzero=list(map(int, out["nzero"])),
+                   bad_fits=list(map(int, out.get("bad_fits", []))))
     every = [None] * world
-    dist.all_gather_object(every, out, group=group)
-    merged = _merge(every, chans, (nsub, nchan), False)
+    dist.all_gather_object(every, scalars, group=group)
+    for r, sc in enumerate(every[1:], 1):
+        if sc != every[0]:
+            raise _native.NativeError("shard %d disagrees on the loop results: %s vs %s" % (r, sc, every[0]))
+    merged = dict(out)
+
+    def gather_cols(a, dtype, to_all=True):
+        t = torch.zeros((nsub, wmax) + a.shape[2:], dtype=dtype, device=dev)
+        t[:, :nc] = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        if to_all:
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t, group=group)
+        else:
+            parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+            dist.gather(t, parts, dst=0, group=group)
+            if rank != 0:
+                return None
+        full = np.empty((nsub, nchan) + a.shape[2:], dtype=t.cpu().numpy().dtype)
+        for (c0, c1), part in zip(chans, parts):
+            full[:, c0:c1] = part[:, :c1 - c0].cpu().numpy()
+        return full
+
+    merged["test"] = gather_cols(out["test"], torch.float64)
+    merged["weights"] = gather_cols(out["weights"], torch.float32)
     if want_residual:
-        parts = [None] * world if rank == 0 else None
-        dist.gather_object(res, parts, dst=0, group=group)
+        R = gather_cols(res if res is not None else np.zeros((nsub, nc, nbin), np.float32), torch.float32,
+                        to_all=False)
         if rank == 0 and merged["n_iter"] > 0:
-            R = np.empty((nsub, nchan, nbin), np.float32)
-            for (c0, c1), part in zip(chans, parts):
-                R[:, c0:c1] = part
             merged["residual"] = R
     return merged
 

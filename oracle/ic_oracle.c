@@ -244,7 +244,10 @@ int orc_lmdif1(int m, const float *T, const float *p, double *x_out, int *nfev_o
         if (fnorm != 0.0 && acnorm != 0.0) {
             double sum = 0.0;
             sum += r * (qtf / fnorm);
-            gnorm = dmax(gnorm, fabs(sum / acnorm));
+            /* scipy keeps gnorm = 0 when this term is NaN (non-finite profile):
+             * info 4 at once with x = 1 (tests/golden/leastsq_nonfinite.npz) */
+            double g = fabs(sum / acnorm);
+            if (g > gnorm) gnorm = g;
         }
         if (gnorm <= gtol) info = 4;
         if (info != 0) break;

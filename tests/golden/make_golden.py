@@ -405,6 +405,67 @@ def run_leastsq_cases(ic, out_dir=HERE):
     print("wrote %s (%d profiles)" % (fn, len(xs)))
 
 
+def leastsq_nonfinite_cases():
+    """Profiles outside the usual range: non-finite samples (NaN / +-Inf in the
+    profile or the template) and exact large multiples of the template, for
+    which scipy's leastsq returns status 8 (the reference then prints "Bad
+    status ..." and zeroes the residual, iterative_cleaner.py:284-286)."""
+    cases = []
+    rng = np.random.default_rng(4711)
+    for nbin in (64, 256, 1024):
+        phase = (np.arange(nbin) + 0.5) / nbin
+        pulse = np.exp(-0.5 * ((phase - 0.3) / 0.02) ** 2)
+        T = (pulse * 1.3e4).astype(np.float32)
+        noise = rng.standard_normal(nbin).astype(np.float32)
+        for kind in range(14):
+            t, p = T.copy(), noise.copy()
+            if kind == 0: p[5] = np.nan
+            if kind == 1: p[nbin // 3] = np.inf
+            if kind == 2: p[nbin // 2] = -np.inf
+            if kind == 3: p[:] = np.nan
+            if kind == 4: t[7] = np.nan
+            if kind == 5: t[nbin // 3] = np.inf
+            if kind == 6: p = (T * np.float32(1e12)).astype(np.float32)
+            if kind == 7: p = (T * np.float32(-4.1e11)).astype(np.float32)
+            if kind == 12: p = (T * np.float32(1e13)).astype(np.float32)
+            if kind == 13: p = (T * np.float32(1e11)).astype(np.float32)
+            if kind == 8: p = (T * np.float32(1e10)).astype(np.float32); p[3] += np.float32(1e-3)
+            if kind == 9: t = (pulse * 1.6e-11).astype(np.float32); p = (t * np.float32(6.8e10)).astype(np.float32)
+            if kind == 10: t = (pulse * 3.4e4).astype(np.float32); p = (t * np.float32(2.8e11)).astype(np.float32)
+            if kind == 11: p = np.full(nbin, np.float32(3e38)); p[::2] = np.float32(-3e38)
+            cases.append((t, p))
+    return cases
+
+
+def run_leastsq_nonfinite(ic, out_dir=HERE):
+    Ts, ps, xs, infos, resid, printed = [], [], [], [], [], []
+    for T, p in leastsq_nonfinite_cases():
+        rec = {}
+        orig = scipy.optimize.leastsq
+
+        def spy(func, x0, *a, **k):
+            res = orig(func, x0, *a, **k)
+            rec["x"], rec["info"] = float(np.asarray(res[0])[0]), int(res[1])
+            return res
+        scipy.optimize.leastsq = spy
+        buf = io.StringIO()
+        try:
+            with contextlib.redirect_stdout(buf), np.errstate(all="ignore"):
+                _, r = ic.remove_profile1d(p, 0, 0, T, [0, 0, 1])
+        finally:
+            scipy.optimize.leastsq = orig
+        Ts.append(T); ps.append(p); xs.append(rec["x"]); infos.append(rec["info"])
+        resid.append(np.asarray(r, dtype=np.float64))
+        printed.append(buf.getvalue())
+    arrays = {"x": np.array(xs), "info": np.array(infos, np.int32), "nbin": np.array([len(t) for t in Ts]),
+              "T": np.concatenate(Ts), "p": np.concatenate(ps), "resid": np.concatenate(resid),
+              "stdout": np.array(printed)}
+    fn = os.path.join(out_dir, "leastsq_nonfinite.npz")
+    np.savez_compressed(fn, **arrays)
+    import collections
+    print("wrote %s (%d profiles, statuses %s)" % (fn, len(xs), dict(collections.Counter(infos))))
+
+
 def run_pulse_region_case(ic, out_dir=HERE):
     """remove_profile1d with an active pulse region (K6: (factor, start, end))."""
     rng = np.random.default_rng(4242)
@@ -454,7 +515,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--skip-big", action="store_true")
-    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap (round-2 fixtures only)")
+    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite (round-2 fixtures only)")
     a = ap.parse_args()
     ic = import_reference()
     only = set(filter(None, a.only.split(",")))
@@ -465,6 +526,8 @@ def main():
             run_long_stats_cases(ic, a.out)
         if "zap" in only:
             run_zap_plot_case(ic, a.out)
+        if "nonfinite" in only:
+            run_leastsq_nonfinite(ic, a.out)
         return
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s12x48x128", 12, 48, 128, 3, 0.05, workdir=wd, out_dir=a.out)
@@ -487,6 +550,7 @@ def main():
     run_long_cases(ic, a.out)
     run_long_stats_cases(ic, a.out)
     run_zap_plot_case(ic, a.out)
+    run_leastsq_nonfinite(ic, a.out)
 
 
 def run_long_cases(ic, out_dir=HERE):

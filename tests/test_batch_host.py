@@ -52,3 +52,51 @@ def test_run_lanes_empty_and_error():
     sessions = [FakeSession(fail_on=7), FakeSession(fail_on=7)]
     with pytest.raises(RuntimeError, match="boom 7"):
         list(batch.run_lanes(sessions, [(k, None, None) for k in range(12)]))
+
+
+class SlowSession(FakeSession):
+    """Counts runs in flight (a run must never be in flight after the lanes end)."""
+
+    inflight = 0
+    guard = threading.Lock()
+
+    def run(self, fetch=True):
+        with SlowSession.guard:
+            SlowSession.inflight += 1
+        try:
+            time.sleep(0.02)
+            return super().run(fetch)
+        finally:
+            with SlowSession.guard:
+                SlowSession.inflight -= 1
+
+
+def test_run_lanes_early_close_joins_workers():
+    """The consumer stops after 3 results: closing the generator returns only
+    once every worker has left ic_run, and nothing runs afterwards."""
+    from iterative_cleaner_amd import batch
+    sessions = [SlowSession() for _ in range(3)]
+    items = [(k, None, None) for k in range(200)]
+    gen = batch.run_lanes(sessions, items)
+    got = [next(gen)["tag"] for _ in range(3)]
+    t0 = time.time()
+    gen.close()
+    assert time.time() - t0 < 5.0
+    assert SlowSession.inflight == 0
+    ran = sum(len(s.ran) for s in sessions)
+    time.sleep(0.1)
+    assert sum(len(s.ran) for s in sessions) == ran < 200
+    assert got == [0, 1, 2]
+
+
+def test_run_lanes_error_stops_the_other_lanes():
+    from iterative_cleaner_amd import batch
+    sessions = [SlowSession(fail_on=5), SlowSession(fail_on=5), SlowSession(fail_on=5)]
+    items = [(k, None, None) for k in range(300)]
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="boom 5"):
+        for _ in batch.run_lanes(sessions, items):
+            pass
+    assert time.time() - t0 < 5.0
+    assert SlowSession.inflight == 0
+    assert sum(len(s.ran) for s in sessions) < 300

@@ -26,6 +26,24 @@ def test_leastsq_cases_bit_exact(oracle_lib):
         off += n
 
 
+def test_leastsq_nonfinite_cases_bit_exact(oracle_lib):
+    """NaN / Inf profiles and templates (scipy keeps x = 1, status 4) and exact
+    large multiples of the template (status 8: the reference prints "Bad
+    status" and zeroes the residual), against the reference's outputs."""
+    z = np.load(os.path.join(GOLDEN, "leastsq_nonfinite.npz"))
+    assert 8 in set(z["info"].tolist())
+    off = 0
+    for k, n in enumerate(z["nbin"]):
+        T, p = z["T"][off:off + n], z["p"][off:off + n]
+        x, info, _ = oracle_lib.lmdif1(T, p)
+        assert np.float64(x).tobytes() == np.float64(z["x"][k]).tobytes(), (k, x, z["x"][k])
+        assert info == z["info"][k], (k, info, z["info"][k])
+        assert (str(z["stdout"][k]) != "") == (info not in (1, 2, 3, 4))
+        _, _, R = oracle_lib.fit_residual(p[None], T)
+        assert bits_equal(R[0], z["resid"][off:off + n].astype(np.float32)), k
+        off += n
+
+
 def test_pulse_region_cases(oracle_lib):
     z = np.load(os.path.join(GOLDEN, "pulse_region_cases.npz"))
     from iterative_cleaner_amd._native import normalise_pulse_region

@@ -32,3 +32,27 @@ def test_cli_psrfits_in_out(tmp_path, monkeypatch, capsys, extra, oracle_lib):
         assert np.array_equal(res.get_data(), dec)              # samples untouched, quantisation kept
     if "-u" in extra:
         assert any("_residual_" in p.name for p in tmp_path.iterdir())
+
+
+def test_cli_stokes_archive_cleans_total_intensity(tmp_path, monkeypatch, capsys, oracle_lib):
+    """An IQUV (Stokes) PSRFITS archive: psrchive's pscrunch keeps I = pol 0, so
+    the loop must clean pol 0 (not pol0 + pol1, the AA+BB rule)."""
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import cleaner, synth
+    monkeypatch.chdir(tmp_path)
+    data, w, shift = synth.make_cube(12, 64, 128, 52, 0.2, npol=4)
+    rng = np.random.default_rng(52)
+    data[:, 1] = rng.standard_normal(data[:, 1].shape).astype(np.float32)     # Q: noise ...
+    data[rng.integers(0, 12, 20), 1, rng.integers(0, 64, 20), :] += 40.0     # ... with Q-only RFI
+    ica.Archive(data, w, shift, filename="iquv.sf", state="Stokes").unload("iquv.sf")
+    src = ica.Archive_load("iquv.sf")
+    assert src.get_state() == "Stokes"
+    dec = src.get_data()
+    ref = oracle_lib.clean_loop(np.ascontiguousarray(dec[:, 0]), src.get_weights(), src.get_dm_shift())
+    wrong = oracle_lib.clean_loop((dec[:, 0] + dec[:, 1]).astype(np.float32), src.get_weights(),
+                                  src.get_dm_shift())
+    assert not bits_equal(ref["weights"], wrong["weights"])     # the rule matters on this archive
+    cleaner.main(cleaner.parse_arguments(["-l", "-q", "iquv.sf"]))
+    res = ica.Archive_load("iquv_cleaned.ar")
+    assert res.get_state() == "Stokes" and res.get_npol() == 4
+    assert bits_equal(res.get_weights(), ref["weights"])
