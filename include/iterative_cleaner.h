@@ -54,6 +54,12 @@ typedef struct {
     int32_t pr_start, pr_end;  /* slice(int(pr[1]), int(pr[2])).indices(nbin) */
     double baseline_duty;      /* archive stand-in remove_baseline duty (0.15) */
     int32_t fit_mode;          /* IC_FIT_EXACT (default) or IC_FIT_CLOSED       */
+    int32_t data_f64;          /* psrchive get_data dtype: 0 = f32
+                                  (default), 1 = f64: apply_weights and the masked
+                                  statistics then run in f64 (iterative_cleaner.py:
+                                  111-112, 206-209): X = f64(R) * f64(w), f64 mean
+                                  sum and ptp, ptp scaled in f64.  The samples must
+                                  still be f32 values (the archive's amplitudes).  */
 } ic_params;
 
 /* ic_params.fit_mode.
@@ -138,6 +144,9 @@ int ic_get_template(void *session, float *T);
 int ic_get_fit(void *session, double *amp, int32_t *info);
 int ic_get_diagnostics(void *session, double *std_o, double *mean_o, float *ptp_o,
                        double *fftmax_o);
+/* The same with ptp in f64 (the data_f64 loop's ptp is an f64 value). */
+int ic_get_diagnostics_f64(void *session, double *std_o, double *mean_o, double *ptp_o,
+                           double *fftmax_o);
 
 /* Per-launch timing of the last ic_run (HIP events on the session stream):
  * fills up to n entries of {kernel id, milliseconds summed over the run,

@@ -23,7 +23,7 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_shard_layout", "ic_session_create_shard", "ic_group_create", "ic_group_destroy",
            "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free",
            "ic_upload_pols", "ic_comprehensive_stats", "ic_get_bad_fits",
-           "ic_fit_profiles")
+           "ic_fit_profiles", "ic_get_diagnostics_f64")
 
 FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)
 FIT_CLOSED = 1   # IC_FIT_CLOSED: closed-form amplitude fused with the diagnostics (fast mode)
@@ -38,7 +38,7 @@ class Params(C.Structure):
                 ("max_iter", C.c_int32), ("chanthresh", C.c_double),
                 ("subintthresh", C.c_double), ("pr_on", C.c_int32), ("pr_factor", C.c_double),
                 ("pr_start", C.c_int32), ("pr_end", C.c_int32), ("baseline_duty", C.c_double),
-                ("fit_mode", C.c_int32)]
+                ("fit_mode", C.c_int32), ("data_f64", C.c_int32)]
 
 
 class RunStats(C.Structure):
@@ -116,6 +116,7 @@ def load_library(path: str = LIB_PATH):
     lib.ic_get_template.argtypes = [vp, vp]
     lib.ic_get_fit.argtypes = [vp, vp, vp]
     lib.ic_get_diagnostics.argtypes = [vp, vp, vp, vp, vp]
+    lib.ic_get_diagnostics_f64.argtypes = [vp, vp, vp, vp, vp]
     lib.ic_get_kernel_times.argtypes = [vp, C.POINTER(KernelTime), C.c_int]
     lib.ic_set_timing.argtypes = [vp, C.c_int]
     lib.ic_get_run_stats.argtypes = [vp, C.POINTER(RunStats)]
@@ -170,14 +171,16 @@ class GpuSession:
     """One cleaning session on one GPU (wraps ic_session_*)."""
 
     def __init__(self, nsub, nchan, nbin, max_iter=5, chanthresh=5.0, subintthresh=5.0,
-                 pulse_region=(0, 0, 1), baseline_duty=0.15, device=0, fit_mode=FIT_EXACT):
+                 pulse_region=(0, 0, 1), baseline_duty=0.15, device=0, fit_mode=FIT_EXACT, data_f64=False):
         self.lib = load_library()
         self.shape = (int(nsub), int(nchan), int(nbin))
         self.max_iter = int(max_iter)
         self.fit_mode = int(fit_mode)
         on, fac, a, b = normalise_pulse_region(list(pulse_region), int(nbin))
         self.params = Params(int(nsub), int(nchan), int(nbin), int(max_iter), float(chanthresh),
-                             float(subintthresh), on, fac, a, b, float(baseline_duty), self.fit_mode)
+                             float(subintthresh), on, fac, a, b, float(baseline_duty), self.fit_mode,
+                             1 if data_f64 else 0)
+        self.data_f64 = bool(data_f64)
         h = C.c_void_p()
         rc = self._create(int(device), h)
         if rc != 0:
@@ -284,11 +287,18 @@ class GpuSession:
         return amp, info
 
     def diagnostics(self):
+        """(std, mean, ptp, fftmax) of the last iteration; ptp is f32 for f32 data
+        (numpy.ma's dtype), f64 with data_f64."""
         nsub, nchan, _ = self.shape
         sd, mn, ff = (np.empty((nsub, nchan), np.float64) for _ in range(3))
-        pt = np.empty((nsub, nchan), np.float32)
-        self._check(self.lib.ic_get_diagnostics(self.h, _ptr(sd), _ptr(mn), _ptr(pt), _ptr(ff)),
-                    "ic_get_diagnostics")
+        if self.data_f64:
+            pt = np.empty((nsub, nchan), np.float64)
+            self._check(self.lib.ic_get_diagnostics_f64(self.h, _ptr(sd), _ptr(mn), _ptr(pt), _ptr(ff)),
+                        "ic_get_diagnostics_f64")
+        else:
+            pt = np.empty((nsub, nchan), np.float32)
+            self._check(self.lib.ic_get_diagnostics(self.h, _ptr(sd), _ptr(mn), _ptr(pt), _ptr(ff)),
+                        "ic_get_diagnostics")
         return sd, mn, pt, ff
 
     def set_timing(self, on: bool):

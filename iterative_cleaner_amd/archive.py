@@ -8,7 +8,8 @@ path must follow.  Every floating-point reduction below has a fixed, written
 order so that the HIP kernels can reproduce it bit-for-bit:
 
 * samples and weights are float32 (``get_data``/``get_weights`` return f32
-  copies);
+  copies; ``get_data_dtype = np.float64`` models a psrchive build whose
+  get_data returns f64 copies of the f32 amplitudes, SURVEY.md §8(b));
 * ``get_state``: psrchive's polarisation state names - "Intensity" (one
   polarisation), "PPQQ" (AA, BB), "Coherence" (AA, BB, CR, CI) or "Stokes"
   (I, Q, U, V);
@@ -179,8 +180,10 @@ class Archive:
     def get_nbin(self): return self._data.shape[3]
 
     # ---------------------------------------------------------------- access
+    get_data_dtype = np.float32
+
     def get_data(self) -> np.ndarray:
-        return self._data.copy()
+        return self._data.astype(self.get_data_dtype)
 
     def get_weights(self) -> np.ndarray:
         return self._weights.copy()

@@ -147,8 +147,20 @@ def _loop_input(ar) -> np.ndarray:
     the GPU pscrunches (ic_upload_pols: total intensity f32(pol0 + pol1))."""
     data = ar.get_data()
     if data.shape[1] == 1 or _state(ar) == "Stokes":
-        return np.ascontiguousarray(data[:, 0], dtype=np.float32)
-    return np.ascontiguousarray(data, dtype=np.float32)
+        data = data[:, 0]
+    cube = np.ascontiguousarray(data, dtype=np.float32)
+    if data.dtype != np.float32 and not np.array_equal(cube, data, equal_nan=True):
+        raise ValueError("get_data() returned %s values that are not f32 amplitudes" % data.dtype)
+    return cube
+
+
+def _data_f64(ar) -> bool:
+    """True when the archive binding's get_data returns f64 (a psrchive build;
+    the masked statistics then run in f64: ic_params.data_f64)."""
+    dt = getattr(ar, "get_data_dtype", None)
+    if dt is not None:
+        return np.dtype(dt) == np.float64
+    return ar.get_data().dtype == np.float64
 
 
 def _device() -> int:
@@ -158,7 +170,8 @@ def _device() -> int:
     return 0
 
 
-def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15, nchan_total=None):
+def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15, nchan_total=None,
+             data_f64=False):
     """Run the GPU loop on a (nsub, nchan, nbin) f32 cube, or on full-polarisation
     data (nsub, npol, nchan, nbin) that the GPU pscrunches; returns the ic_run dict
     (+ ``residual`` when requested).  Under channel sharding (dist.channel_sharding)
@@ -185,12 +198,12 @@ def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_d
             np.ascontiguousarray(cube), np.ascontiguousarray(w0), np.asarray(shift), (nsub, nchan_total, nbin),
             dev, want_residual=want_residual,
             max_iter=args.max_iter, chanthresh=args.chanthresh, subintthresh=args.subintthresh,
-            pulse_region=args.pulse_region, baseline_duty=baseline_duty)
+            pulse_region=args.pulse_region, baseline_duty=baseline_duty, data_f64=data_f64)
     if nchan_total is not None and nchan_total != nchan:
         raise ValueError("a channel slice of an archive needs channel sharding")
     with _native.GpuSession(nsub, nchan, nbin, args.max_iter, args.chanthresh, args.subintthresh,
                             args.pulse_region, baseline_duty,
-                            device=_device() if device is None else device) as s:
+                            device=_device() if device is None else device, data_f64=data_f64) as s:
         if pols:
             s.upload_pols(cube, w0, shift)
         else:
@@ -279,7 +292,7 @@ def clean(ar, args, arch):
     shift = _dm_shift(ar)
     duty = ar.get_baseline_duty() if hasattr(ar, "get_baseline_duty") else 0.15
     out = run_loop(cube, orig_weights, shift, args, want_residual=args.unload_res, baseline_duty=duty,
-                   nchan_total=nchan_total)
+                   nchan_total=nchan_total, data_f64=_data_f64(ar))
     del cube
 
     x = 0

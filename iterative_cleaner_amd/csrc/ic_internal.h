@@ -29,7 +29,7 @@ struct ShardGeom {
     int32_t row0[kMaxShards + 1];
 };
 
-// bytes of one exchange block of n elements of esz bytes (28 = std+mean+fft+ptp),
+// bytes of one exchange block of n elements of esz bytes (32 = std+mean+fft+ptp),
 // padded so that every block, and the f64 fields inside it, start 8-aligned
 __host__ __device__ inline size_t shard_block_bytes(size_t n, size_t esz) { return ((n * esz + 7) / 8) * 8; }
 
@@ -79,7 +79,8 @@ struct LineStatsArgs {
     int nsub, nchan;
     const uint8_t *valid;
     const double *std_d, *mean_d, *fft_d;
-    const float *ptp_d;
+    const double *ptp_d;            // ptp (f32 values unless data_f64)
+    int ptp_f32;                    // 1: ptp lines use f32 arithmetic (numpy.ma on f32 data)
     double *col_med, *col_mad;      // [4][nchan]
     double *row_med, *row_mad;      // [4][nsub]
 };
@@ -117,14 +118,14 @@ hipError_t launch_unpack_windows(hipStream_t st, const ShardGeom &g, int blk, co
                                  int32_t *flags);
 hipError_t launch_unpack_fscrunch(hipStream_t st, const ShardGeom &g, int rows_pad, long blk, int nbin,
                                   const float *recv, float *F, float *wf);
-// diagnostics rows -> per-destination blocks [std|mean|fft (f64)|ptp (f32)] x rows_d x nchan_loc
+// diagnostics rows -> per-destination blocks [std|mean|fft|ptp (f64)] x rows_d x nchan_loc
 // (valid == true: the single u8 field `valid` instead)
 hipError_t launch_pack_rows(hipStream_t st, const ShardGeom &g, int nchan_loc, const double *std_d,
-                            const double *mean_d, const double *fft_d, const float *ptp_d, const uint8_t *valid,
+                            const double *mean_d, const double *fft_d, const double *ptp_d, const uint8_t *valid,
                             unsigned char *send);
 // per-source blocks -> owned rows [rows_own][nchan_g] of each field
 hipError_t launch_assemble_rows(hipStream_t st, const ShardGeom &g, const unsigned char *recv, double *std_r,
-                                double *mean_r, double *fft_r, float *ptp_r, uint8_t *valid_r);
+                                double *mean_r, double *fft_r, double *ptp_r, uint8_t *valid_r);
 // gathered [world][8 * rows_pad] (rank p: med [4][rows_p], mad [4][rows_p]) -> row_med/row_mad [4][nsub]
 hipError_t launch_unpack_rowstats(hipStream_t st, const ShardGeom &g, int rows_pad, const double *recv,
                                   double *row_med, double *row_mad);
@@ -169,8 +170,8 @@ struct DiagArgs {
     int pr_on;
     double pr_factor;
     int pr_start, pr_end;
-    double *std_o, *mean_o, *fft_o;
-    float *ptp_o;
+    double *std_o, *mean_o, *fft_o, *ptp_o;
+    int data_f64;      // psrchive get_data returns f64: X = f64(R) * f64(w), f64 mean and ptp
 };
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a);
 // dynamic LDS the generic k_diag needs for one wave (0 for the power-of-two kernels)
@@ -183,7 +184,7 @@ hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which = 
 // may be null), [3+h] new weights != history h (iterative_cleaner.py:127-141)
 hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const int32_t *info,
                           const float *w0,
-                          const double *std_d, const double *mean_d, const float *ptp_d,
+                          const double *std_d, const double *mean_d, const double *ptp_d, int ptp_f32,
                           const double *fft_d, const double *col_med, const double *col_mad,
                           const double *row_med, const double *row_mad, double chanthresh,
                           double subintthresh, double *test, float *W, float *hist, int iter,

@@ -27,6 +27,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ic_internal.h"
 
 namespace icgpu {
@@ -101,6 +103,7 @@ struct OpMaxF {
 };
 struct OpMinF {
     __device__ __forceinline__ float operator()(float a, float b) const { return fminf(a, b); }
+    __device__ __forceinline__ double operator()(double a, double b) const { return fmin(a, b); }
 };
 struct OpOr {
     __device__ __forceinline__ int operator()(int a, int b) const { return a | b; }
@@ -1607,10 +1610,11 @@ __host__ __device__ inline DiagLayout diag_layout(int n, int nleaf, int nops)
     L.ntw = pow2 ? n / 2 : n;
     L.cw_off = 0;                                            // buffer A: n/2 complex
     const size_t cwb = (size_t)(pow2 ? n / 2 : 1) * 16;
-    L.x_off = cwb;                                           // buffer B (n/2 complex) aliases X (n f32)
-    const size_t xb = ((size_t)n * 4 + 15) & ~(size_t)15;
+    L.x_off = cwb;                                           // buffer B (n/2 complex) aliases X (n f64)
+    const size_t xb = ((size_t)n * 8 + 15) & ~(size_t)15;
+    const size_t pb = ((size_t)n * 4 + 15) & ~(size_t)15;
     L.p_off = L.x_off + (pow2 ? (cwb > xb ? cwb : xb) : xb);  // DIAG_CLOSED: the fit-cube row
-    L.scr_off = L.p_off + xb;
+    L.scr_off = L.p_off + pb;
     L.per_wave = L.scr_off + (size_t)(nleaf * 9 + nops + 8) * 8;
     L.per_wave = (L.per_wave + 15) & ~(size_t)15;
     return L;
@@ -1635,7 +1639,7 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
     __syncthreads();
     unsigned char *wb = smem + (size_t)lay.ntw * 16 + (size_t)wave * lay.per_wave;
     double2 *cw = (double2 *)(wb + lay.cw_off);
-    float *X = (float *)(wb + lay.x_off);
+    double *X = (double *)(wb + lay.x_off);   // f32 values unless data_f64
     float *Pr = (float *)(wb + lay.p_off);
     double *scr = (double *)(wb + lay.scr_off);
     const bool pow2 = (n & (n - 1)) == 0 && n >= 4;
@@ -1681,6 +1685,7 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
         }
         const bool ok = stt >= 1 && stt <= 4;
         // residual -> X (dispersed frame): X[j] = f32(f32(r[i]) * w), j = (i + sh) mod n
+        // (f64(f32(r[i])) * f64(w) for f64 data)
         for (int i = lane; i < n; i += 64) {
             float R = 0.0f;
             if (mode == DIAG_STATS) {
@@ -1693,14 +1698,16 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
             }
             int j = i + sh;
             if (j >= n) j -= n;
-            X[j] = R * w;
+            X[j] = a.data_f64 ? (double)R * (double)w : (double)(R * w);
         }
         wave_sync();
-        double mean = 0.0, sd = 0.0;
-        float ptp = 1e20f;
+        double mean = 0.0, sd = 0.0, ptp = a.data_f64 ? 1e20 : (double)1e20f;   // numpy.ma fill value
         if (valid) {
-            const float s32 = wave_pairwise<float>(pl, [&](int q) { return X[q]; }, (float *)scr, lane);
-            mean = (double)s32 / (double)n;
+            if (a.data_f64)
+                mean = wave_pairwise<double>(pl, [&](int q) { return X[q]; }, scr, lane) / (double)n;
+            else
+                mean = (double)wave_pairwise<float>(pl, [&](int q) { return (float)X[q]; }, (float *)scr, lane) /
+                       (double)n;
             const double mu = mean;
             const double ss = wave_pairwise<double>(
                 pl,
@@ -1710,18 +1717,19 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
                 },
                 scr, lane);
             sd = sqrt(ss / (double)n);
-            float mx = -INFINITY, mn = INFINITY;
+            double mx = -INFINITY, mn = INFINITY;
             int nan = 0;
             for (int q = lane; q < n; q += 64) {
-                const float v = X[q];
+                const double v = X[q];
                 if (isnan(v)) nan = 1;
-                mx = fmaxf(mx, v);
-                mn = fminf(mn, v);
+                mx = fmax(mx, v);
+                mn = fmin(mn, v);
             }
             mx = wave_tree<64>(mx, OpMaxF());
             mn = wave_tree<64>(mn, OpMinF());
             nan = wave_tree<64>(nan, OpOr());
-            ptp = nan ? NAN : (mx - mn);
+            // max - min in the data dtype (exact widening of f32 values)
+            ptp = nan ? (double)NAN : (a.data_f64 ? mx - mn : (double)((float)mx - (float)mn));
         }
         // fftmax: max_k |rfft(v)_k|, v = f64(X) - mean (valid) or f64(X) (invalid)
         const double mu = valid ? mean : 0.0;
@@ -1802,7 +1810,7 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
         if (lane == 0) {
             a.std_o[k] = valid ? sd : 0.0;
             a.mean_o[k] = valid ? mean : 0.0;
-            a.ptp_o[k] = valid ? ptp : 1e20f;
+            a.ptp_o[k] = ptp;
             a.fft_o[k] = nanf ? NAN : best;
         }
     }
@@ -1830,7 +1838,7 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
 //                fit cube row p = f32(ded - base0) formed from the raw cube),
 //                then the same residual; writes amp / info
 //   DIAG_STATS   comprehensive_stats alone (ic.py:181-226): X = f32(row * w)
-template <int N>
+template <int N, bool D64 = false>
 struct P2 {
     static constexpr int WPP = N >= 2048 ? N / 1024 : 1;   // waves per profile
     static constexpr int TPP = 64 * WPP;                    // threads per profile
@@ -1844,7 +1852,7 @@ struct P2 {
     static constexpr int WACT = ACT < 64 ? ACT : 64;        // ... per wave
     static constexpr int NPT = N / TPP;                     // samples per thread
     static constexpr int XPAD = N + 8 * NL;
-    static constexpr int XBYTES = ((XPAD * 4 + 15) / 16) * 16;
+    static constexpr int XBYTES = ((XPAD * (D64 ? 8 : 4) + 15) / 16) * 16;   // X: f32, or f64 (data_f64)
     static constexpr int CBYTES = M * 16;   // complex points at cidx(q)
     static constexpr int WORK_BYTES = XBYTES > CBYTES ? XBYTES : CBYTES;
     static constexpr int RED_BYTES = WPP > 1 ? 512 : 0;     // cross-wave partials
@@ -1919,8 +1927,8 @@ __device__ __forceinline__ T chain_total(const T (&cs)[P2<N>::CPL], T *red, int 
 // stw: this stage's twiddles w^(r k), w = exp(-2 pi i/(R NS)), as [k][r-1]
 // (host-built in long double; no recurrences).  FIRST: the input is the real
 // signal X (f32, padded addresses) minus mu, read as complex pairs.
-template <int R, int NS, bool FIRST, int M, int TPP>
-__device__ __forceinline__ void p2_stage(double2 *C, const float *X, double mu, const double2 *stw, int t)
+template <int R, int NS, bool FIRST, int M, int TPP, typename XT>
+__device__ __forceinline__ void p2_stage(double2 *C, const XT *X, double mu, const double2 *stw, int t)
 {
     constexpr int NB = M / R;
     constexpr int BPL = (NB + TPP - 1) / TPP;
@@ -1933,8 +1941,13 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, double mu, 
             for (int r = 0; r < R; ++r) {
                 const int q = b + r * NB;
                 if (FIRST) {
-                    const float2 xv = *(const float2 *)(X + xaddr(2 * q));
-                    v[u][r] = make_double2((double)xv.x - mu, (double)xv.y - mu);
+                    if constexpr (sizeof(XT) == 8) {
+                        const double2 xv = *(const double2 *)(X + xaddr(2 * q));
+                        v[u][r] = make_double2(xv.x - mu, xv.y - mu);
+                    } else {
+                        const float2 xv = *(const float2 *)(X + xaddr(2 * q));
+                        v[u][r] = make_double2((double)xv.x - mu, (double)xv.y - mu);
+                    }
                 } else {
                     v[u][r] = C[cidx(q)];
                 }
@@ -1963,15 +1976,15 @@ __device__ __forceinline__ void p2_stage(double2 *C, const float *X, double mu, 
 
 // the whole N/2-point FFT as a compile-time chain of stages (radix 8 while >= 3
 // levels remain, then 4 or 2); OFF = offset of the next stage table in tw
-template <int M, int TPP, int LG, int DONE, int NS, int OFF>
-__device__ __forceinline__ void p2_fft(double2 *C, const float *X, double mu, const double2 *tw, int t)
+template <int M, int TPP, int LG, int DONE, int NS, int OFF, typename XT>
+__device__ __forceinline__ void p2_fft(double2 *C, const XT *X, double mu, const double2 *tw, int t)
 {
     if constexpr (DONE < LG) {
         constexpr int REM = LG - DONE;
         constexpr int R = REM >= 3 ? 8 : (REM == 2 ? 4 : 2);
         constexpr int LR = R == 8 ? 3 : (R == 4 ? 2 : 1);
-        p2_stage<R, NS, DONE == 0, M, TPP>(C, X, mu, tw + OFF, t);
-        p2_fft<M, TPP, LG, DONE + LR, NS * R, (NS > 1 ? OFF + NS * (R - 1) : OFF)>(C, X, mu, tw, t);
+        p2_stage<R, NS, DONE == 0, M, TPP, XT>(C, X, mu, tw + OFF, t);
+        p2_fft<M, TPP, LG, DONE + LR, NS * R, (NS > 1 ? OFF + NS * (R - 1) : OFF), XT>(C, X, mu, tw, t);
     }
 }
 
@@ -1991,10 +2004,14 @@ __device__ __forceinline__ void p2_fft(double2 *C, const float *X, double mu, co
 template <int N>
 constexpr int p2_min_waves() { return N >= 2048 ? 4 : (N == 1024 ? IC_P2_MINW_1024 : 1); }
 
-template <int N, int MODE>
+// D64 (data_f64): psrchive's get_data returns f64, so apply_weights and the
+// masked statistics run in f64 (iterative_cleaner.py:111-112, :206-209): X =
+// f64(R) * f64(w), the mean's pairwise sum and ptp in f64.
+template <int N, int MODE, bool D64>
 __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) void k_diag_p2(DiagArgs a)
 {
-    using C = P2<N>;
+    using C = P2<N, D64>;
+    using XT = typename std::conditional<D64, double, float>::type;
     constexpr int WPP = C::WPP, TPP = C::TPP, NPT = C::NPT;
     // one-wave groups keep the template and the next row in registers; the
     // multi-wave groups (N >= 2048) read both when needed and rely on occupancy
@@ -2015,7 +2032,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         __syncthreads();
     }
     unsigned char *gb = smem + (size_t)C::TW_LDS * 16 + (size_t)group * C::GROUP_BYTES;
-    float *X = (float *)gb;
+    XT *X = (XT *)gb;
     double2 *Cb = (double2 *)gb;   // aliases X after the first FFT stage has read it
     double *red = (double *)(gb + C::WORK_BYTES);   // 64 slots of 8 B (WPP > 1)
     const unsigned P = (unsigned)a.nsub * (unsigned)a.nchan;
@@ -2074,7 +2091,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
 #pragma unroll
             for (int u = 0; u < NPT; ++u) {
                 const int j = t + TPP * u;
-                X[xaddr((j - sh) & (N - 1))] = pv[u] - bk;
+                X[xaddr((j - sh) & (N - 1))] = (XT)(pv[u] - bk);
             }
             gsync<WPP>();
             double cs[C::CPL];
@@ -2098,7 +2115,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             x = TT != 0.0 ? dot / TT : 0.0;
             st = isfinite(x) ? 1 : 5;
 #pragma unroll
-            for (int u = 0; u < NPT; ++u) pv[u] = X[xaddr(t + TPP * u)];
+            for (int u = 0; u < NPT; ++u) pv[u] = (float)X[xaddr(t + TPP * u)];
             if (t == 0) {
                 a.amp[k] = x;
                 a.info[k] = st;
@@ -2107,9 +2124,14 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         }
         const bool ok = st >= 1 && st <= 4;
         // residual -> X (dispersed frame, padded addresses)
+        // X = apply_weights(R, w0): f32(R * w), or f64(R) * f64(w) for f64 data
+        auto weigh = [&](float R) -> XT {
+            if constexpr (D64) return (double)R * (double)w;
+            else return R * w;
+        };
         if (mode == DIAG_STATS) {
 #pragma unroll
-            for (int u = 0; u < NPT; ++u) X[xaddr(t + TPP * u)] = pv[u] * w;
+            for (int u = 0; u < NPT; ++u) X[xaddr(t + TPP * u)] = weigh(pv[u]);
         } else if (a.pr_on) {
 #pragma unroll
             for (int u = 0; u < NPT; ++u) {
@@ -2118,7 +2140,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
                 double e = uu - (double)pv[u];
                 if (i >= a.pr_start && i < a.pr_end) e = e * a.pr_factor;
                 const float R = ok ? (float)e : 0.0f;
-                X[xaddr((i + sh) & (N - 1))] = R * w;
+                X[xaddr((i + sh) & (N - 1))] = weigh(R);
             }
         } else {
 #pragma unroll
@@ -2127,7 +2149,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
                 const double uu = x * (TREG ? tv[u] : T[i]);
                 const double e = uu - (double)pv[u];
                 const float R = ok ? (float)e : 0.0f;
-                X[xaddr((i + sh) & (N - 1))] = R * w;
+                X[xaddr((i + sh) & (N - 1))] = weigh(R);
             }
         }
         if (k + stride < P) {
@@ -2146,29 +2168,29 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             nsh = mode == DIAG_STATS ? 0 : a.shift[kn % (unsigned)nchan];
         }
         gsync<WPP>();
-        double mean = 0.0, sd = 0.0, fftv = 0.0;
-        float ptp = 1e20f;
+        // masked ptp data is numpy.ma's fill value of the dtype: 1e20 (f64) / f32(1e20)
+        double mean = 0.0, sd = 0.0, fftv = 0.0, ptp = D64 ? 1e20 : (double)1e20f;
         if (valid) {
             // chain values -> registers
-            float v[C::CPL][C::CL];
+            XT v[C::CPL][C::CL];
             const bool act = t < C::ACT;
 #pragma unroll
             for (int sl = 0; sl < C::CPL; ++sl) {
                 const int ch = t + TPP * sl;
                 const int base = (ch >> 3) * C::LEAF + (ch & 7);
 #pragma unroll
-                for (int q = 0; q < C::CL; ++q) v[sl][q] = act ? X[xaddr(base + 8 * q)] : 0.0f;
+                for (int q = 0; q < C::CL; ++q) v[sl][q] = act ? X[xaddr(base + 8 * q)] : (XT)0;
             }
-            // mean: f32 pairwise sum
-            float fs[C::CPL];
+            // mean: pairwise sum in the data dtype (f32, or f64 for f64 data)
+            XT fs[C::CPL];
 #pragma unroll
             for (int sl = 0; sl < C::CPL; ++sl) {
-                float r = v[sl][0];
+                XT r = v[sl][0];
 #pragma unroll
                 for (int q = 1; q < C::CL; ++q) r = r + v[sl][q];
                 fs[sl] = r;
             }
-            const float s32 = 0.0f + chain_total<N, float>(fs, (float *)(red + 16), wave, lane);
+            const XT s32 = (XT)0 + chain_total<N, XT>(fs, (XT *)(red + 16), wave, lane);
             mean = (double)s32 / (double)N;
             // var: f64 pairwise sum of (f64(X) - mean)^2
             double ds[C::CPL];
@@ -2186,26 +2208,26 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             }
             const double ss = 0.0 + chain_total<N, double>(ds, red + 24, wave, lane);
             sd = sqrt(ss / (double)N);
-            // ptp (NaN-propagating)
-            float mx = -INFINITY, mn = INFINITY;
+            // ptp (NaN-propagating), in the data dtype
+            XT mx = -INFINITY, mn = INFINITY;
             int nan = 0;
             if (act) {
 #pragma unroll
                 for (int sl = 0; sl < C::CPL; ++sl)
 #pragma unroll
                     for (int q = 0; q < C::CL; ++q) {
-                        const float tq = v[sl][q];
+                        const XT tq = v[sl][q];
                         nan |= isnan(tq);
-                        mx = fmaxf(mx, tq);
-                        mn = fminf(mn, tq);
+                        mx = OpMaxF()(mx, tq);
+                        mn = OpMinF()(mn, tq);
                     }
             }
-            mx = group_tree<WPP, 64>(mx, OpMaxF(), (float *)(red + 32), wave, lane);
-            mn = group_tree<WPP, 64>(mn, OpMinF(), (float *)(red + 36), wave, lane);
+            mx = group_tree<WPP, 64>(mx, OpMaxF(), (XT *)(red + 32), wave, lane);
+            mn = group_tree<WPP, 64>(mn, OpMinF(), (XT *)(red + 36), wave, lane);
             nan = group_tree<WPP, 64>(nan, OpOr(), (int *)(red + 40), wave, lane);
-            ptp = nan ? NAN : (mx - mn);
+            ptp = nan ? (double)NAN : (double)(XT)(mx - mn);
             // rFFT of f64(X) - mean: N/2-point complex Stockham, in place
-            p2_fft<C::M, TPP, C::LG, 0, 1, C::M>(Cb, X, mean, tw, t);
+            p2_fft<C::M, TPP, C::LG, 0, 1, C::M, XT>(Cb, X, mean, tw, t);
             // X_k = E_k + w^k O_k, computed as 2 X_k (the 1/2 factors are exact
             // powers of two, applied once to the maximum)
             // k = 0 .. M-1 on all threads; the Nyquist term k = M (w = -1, Z_M = Z_0)
@@ -2246,7 +2268,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         if (t == 0) {
             a.std_o[k] = valid ? sd : 0.0;
             a.mean_o[k] = valid ? mean : 0.0;
-            a.ptp_o[k] = valid ? ptp : 1e20f;
+            a.ptp_o[k] = ptp;
             a.fft_o[k] = fftv;
         }
     }
@@ -2443,7 +2465,7 @@ __global__ __launch_bounds__(256) void k_linestats(LineStatsArgs a, int rows, in
     unsigned long long *keys = (unsigned long long *)(lsm + (size_t)wave * per_wave + 1024);
     const int nline = rows ? a.nsub : a.nchan;
     const int diag = line / nline, idx = line % nline;
-    const bool f32 = diag == 2, plain = diag == 3;
+    const bool f32 = diag == 2 && a.ptp_f32, plain = diag == 3;
     // gather the valid values (ballot compaction keeps no particular order: the
     // selection does not need one)
     int cnt = 0, nan = 0;
@@ -2454,7 +2476,7 @@ __global__ __launch_bounds__(256) void k_linestats(LineStatsArgs a, int rows, in
         if (q < len) {
             const size_t kk = rows ? (size_t)idx * a.nchan + q : (size_t)q * a.nchan + idx;
             v = plain ? true : (a.valid[kk] != 0);
-            d = diag == 0 ? a.std_d[kk] : diag == 1 ? a.mean_d[kk] : diag == 2 ? (double)a.ptp_d[kk] : a.fft_d[kk];
+            d = diag == 0 ? a.std_d[kk] : diag == 1 ? a.mean_d[kk] : diag == 2 ? a.ptp_d[kk] : a.fft_d[kk];
         }
         const unsigned long long m = __ballot(v);
         if (v) keys[cnt + __popcll(m & ((1ull << lane) - 1ull))] = key64(d);
@@ -2535,7 +2557,7 @@ __device__ __forceinline__ double nanmax2(double a, double b)
 __global__ __launch_bounds__(256) void k_combine(
     int nsub, int nchan, const uint8_t *__restrict__ valid, const int32_t *__restrict__ info,
     const float *__restrict__ w0,
-    const double *__restrict__ std_d, const double *__restrict__ mean_d, const float *__restrict__ ptp_d,
+    const double *__restrict__ std_d, const double *__restrict__ mean_d, const double *__restrict__ ptp_d, int ptp_f32,
     const double *__restrict__ fft_d, const double *__restrict__ col_med, const double *__restrict__ col_mad,
     const double *__restrict__ row_med, const double *__restrict__ row_mad, double cth, double sth,
     double *__restrict__ test, float *__restrict__ W, float *__restrict__ hist, int iter,
@@ -2557,8 +2579,13 @@ __global__ __launch_bounds__(256) void k_combine(
                        scale_masked_d(std_d[k], v, row_med[s], row_mad[s], sth));
         S[1] = nanmax2(scale_masked_d(mean_d[k], v, col_med[nchan + c], col_mad[nchan + c], cth),
                        scale_masked_d(mean_d[k], v, row_med[nsub + s], row_mad[nsub + s], sth));
-        S[2] = nanmax2(scale_masked_f(ptp_d[k], v, (float)col_med[2 * nchan + c], (float)col_mad[2 * nchan + c], cth),
-                       scale_masked_f(ptp_d[k], v, (float)row_med[2 * nsub + s], (float)row_mad[2 * nsub + s], sth));
+        // ptp: numpy.ma in f32 for f32 data (Appendix A.5), f64 for f64 data
+        S[2] = ptp_f32 ? nanmax2(scale_masked_f((float)ptp_d[k], v, (float)col_med[2 * nchan + c],
+                                                (float)col_mad[2 * nchan + c], cth),
+                                 scale_masked_f((float)ptp_d[k], v, (float)row_med[2 * nsub + s],
+                                                (float)row_mad[2 * nsub + s], sth))
+                       : nanmax2(scale_masked_d(ptp_d[k], v, col_med[2 * nchan + c], col_mad[2 * nchan + c], cth),
+                                 scale_masked_d(ptp_d[k], v, row_med[2 * nsub + s], row_mad[2 * nsub + s], sth));
         S[3] = nanmax2(scale_plain(fft_d[k], col_med[3 * nchan + c], col_mad[3 * nchan + c], cth),
                        scale_plain(fft_d[k], row_med[3 * nsub + s], row_mad[3 * nsub + s], sth));
         double t;
@@ -2646,11 +2673,11 @@ __device__ __forceinline__ int geom_chan_owner(const ShardGeom &g, int c)
 // the blocks of d' < d.
 __global__ __launch_bounds__(256) void k_pack_rows(ShardGeom g, int nchan_loc, const double *__restrict__ std_d,
                                                    const double *__restrict__ mean_d, const double *__restrict__ fft_d,
-                                                   const float *__restrict__ ptp_d, const uint8_t *__restrict__ valid,
+                                                   const double *__restrict__ ptp_d, const uint8_t *__restrict__ valid,
                                                    unsigned char *__restrict__ send)
 {
     const size_t P = (size_t)g.nsub * nchan_loc;
-    const size_t esz = valid ? 1 : 28;
+    const size_t esz = valid ? 1 : 32;
     for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < P; k += (size_t)gridDim.x * blockDim.x) {
         const int s = (int)(k / nchan_loc);
         const int d = geom_row_owner(g, s);
@@ -2665,7 +2692,7 @@ __global__ __launch_bounds__(256) void k_pack_rows(ShardGeom g, int nchan_loc, c
             ((double *)blk)[e] = std_d[k];
             ((double *)blk)[n_d + e] = mean_d[k];
             ((double *)blk)[2 * n_d + e] = fft_d[k];
-            ((float *)(blk + 24 * n_d))[e] = ptp_d[k];
+            ((double *)blk)[3 * n_d + e] = ptp_d[k];
         }
     }
 }
@@ -2674,12 +2701,12 @@ __global__ __launch_bounds__(256) void k_pack_rows(ShardGeom g, int nchan_loc, c
 // elements per field, after the padded blocks of sources p' < p).
 __global__ __launch_bounds__(256) void k_assemble_rows(ShardGeom g, const unsigned char *__restrict__ recv,
                                                        double *__restrict__ std_r, double *__restrict__ mean_r,
-                                                       double *__restrict__ fft_r, float *__restrict__ ptp_r,
+                                                       double *__restrict__ fft_r, double *__restrict__ ptp_r,
                                                        uint8_t *__restrict__ valid_r)
 {
     const int rows = g.row0[g.rank + 1] - g.row0[g.rank];
     const size_t n = (size_t)rows * g.nchan_g;
-    const size_t esz = valid_r ? 1 : 28;
+    const size_t esz = valid_r ? 1 : 32;
     for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
         const int r = (int)(k / g.nchan_g), c = (int)(k % g.nchan_g);
         const int p = geom_chan_owner(g, c);
@@ -2695,7 +2722,7 @@ __global__ __launch_bounds__(256) void k_assemble_rows(ShardGeom g, const unsign
             std_r[k] = ((const double *)blk)[e];
             mean_r[k] = ((const double *)blk)[n_p + e];
             fft_r[k] = ((const double *)blk)[2 * n_p + e];
-            ptp_r[k] = ((const float *)(blk + 24 * n_p))[e];
+            ptp_r[k] = ((const double *)blk)[3 * n_p + e];
         }
     }
 }
@@ -2850,7 +2877,7 @@ hipError_t launch_unpack_fscrunch(hipStream_t st, const ShardGeom &g, int rows_p
 }
 
 hipError_t launch_pack_rows(hipStream_t st, const ShardGeom &g, int nchan_loc, const double *std_d,
-                            const double *mean_d, const double *fft_d, const float *ptp_d, const uint8_t *valid,
+                            const double *mean_d, const double *fft_d, const double *ptp_d, const uint8_t *valid,
                             unsigned char *send)
 {
     const size_t P = (size_t)g.nsub * nchan_loc;
@@ -2861,7 +2888,7 @@ hipError_t launch_pack_rows(hipStream_t st, const ShardGeom &g, int nchan_loc, c
 }
 
 hipError_t launch_assemble_rows(hipStream_t st, const ShardGeom &g, const unsigned char *recv, double *std_r,
-                                double *mean_r, double *fft_r, float *ptp_r, uint8_t *valid_r)
+                                double *mean_r, double *fft_r, double *ptp_r, uint8_t *valid_r)
 {
     const size_t n = (size_t)(g.row0[g.rank + 1] - g.row0[g.rank]) * g.nchan_g;
     if (n == 0) return hipSuccess;
@@ -2930,6 +2957,26 @@ hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, lo
     return hipGetLastError();
 }
 
+template <int NN, bool D64>
+static hipError_t launch_p2(hipStream_t st, const DiagArgs &a, size_t P)
+{
+    using C = P2<NN, D64>;
+    const size_t fixed = (size_t)C::TW_LDS * 16;
+    int gpb = C::WPP > 1 ? 1 : 8;
+    while (gpb > 1 && fixed + gpb * (size_t)C::GROUP_BYTES > 150 * 1024) --gpb;
+    const size_t shm = fixed + gpb * (size_t)C::GROUP_BYTES;
+    const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
+    if (a.mode == DIAG_EXACT)
+        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_EXACT, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
+    else if (a.mode == DIAG_CLOSED)
+        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_CLOSED, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
+    else if (!D64)   // comprehensive_stats alone takes f32 data
+        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_STATS, false>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
 {
     const int nbin = a.nbin;
@@ -2940,19 +2987,8 @@ hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
         return hipErrorInvalidValue;
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
-        using C = P2<NN>;                                                                          \
-        const size_t fixed = (size_t)C::TW_LDS * 16;                                               \
-        int gpb = C::WPP > 1 ? 1 : 8;                                                              \
-        while (gpb > 1 && fixed + gpb * (size_t)C::GROUP_BYTES > 150 * 1024) --gpb;                \
-        const size_t shm = fixed + gpb * (size_t)C::GROUP_BYTES;                                   \
-        const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);               \
-        if (a.mode == DIAG_EXACT)                                                                  \
-            hipLaunchKernelGGL((k_diag_p2<NN, DIAG_EXACT>), dim3(grid), dim3(C::TPP * gpb), shm, st, a); \
-        else if (a.mode == DIAG_CLOSED)                                                            \
-            hipLaunchKernelGGL((k_diag_p2<NN, DIAG_CLOSED>), dim3(grid), dim3(C::TPP * gpb), shm, st, a); \
-        else                                                                                       \
-            hipLaunchKernelGGL((k_diag_p2<NN, DIAG_STATS>), dim3(grid), dim3(C::TPP * gpb), shm, st, a); \
-        return hipGetLastError();                                                                  \
+        if (a.data_f64) return launch_p2<NN, true>(st, a, P);                                      \
+        return launch_p2<NN, false>(st, a, P);                                                     \
     }
     IC_P2(64) IC_P2(128) IC_P2(256) IC_P2(512) IC_P2(1024) IC_P2(2048) IC_P2(4096)
 #undef IC_P2
@@ -3011,7 +3047,7 @@ hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
 
 hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const int32_t *info,
                           const float *w0,
-                          const double *std_d, const double *mean_d, const float *ptp_d,
+                          const double *std_d, const double *mean_d, const double *ptp_d, int ptp_f32,
                           const double *fft_d, const double *col_med, const double *col_mad,
                           const double *row_med, const double *row_mad, double chanthresh,
                           double subintthresh, double *test, float *W, float *hist, int iter,
@@ -3020,7 +3056,7 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
     const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 256), 1024);
     hipLaunchKernelGGL(k_combine, dim3(grid), dim3(256), 0, st, nsub, nchan, valid, info, w0, std_d,
-                       mean_d, ptp_d, fft_d, col_med, col_mad, row_med, row_mad, chanthresh, subintthresh,
+                       mean_d, ptp_d, ptp_f32, fft_d, col_med, col_mad, row_med, row_mad, chanthresh, subintthresh,
                        test, W, hist, iter, counters);
     return hipGetLastError();
 }

@@ -86,7 +86,7 @@ struct Session {
     double *xr_send = nullptr, *xr_recv = nullptr;          // row medians / MADs
     std::vector<size_t> dsb, drb, vsb, vrb;                 // block bytes: diag, valid
     double *std_r = nullptr, *mean_r = nullptr, *fft_r = nullptr;   // owned rows [rows_own][nchan_g]
-    float *ptp_r = nullptr;
+    double *ptp_r = nullptr;
     uint8_t *valid_r = nullptr;
     // device buffers
     float *raw = nullptr, *D = nullptr, *w0 = nullptr, *W = nullptr, *base = nullptr, *base0 = nullptr;
@@ -98,7 +98,8 @@ struct Session {
     hipStream_t copy_stream = nullptr;
     int cur = 0, fifo[2] = {0, 0}, fifo_n = 0;
     bool ever_uploaded = false;
-    float *F = nullptr, *wf = nullptr, *T = nullptr, *ptp = nullptr, *hist = nullptr;
+    float *F = nullptr, *wf = nullptr, *T = nullptr, *hist = nullptr;
+    double *ptp = nullptr;      // f64 storage; f32 values unless p.data_f64
     uint8_t *valid = nullptr;
     int32_t *shift = nullptr, *win = nullptr, *wflag = nullptr, *info = nullptr, *counters = nullptr;
     double *part = nullptr, *part2 = nullptr, *wpart = nullptr, *T64 = nullptr, *amp = nullptr, *std_ = nullptr,
@@ -469,6 +470,7 @@ int shard_rowstats(Session *s, const LineStatsArgs &la)
     lr.mean_d = s->mean_r;
     lr.fft_d = s->fft_r;
     lr.ptp_d = s->ptp_r;
+    lr.ptp_f32 = la.ptp_f32;
     lr.col_med = lr.col_mad = nullptr;
     lr.row_med = s->xr_send;
     lr.row_mad = s->xr_send + 4 * s->rows_own;
@@ -701,9 +703,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         for (int r = 0; r < world; ++r) {
             const size_t rows_r = (size_t)(rr[2 * r + 1] - rr[2 * r]);
             const size_t nch_r = (size_t)(cr[2 * r + 1] - cr[2 * r]);
-            s->dsb.push_back(shard_block_bytes(rows_r * nchan, 28));
+            s->dsb.push_back(shard_block_bytes(rows_r * nchan, 32));
             s->vsb.push_back(shard_block_bytes(rows_r * nchan, 1));
-            s->drb.push_back(shard_block_bytes((size_t)s->rows_own * nch_r, 28));
+            s->drb.push_back(shard_block_bytes((size_t)s->rows_own * nch_r, 32));
             s->vrb.push_back(shard_block_bytes((size_t)s->rows_own * nch_r, 1));
             dsend += s->dsb.back();
             drecv += s->drb.back();
@@ -1009,6 +1011,7 @@ DiagArgs diag_args(Session *s, int pr_start, int pr_end)
     a.mean_o = s->mean;
     a.fft_o = s->fft;
     a.ptp_o = s->ptp;
+    a.data_f64 = p.data_f64 != 0;
     return a;
 }
 
@@ -1044,6 +1047,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     la.mean_d = s->mean;
     la.fft_d = s->fft;
     la.ptp_d = s->ptp;
+    la.ptp_f32 = !p.data_f64;
     la.col_med = s->lstat;
     la.col_mad = s->lstat + 4 * nchan;
     la.row_med = s->lstat + 8 * nchan;
@@ -1070,7 +1074,8 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             if (int rc = shard_rowstats(s, la)) return rc;
         CK(hipMemsetAsync(s->counters, 0, sizeof(int32_t) * (p.max_iter + 5), s->stream));
         LAUNCH(s, K_COMBINE,
-               launch_combine(s->stream, nsub, nchan, s->valid, s->info, s->w0, s->std_, s->mean, s->ptp, s->fft,
+               launch_combine(s->stream, nsub, nchan, s->valid, s->info, s->w0, s->std_, s->mean, s->ptp, la.ptp_f32,
+                              s->fft,
                               la.col_med, la.col_mad, la.row_med, la.row_mad, p.chanthresh, p.subintthresh,
                               s->test, s->W, s->hist, n_iter, s->counters));
         if (s->comm)
@@ -1194,16 +1199,26 @@ int ic_get_fit(void *session, double *amp, int32_t *info)
     return IC_OK;
 }
 
-int ic_get_diagnostics(void *session, double *std_o, double *mean_o, float *ptp_o, double *fftmax_o)
+int ic_get_diagnostics_f64(void *session, double *std_o, double *mean_o, double *ptp_o, double *fftmax_o)
 {
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null argument");
     if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
     if (std_o) CK(hipMemcpyAsync(std_o, s->std_, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
     if (mean_o) CK(hipMemcpyAsync(mean_o, s->mean, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
-    if (ptp_o) CK(hipMemcpyAsync(ptp_o, s->ptp, sizeof(float) * s->P, hipMemcpyDeviceToHost, s->stream));
+    if (ptp_o) CK(hipMemcpyAsync(ptp_o, s->ptp, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
     if (fftmax_o) CK(hipMemcpyAsync(fftmax_o, s->fft, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
     CK(hipStreamSynchronize(s->stream));
+    return IC_OK;
+}
+
+int ic_get_diagnostics(void *session, double *std_o, double *mean_o, float *ptp_o, double *fftmax_o)
+{
+    Session *s = (Session *)session;
+    if (!s) return fail(IC_EINVAL, "null argument");
+    std::vector<double> ptp(ptp_o ? s->P : 0);
+    if (int rc = ic_get_diagnostics_f64(session, std_o, mean_o, ptp_o ? ptp.data() : nullptr, fftmax_o)) return rc;
+    for (size_t k = 0; k < ptp.size(); ++k) ptp_o[k] = (float)ptp[k];   // exact unless data_f64
     return IC_OK;
 }
 
@@ -1246,14 +1261,14 @@ int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const floa
         size_t bytes;
     } al[] = {{&bD, 4 * N},       {&bw, 4 * P},      {&bvalid, P},      {&bW, 4 * P},
               {&bhist, 8 * P},    {&bstd, 8 * P},    {&bmean, 8 * P},   {&bfft, 8 * P},
-              {&bptp, 4 * P},     {&btest, 8 * P},   {&blstat, 8 * 16 * ((size_t)nsub + nchan)},
+              {&bptp, 8 * P},     {&btest, 8 * P},   {&blstat, 8 * 16 * ((size_t)nsub + nchan)},
               {&bcnt, 4 * 8},     {&btw, 16 * (size_t)nbin}, {&btw2, 16 * (size_t)nbin + 16}, {&bplan, sizeof plan}};
     for (auto &x : al)
         if (hipMalloc(&x.b->p, x.bytes + 16) != hipSuccess) return fail(IC_ENOMEM, "hipMalloc(%zu) failed", x.bytes);
     float *D = (float *)bD.p, *w0 = (float *)bw.p, *W = (float *)bW.p, *hist = (float *)bhist.p;
     uint8_t *valid = (uint8_t *)bvalid.p;
     double *sd = (double *)bstd.p, *mn = (double *)bmean.p, *ff = (double *)bfft.p, *test = (double *)btest.p;
-    float *pt = (float *)bptp.p;
+    double *pt = (double *)bptp.p;
     double *lstat = (double *)blstat.p;
     int32_t *cnt = (int32_t *)bcnt.p;
     CK(hipMemcpyAsync(D, data, 4 * N, hipMemcpyHostToDevice, st));
@@ -1288,19 +1303,22 @@ int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const floa
     la.mean_d = mn;
     la.fft_d = ff;
     la.ptp_d = pt;
+    la.ptp_f32 = 1;
     la.col_med = lstat;
     la.col_mad = lstat + 4 * nchan;
     la.row_med = lstat + 8 * nchan;
     la.row_mad = lstat + 8 * nchan + 4 * nsub;
     CK(launch_linestats(st, la, 3));
-    CK(launch_combine(st, nsub, nchan, valid, nullptr, w0, sd, mn, pt, ff, la.col_med, la.col_mad, la.row_med, la.row_mad,
+    CK(launch_combine(st, nsub, nchan, valid, nullptr, w0, sd, mn, pt, 1, ff, la.col_med, la.col_mad, la.row_med, la.row_mad,
                       chanthresh, subintthresh, test, W, hist, 1, cnt));
     CK(hipMemcpyAsync(test_out, test, 8 * P, hipMemcpyDeviceToHost, st));
     if (std_o) CK(hipMemcpyAsync(std_o, sd, 8 * P, hipMemcpyDeviceToHost, st));
     if (mean_o) CK(hipMemcpyAsync(mean_o, mn, 8 * P, hipMemcpyDeviceToHost, st));
-    if (ptp_o) CK(hipMemcpyAsync(ptp_o, pt, 4 * P, hipMemcpyDeviceToHost, st));
+    std::vector<double> ptp64(ptp_o ? P : 0);
+    if (ptp_o) CK(hipMemcpyAsync(ptp64.data(), pt, 8 * P, hipMemcpyDeviceToHost, st));
     if (fftmax_o) CK(hipMemcpyAsync(fftmax_o, ff, 8 * P, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
+    for (size_t k = 0; k < ptp64.size(); ++k) ptp_o[k] = (float)ptp64[k];
     return IC_OK;
 }
 

@@ -64,6 +64,18 @@ def make_cube(nsub, nchan, nbin, seed=0, rfi_frac=0.05, npol=1, dead_frac=0.02):
     return np.ascontiguousarray(data4), weights, shift
 
 
+def fractional_weights(w):
+    """A deterministic edit putting non-dyadic fractional weights (0.3, 0.7) and
+    0.5 on some live profiles (apply_weights multiplies by them, ic.py:296)."""
+    w = np.array(w, dtype=np.float32, copy=True)
+    nsub, nchan = w.shape
+    for s in range(nsub):
+        for c in range((s * 7) % 5, nchan, 5):
+            if w[s, c] != 0:
+                w[s, c] = (0.3, 0.7, 0.5)[(s + c) % 3]
+    return w
+
+
 def make_archive(nsub, nchan, nbin, seed=0, rfi_frac=0.05, npol=1,
                  filename="synthetic.ar", **kw) -> Archive:
     data, weights, shift = make_cube(nsub, nchan, nbin, seed, rfi_frac, npol, **kw)

@@ -642,6 +642,46 @@ void orc_diagnostics(int P, int n, const float *X, const uint8_t *valid,
     free(d); free(sq); free(work);
 }
 
+/* f64 data (psrchive get_data returning f64; ic_params.data_f64): X is the f64
+ * product f64(R) * f64(w), and numpy.ma sums, ptp and scales in f64
+ * (iterative_cleaner.py:111-112, :206-209). */
+void orc_diagnostics_f64(int P, int n, const double *X, const uint8_t *valid,
+                         double *std_o, double *mean_o, double *ptp_o, double *fft_o)
+{
+    double *d = (double *)malloc(sizeof(double) * (size_t)n);
+    double *sq = (double *)malloc(sizeof(double) * (size_t)n);
+    double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
+    for (int k = 0; k < P; ++k) {
+        const double *x = X + (size_t)k * n;
+        if (!valid[k]) {
+            std_o[k] = 0.0;
+            mean_o[k] = 0.0;
+            ptp_o[k] = 1e20;    /* numpy.ma's f64 fill value (f32 data: f32(1e20)) */
+            for (int i = 0; i < n; ++i) d[i] = x[i];
+            fft_o[k] = fftmax(d, n, work);
+            continue;
+        }
+        double mean = orc_sum_f64(x, n) / (double)n;
+        for (int i = 0; i < n; ++i) {
+            d[i] = x[i] - mean;
+            sq[i] = d[i] * d[i];
+        }
+        double var = orc_sum_f64(sq, n) / (double)n;
+        double mx = x[0], mn = x[0];
+        int nan = 0;
+        for (int i = 0; i < n; ++i) {
+            if (isnan(x[i])) nan = 1;
+            if (x[i] > mx) mx = x[i];
+            if (x[i] < mn) mn = x[i];
+        }
+        std_o[k] = sqrt(var);
+        mean_o[k] = mean;
+        ptp_o[k] = nan ? NAN : (mx - mn);
+        fft_o[k] = fftmax(d, n, work);
+    }
+    free(d); free(sq); free(work);
+}
+
 /* ------------------------------------------------------ medians + scalers */
 static int cmp_d(const void *a, const void *b)
 {
@@ -810,10 +850,29 @@ static double nanmax2(double a, double b)
     return a > b ? a : b;
 }
 
+static void test_impl(int nsub, int nchan, const uint8_t *valid, const double *std_d, const double *mean_d,
+                      const float *ptp_d, const double *ptp64, const double *fft_d, double chanthresh,
+                      double subintthresh, double *test);
+
 /* scalers + combine: test (nsub*nchan) from the 4 diagnostics. */
 void orc_test(int nsub, int nchan, const uint8_t *valid, const double *std_d,
               const double *mean_d, const float *ptp_d, const double *fft_d,
               double chanthresh, double subintthresh, double *test)
+{
+    test_impl(nsub, nchan, valid, std_d, mean_d, ptp_d, NULL, fft_d, chanthresh, subintthresh, test);
+}
+
+/* the same for f64 data: ptp is f64 and scaled in f64 */
+void orc_test_f64(int nsub, int nchan, const uint8_t *valid, const double *std_d,
+                  const double *mean_d, const double *ptp_d, const double *fft_d,
+                  double chanthresh, double subintthresh, double *test)
+{
+    test_impl(nsub, nchan, valid, std_d, mean_d, NULL, ptp_d, fft_d, chanthresh, subintthresh, test);
+}
+
+static void test_impl(int nsub, int nchan, const uint8_t *valid, const double *std_d, const double *mean_d,
+                      const float *ptp_d, const double *ptp64, const double *fft_d, double chanthresh,
+                      double subintthresh, double *test)
 {
     size_t P = (size_t)nsub * nchan;
     int L = nsub > nchan ? nsub : nchan;
@@ -826,14 +885,16 @@ void orc_test(int nsub, int nchan, const uint8_t *valid, const double *std_d,
         for (int c = 0; c < nchan; ++c) {
             if (which == 0) scale_line_masked_d(nsub, std_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, bufd);
             if (which == 1) scale_line_masked_d(nsub, mean_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, bufd);
-            if (which == 2) scale_line_masked_f(nsub, ptp_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, buff);
+            if (which == 2 && ptp64) scale_line_masked_d(nsub, ptp64 + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, bufd);
+            if (which == 2 && !ptp64) scale_line_masked_f(nsub, ptp_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, buff);
             if (which == 3) scale_line_plain(nsub, fft_d + c, nchan, chanthresh, ch + c, nchan, bufd);
         }
         for (int s = 0; s < nsub; ++s) {
             size_t o = (size_t)s * nchan;
             if (which == 0) scale_line_masked_d(nchan, std_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, bufd);
             if (which == 1) scale_line_masked_d(nchan, mean_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, bufd);
-            if (which == 2) scale_line_masked_f(nchan, ptp_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, buff);
+            if (which == 2 && ptp64) scale_line_masked_d(nchan, ptp64 + o, valid + o, 1, 1, subintthresh, sb + o, 1, bufd);
+            if (which == 2 && !ptp64) scale_line_masked_f(nchan, ptp_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, buff);
             if (which == 3) scale_line_plain(nchan, fft_d + o, 1, subintthresh, sb + o, 1, bufd);
         }
         for (size_t k = 0; k < P; ++k) S[which * P + k] = nanmax2(ch[k], sb[k]);
@@ -856,6 +917,7 @@ typedef struct {
     int32_t pr_start, pr_end;
     double baseline_duty;
     int32_t fit_mode;   /* 0: exact leastsq (orc_fit_residual), 1: closed form (orc_fit_closed) */
+    int32_t data_f64;   /* 1: get_data returns f64 (orc_diagnostics_f64 / orc_test_f64) */
 } orc_params;
 
 /* One full clean loop (iterative_cleaner.py:83-146).
@@ -863,11 +925,11 @@ typedef struct {
  * Outputs: test (P), weights (P), loops, changed[max_iter], nzero[max_iter];
  * optional (may be NULL): R_last (P*nbin, dispersed frame, unweighted),
  * T_all (max_iter*nbin), amp_last/info_last (P),
- * diag_last: std, mean (P f64), ptp (P f32), fft (P f64). */
+ * diag_last: std, mean (P f64), ptp (P, f64 storage: f32 values unless data_f64), fft (P f64). */
 int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, const int32_t *shift,
                    double *test, float *weights, int32_t *loops_out, int32_t *changed,
                    int32_t *nzero, float *R_last, float *T_all, double *amp_last,
-                   int32_t *info_last, double *std_l, double *mean_l, float *ptp_l, double *fft_l)
+                   int32_t *info_last, double *std_l, double *mean_l, double *ptp_l, double *fft_l)
 {
     const int nsub = pp->nsub, nchan = pp->nchan, n = pp->nbin;
     const size_t P = (size_t)nsub * nchan, N = P * (size_t)n;
@@ -879,6 +941,8 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
     int32_t *info = (int32_t *)malloc(sizeof(int32_t) * P);
     double *sd = (double *)malloc(sizeof(double) * P), *mn = (double *)malloc(sizeof(double) * P);
     float *pt = (float *)malloc(sizeof(float) * P);
+    double *pt64 = (double *)malloc(sizeof(double) * P);
+    double *X64 = pp->data_f64 ? (double *)malloc(sizeof(double) * N) : NULL;
     double *ff = (double *)malloc(sizeof(double) * P);
     uint8_t *valid = (uint8_t *)malloc(P);
     int maxit = pp->max_iter;
@@ -909,11 +973,18 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
                 for (int j = 0; j < n; ++j) {
                     int i = j - sh;
                     if (i < 0) i += n;
-                    o[j] = r[i] * w;
+                    if (X64) X64[k * n + j] = (double)r[i] * (double)w;
+                    else o[j] = r[i] * w;
                 }
             }
-        orc_diagnostics((int)P, n, X, valid, sd, mn, pt, ff);
-        orc_test(nsub, nchan, valid, sd, mn, pt, ff, pp->chanthresh, pp->subintthresh, test);
+        if (X64) {
+            orc_diagnostics_f64((int)P, n, X64, valid, sd, mn, pt64, ff);
+            orc_test_f64(nsub, nchan, valid, sd, mn, pt64, ff, pp->chanthresh, pp->subintthresh, test);
+        } else {
+            orc_diagnostics((int)P, n, X, valid, sd, mn, pt, ff);
+            orc_test(nsub, nchan, valid, sd, mn, pt, ff, pp->chanthresh, pp->subintthresh, test);
+            for (size_t k = 0; k < P; ++k) pt64[k] = (double)pt[k];
+        }
         int ndiff = 0, nz = 0;
         for (size_t k = 0; k < P; ++k) {
             float w = (test[k] >= 1.0) ? 0.0f : w0[k];
@@ -949,10 +1020,10 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
     if (info_last) memcpy(info_last, info, sizeof(int32_t) * P);
     if (std_l) memcpy(std_l, sd, sizeof(double) * P);
     if (mean_l) memcpy(mean_l, mn, sizeof(double) * P);
-    if (ptp_l) memcpy(ptp_l, pt, sizeof(float) * P);
+    if (ptp_l) memcpy(ptp_l, pt64, sizeof(double) * P);
     if (fft_l) memcpy(fft_l, ff, sizeof(double) * P);
     *loops_out = loops;
     free(D); free(Rd); free(X); free(T); free(amp); free(info); free(sd); free(mn);
-    free(pt); free(ff); free(valid); free(hist); free(Wcur);
+    free(pt); free(pt64); free(X64); free(ff); free(valid); free(hist); free(Wcur);
     return 0;
 }

@@ -24,7 +24,7 @@ class OrcParams(C.Structure):
                 ("max_iter", C.c_int32), ("chanthresh", C.c_double),
                 ("subintthresh", C.c_double), ("pr_on", C.c_int32),
                 ("pr_factor", C.c_double), ("pr_start", C.c_int32), ("pr_end", C.c_int32),
-                ("baseline_duty", C.c_double), ("fit_mode", C.c_int32)]
+                ("baseline_duty", C.c_double), ("fit_mode", C.c_int32), ("data_f64", C.c_int32)]
 
 
 def _p(a):
@@ -48,6 +48,8 @@ def lib():
         _lib.orc_template.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_double, C.c_void_p]
         _lib.orc_diagnostics.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6
         _lib.orc_test.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 5 + [C.c_double, C.c_double, C.c_void_p]
+        _lib.orc_test_f64.argtypes = _lib.orc_test.argtypes
+        _lib.orc_diagnostics_f64.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6
         _lib.orc_sum_f32.restype = C.c_float
         _lib.orc_sum_f32.argtypes = [C.c_void_p, C.c_int]
         _lib.orc_sum_f64.restype = C.c_double
@@ -132,17 +134,32 @@ def diagnostics(X, valid):
     return sd.reshape(shp), mn.reshape(shp), pt.reshape(shp), ff.reshape(shp)
 
 
+def diagnostics_f64(X, valid):
+    """Diagnostics of f64 data (data_f64): X is the f64 weighted cube."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    shp = X.shape[:-1]
+    P, n = int(np.prod(shp)), X.shape[-1]
+    v = np.ascontiguousarray(valid, dtype=np.uint8).reshape(P)
+    sd, mn, pt, ff = (np.empty(P, np.float64) for _ in range(4))
+    lib().orc_diagnostics_f64(P, n, _p(X), _p(v), _p(sd), _p(mn), _p(pt), _p(ff))
+    return sd.reshape(shp), mn.reshape(shp), pt.reshape(shp), ff.reshape(shp)
+
+
 def test_values(valid, std, mean, ptp, fft, ct, st):
+    """Scaled test values; ptp f32 (f32 data) or f64 (f64 data: scaled in f64)."""
     nsub, nchan = np.shape(valid)
     out = np.empty((nsub, nchan), np.float64)
-    lib().orc_test(nsub, nchan, _p(np.ascontiguousarray(valid, np.uint8)),
-                   _p(np.ascontiguousarray(std, np.float64)), _p(np.ascontiguousarray(mean, np.float64)),
-                   _p(f32(ptp)), _p(np.ascontiguousarray(fft, np.float64)), float(ct), float(st), _p(out))
+    d64 = np.asarray(ptp).dtype == np.float64
+    fn = lib().orc_test_f64 if d64 else lib().orc_test
+    fn(nsub, nchan, _p(np.ascontiguousarray(valid, np.uint8)),
+       _p(np.ascontiguousarray(std, np.float64)), _p(np.ascontiguousarray(mean, np.float64)),
+       _p(np.ascontiguousarray(ptp, np.float64) if d64 else f32(ptp)), _p(np.ascontiguousarray(fft, np.float64)),
+       float(ct), float(st), _p(out))
     return out
 
 
 def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pulse_region=None,
-               duty=0.15, want_residual=False, want_details=False, fit_mode=0):
+               duty=0.15, want_residual=False, want_details=False, fit_mode=0, data_f64=False):
     """Whole loop; returns dict(test, weights, loops, changed, nzero, [...])."""
     raw = f32(raw)
     nsub, nchan, n = raw.shape
@@ -151,7 +168,7 @@ def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pul
     if pulse_region is not None:
         pr_on, fac, a, b = 1, float(pulse_region[0]), int(pulse_region[1]), int(pulse_region[2])
     prm = OrcParams(nsub, nchan, n, max_iter, float(chanthresh), float(subintthresh), pr_on, fac, a, b, duty,
-                    int(fit_mode))
+                    int(fit_mode), 1 if data_f64 else 0)
     test = np.empty((nsub, nchan), np.float64)
     weights = np.empty((nsub, nchan), np.float32)
     loops = np.zeros(1, np.int32)
@@ -163,7 +180,7 @@ def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pul
     info = np.empty(P, np.int32) if want_details else None
     sd = np.empty(P, np.float64) if want_details else None
     mn = np.empty(P, np.float64) if want_details else None
-    pt = np.empty(P, np.float32) if want_details else None
+    pt = np.empty(P, np.float64) if want_details else None
     ff = np.empty(P, np.float64) if want_details else None
     lib().orc_clean_loop(C.byref(prm), _p(raw), _p(f32(w0)), _p(np.ascontiguousarray(shift, np.int32)),
                          _p(test), _p(weights), _p(loops), _p(changed), _p(nzero), _p(R), _p(T_all),
@@ -175,5 +192,6 @@ def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pul
     if want_details:
         out.update(T=T_all, amp=amp.reshape(nsub, nchan), info=info.reshape(nsub, nchan),
                    std=sd.reshape(nsub, nchan), mean=mn.reshape(nsub, nchan),
-                   ptp=pt.reshape(nsub, nchan), fft=ff.reshape(nsub, nchan))
+                   ptp=(pt if data_f64 else pt.astype(np.float32)).reshape(nsub, nchan),
+                   fft=ff.reshape(nsub, nchan))
     return out

@@ -142,21 +142,35 @@ class Recorder:
         return False
 
 
+def _load_f64(path):
+    """The stand-in as a psrchive build whose get_data returns f64."""
+    ar = ica.Archive_load(path)
+    ar.get_data_dtype = np.float64
+    return ar
+
+
 def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
-                   keep_cubes=True, npol=1, workdir=None, out_dir=HERE, residual_full=True):
+                   keep_cubes=True, npol=1, workdir=None, out_dir=HERE, residual_full=True, data_f64=False,
+                   frac_weights=False):
     data, weights, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi, npol=npol)
+    if frac_weights:
+        weights = synth.fractional_weights(weights)
     path = os.path.join(workdir, "%s.ar" % name)
     ar = ica.Archive(data, weights, shift, filename=path)
     ar.unload(path)
-    ar = ica.Archive_load(path)
+    loader = _load_f64 if data_f64 else ica.Archive_load
+    ar = loader(path)
     args = ref_args(ic, ["-l", *extra_args])
     buf = io.StringIO()
     cwd = os.getcwd()
     os.chdir(workdir)
+    stub = sys.modules["psrchive"]
+    stub.Archive_load = loader          # the reference's reload (:150) sees the same binding
     try:
         with Recorder(ic) as rec, contextlib.redirect_stdout(buf):
             out_ar = ic.clean(ar, args, path)
     finally:
+        stub.Archive_load = ica.Archive_load
         os.chdir(cwd)
     stdout = buf.getvalue()
     loops = None
@@ -173,7 +187,8 @@ def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
         "loops": np.array(loops if loops is not None else -1),
         "meta": np.array(json.dumps({
             "name": name, "nsub": nsub, "nchan": nchan, "nbin": nbin, "seed": seed,
-            "rfi": rfi, "npol": npol, "extra_args": list(extra_args),
+            "rfi": rfi, "npol": npol, "extra_args": list(extra_args), "data_f64": bool(data_f64),
+            "frac_weights": bool(frac_weights),
             "args": {k: v for k, v in vars(args).items() if k != "archive"},
             "numpy": np.__version__, "scipy": scipy.__version__})),
     }
@@ -515,7 +530,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--skip-big", action="store_true")
-    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite (round-2 fixtures only)")
+    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64 (round-2 fixtures only)")
     a = ap.parse_args()
     ic = import_reference()
     only = set(filter(None, a.only.split(",")))
@@ -528,6 +543,8 @@ def main():
             run_zap_plot_case(ic, a.out)
         if "nonfinite" in only:
             run_leastsq_nonfinite(ic, a.out)
+        if "f64" in only:
+            run_f64_cases(ic, a.out)
         return
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s12x48x128", 12, 48, 128, 3, 0.05, workdir=wd, out_dir=a.out)
@@ -551,6 +568,21 @@ def main():
     run_long_stats_cases(ic, a.out)
     run_zap_plot_case(ic, a.out)
     run_leastsq_nonfinite(ic, a.out)
+    run_f64_cases(ic, a.out)
+
+
+def run_f64_cases(ic, out_dir=HERE):
+    """clean() through a binding whose get_data returns f64 (ic.py:111-112, :206-209
+    then run in f64), with fractional weights (f64 products differ from f32)."""
+    with tempfile.TemporaryDirectory() as wd:
+        run_clean_case(ic, "s12x48x128_f64", 12, 48, 128, 3, 0.05, data_f64=True, frac_weights=True,
+                       workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s12x48x128_fracw", 12, 48, 128, 3, 0.05, frac_weights=True, keep_cubes=False,
+                       workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s6x48x1024_f64", 6, 48, 1024, 43, 0.05, keep_cubes=False, data_f64=True,
+                       workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s8x40x100_f64_thr3", 8, 40, 100, 7, 0.2, extra_args=("-c", "3", "-s", "3"),
+                       keep_cubes=False, data_f64=True, workdir=wd, out_dir=out_dir)
 
 
 def run_long_cases(ic, out_dir=HERE):

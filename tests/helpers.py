@@ -23,6 +23,8 @@ def load_clean_case(path):
                                       meta["rfi"], npol=meta["npol"])
     assert hashlib.sha256(data.tobytes()).hexdigest() == str(z["input_sha256"]), \
         "synthetic generator drifted from the golden fixture"
+    if meta.get("frac_weights"):
+        w0 = synth.fractional_weights(w0)
     raw = data[:, 0] if meta["npol"] == 1 else (data[:, 0] + data[:, 1]).astype(np.float32)
     return z, meta, np.ascontiguousarray(raw), w0, shift, meta["args"]
 

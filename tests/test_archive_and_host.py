@@ -171,7 +171,7 @@ def test_set_weights_archive_nan_never_zaps():
 def _declared_symbols():
     hdr = open(os.path.join(REPO, "include", "iterative_cleaner.h")).read()
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    return sorted(set(re.findall(r"\b(ic_[a-z_]+)\s*\(", hdr)))
+    return sorted(set(re.findall(r"\b(ic_[a-z0-9_]+)\s*\(", hdr)))
 
 
 def test_library_exports_every_declared_symbol():

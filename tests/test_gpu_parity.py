@@ -20,11 +20,11 @@ TEST_ATOL = 1e-9
 FIT_MODES = {"rounds": 0, "tail": 1 << 40, "default": None}
 
 
-def _session(shape, args, duty=0.15, fit_mode="default"):
+def _session(shape, args, duty=0.15, fit_mode="default", data_f64=False):
     from iterative_cleaner_amd import _native
     nsub, nchan, nbin = shape
     s = _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"],
-                           args["subintthresh"], args["pulse_region"], duty, device=0)
+                           args["subintthresh"], args["pulse_region"], duty, device=0, data_f64=data_f64)
     if FIT_MODES[fit_mode] is not None:
         s.set_fit_tail(FIT_MODES[fit_mode])
     return s
@@ -51,7 +51,7 @@ def _close_test(a, b):
 def test_loop_matches_reference(path, fit_mode):
     z, meta, raw, w0, shift, args = load_clean_case(path)
     nit = int(z["n_iter"])
-    with _session(raw.shape, args, fit_mode=fit_mode) as s:
+    with _session(raw.shape, args, fit_mode=fit_mode, data_f64=meta.get("data_f64", False)) as s:
         s.upload(raw, w0, shift)
         out = s.run()
         T = s.template()
@@ -86,10 +86,22 @@ def test_clean_stdout_matches_reference(path, tmp_path, monkeypatch, capsys):
     from iterative_cleaner_amd import synth
     data, w0_, shift_ = synth.make_cube(meta["nsub"], meta["nchan"], meta["nbin"], meta["seed"],
                                         meta["rfi"], npol=meta["npol"])
+    if meta.get("frac_weights"):
+        w0_ = synth.fractional_weights(w0_)
     monkeypatch.chdir(tmp_path)
     arpath = str(tmp_path / ("%s.ar" % meta["name"]))
     ica.Archive(data, w0_, shift_, filename=arpath).unload(arpath)
     ar = ica.Archive_load(arpath)
+    if meta.get("data_f64"):
+        # a binding whose get_data returns f64 (the reference's reload at :150 saw the same)
+        ar.get_data_dtype = np.float64
+        orig_load = ica.Archive_load
+
+        def load64(path):
+            a = orig_load(path)
+            a.get_data_dtype = np.float64
+            return a
+        monkeypatch.setattr(ica, "Archive_load", load64)
     ns = cleaner.parse_arguments(["-l", *meta["extra_args"], arpath])
     out_ar = cleaner.clean(ar, ns, arpath)
     printed = capsys.readouterr().out
