@@ -11,6 +11,13 @@ TAG=${1:?tag}; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# the in-tree library must be built from the sources being shipped
+for src in iterative_cleaner_amd/csrc/*.hip iterative_cleaner_amd/csrc/*.h include/*.h; do
+    if [ "$src" -nt iterative_cleaner_amd/libicgpu.so ]; then
+        echo "libicgpu.so is older than $src: rebuild (make -C iterative_cleaner_amd/csrc) first"
+        exit 2
+    fi
+done
 n=0
 for step in "$@"; do
     n=$((n + 1))
