@@ -373,7 +373,12 @@ def main():
     ap.add_argument("--no-flip-check", action="store_true",
                     help="closed mode: skip the (untimed) exact run that counts zap-mask flips "
                          "(profiling passes, whose kernel tallies it would mix in)")
+    ap.add_argument("--dedisp", choices=("shift", "fft"), default="shift",
+                    help="shift: integer dedispersion shifts (default); fft: fractional delays, dedispersed by "
+                         "psrchive's FFT phase rotation (dedisp_mode IC_DEDISP_FFT, exact fit only)")
     a = ap.parse_args()
+    if a.dedisp == "fft" and a.fit_mode != "exact":
+        raise SystemExit("--dedisp fft needs --fit-mode exact")
 
     import torch
     import torch.distributed as dist
@@ -406,27 +411,31 @@ def main():
     P_total = nsub * nchan
     if a.batch:
         return batch_main(a, workload, rank, world, local, dev)
+    delay = None
+    if a.dedisp == "fft":
+        from iterative_cleaner_amd import synth
+        delay = synth.fractional_delays(np.arange(nchan) % 7, nbin)   # the generators' integer shifts + fractions
     if sharded:
         chans, _ = _native.shard_layout(nsub, nchan, world)
         c0, c1 = chans[rank]
         cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, c0, c1, dev)
         comm = TorchComm(dev)
         sess = _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm, max_iter=5, device=local,
-                                    fit_mode=fit_mode)
+                                    fit_mode=fit_mode, delay=None if delay is None else delay[c0:c1])
         per_rank_P = nsub * (c1 - c0)
     else:
         if workload in BLOCKWISE:
             cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, 0, nchan, dev)
         else:
             cube, w0, shift = make_cube_device(nsub, nchan, nbin, seed + 7919 * rank, rfi, dev)
-        sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local, fit_mode=fit_mode)
+        sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local, fit_mode=fit_mode, delay=delay)
         per_rank_P = P_total
         if world > 1:
             P_total = P_total * world          # replicas: every rank cleans its own archive
     torch.cuda.synchronize()
     sess.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
     fast = None
-    if fit_mode == _native.FIT_EXACT and not sharded and world == 1 and not a.no_fast_summary:
+    if fit_mode == _native.FIT_EXACT and not sharded and world == 1 and not a.no_fast_summary and delay is None:
         # the north star's fast mode on the same archive, beside the exact line
         fast = fast_mode_summary(_native, cube, w0, shift, (nsub, nchan, nbin), local, a.steps, torch)
     flips = None
@@ -495,6 +504,8 @@ def main():
         wl_key = workload if not sharded else "%s/%d" % (workload, world)
         if fit_mode == _native.FIT_CLOSED:
             wl_key += "/closed"
+        if delay is not None:
+            wl_key += "/fft"
         traffic, src = pmc_traffic(wl_key, dom)
         valu, vsrc = pmc_valu(wl_key)
         hbm = {"achieved": round(hbm_s8d, 1) if hbm_s8d else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -543,8 +554,9 @@ def main():
             "config": {"workload": "%s %dx%dx%d (nsub x nchan x nbin), max_iter 5, thresholds 5/5, %s"
                                    % (workload, nsub, nchan, nbin,
                                       "exact leastsq fit" if fit_mode == _native.FIT_EXACT else
-                                      "closed-form fit (fit_mode 1: fast mode, not the reference's arithmetic)"),
-                       "fit_mode": a.fit_mode,
+                                      "closed-form fit (fit_mode 1: fast mode, not the reference's arithmetic)")
+                                   + (", fractional dedispersion (FFT phase rotation)" if delay is not None else ""),
+                       "fit_mode": a.fit_mode, "dedisp": a.dedisp,
                        "profiles_per_archive": nsub * nchan, "loops": loops[-1], "iterations": n_iter,
                        "fit_rounds": stats["fit_rounds"],
                        "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"])

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define IC_ABI_VERSION 4
+#define IC_ABI_VERSION 5
 
 #define IC_OK 0
 #define IC_EINVAL -1   /* bad argument / shape                         */
@@ -60,6 +60,7 @@ typedef struct {
                                   111-112, 206-209): X = f64(R) * f64(w), f64 mean
                                   sum and ptp, ptp scaled in f64.  The samples must
                                   still be f32 values (the archive's amplitudes).  */
+    int32_t dedisp_mode;       /* IC_DEDISP_SHIFT (default) or IC_DEDISP_FFT       */
 } ic_params;
 
 /* ic_params.fit_mode.
@@ -76,6 +77,22 @@ typedef struct {
  *                  the last bits, and rarely a profile's zap decision flips. */
 #define IC_FIT_EXACT 0
 #define IC_FIT_CLOSED 1
+
+/* ic_params.dedisp_mode: how dedisperse / dededisperse (iterative_cleaner.py:91,
+ * :100, :104) move a channel's samples.
+ *   IC_DEDISP_SHIFT  integer rotation by shift[c] bins (ded[i] = raw[(i+shift)%nbin]),
+ *                    the archive stand-in's default.
+ *   IC_DEDISP_FFT    psrchive's FFT phase rotation by a fractional delay of
+ *                    delay[c] bins (ic_set_delays): forward real FFT, harmonic k
+ *                    times exp(+-2 pi i k delay / nbin), inverse real FFT, in the
+ *                    arithmetic order written in iterative_cleaner_amd/
+ *                    phase_rotation.py (bit-identical to it and to the C oracle;
+ *                    within one f32 ulp of numpy's irfft(rfft(x) * phasor);
+ *                    parity with real psrchive unpinned).  nbin must be a power of
+ *                    two in 64..4096 and fit_mode IC_FIT_EXACT; the shift arrays
+ *                    of the uploads are then unused (pass zeros). */
+#define IC_DEDISP_SHIFT 0
+#define IC_DEDISP_FFT 1
 
 /* Library / device info. */
 int ic_abi_version(void);
@@ -127,6 +144,18 @@ void ic_host_free(void *ptr);
  *                                      (:135-140), 0 if it hit max_iter (:143) */
 int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_out,
            int32_t *changed_out, int32_t *nzero_out, int32_t *n_iter_out, int32_t *converged_out);
+
+/* Fractional delays of the session's channels (dedisp_mode IC_DEDISP_FFT):
+ * delay_bins [nchan] f64 (a shard: its nchan_loc channels), in bins, finite;
+ * dedisperse moves sample j + delay to j.  Required before ic_run; kept until
+ * changed. */
+int ic_set_delays(void *session, const double *delay_bins);
+
+/* dedisperse (sign +1) or dededisperse (sign -1) a cube [nsub][nchan][nbin] f32
+ * by the FFT phase rotation on the GPU (the operation IC_DEDISP_FFT applies at
+ * iterative_cleaner.py:91/:100/:104).  Synchronous; in and out may alias. */
+int ic_rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, const double *delay_bins,
+                       int sign, float *out);
 
 /* The last iteration's residual cube (:101-108), dispersed frame, unweighted,
  * f32 [nsub][nchan][nbin] — what --unload_res writes (:161-162). */

@@ -13,7 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # IC_LIBRARY: an alternative build of the same library (A/B measurements)
 LIB_PATH = os.environ.get("IC_LIBRARY") or os.path.join(HERE, "libicgpu.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # symbols exported by libicgpu.so, as declared in include/iterative_cleaner.h
 EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session_destroy",
@@ -23,10 +23,12 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_shard_layout", "ic_session_create_shard", "ic_group_create", "ic_group_destroy",
            "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free",
            "ic_upload_pols", "ic_comprehensive_stats", "ic_get_bad_fits",
-           "ic_fit_profiles", "ic_get_diagnostics_f64")
+           "ic_fit_profiles", "ic_get_diagnostics_f64", "ic_set_delays", "ic_rotate_profiles")
 
 FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)
 FIT_CLOSED = 1   # IC_FIT_CLOSED: closed-form amplitude fused with the diagnostics (fast mode)
+DEDISP_SHIFT = 0  # IC_DEDISP_SHIFT: integer dedispersion shifts
+DEDISP_FFT = 1    # IC_DEDISP_FFT: fractional delays, FFT phase rotation (phase_rotation.py)
 
 
 class NativeError(RuntimeError):
@@ -38,7 +40,7 @@ class Params(C.Structure):
                 ("max_iter", C.c_int32), ("chanthresh", C.c_double),
                 ("subintthresh", C.c_double), ("pr_on", C.c_int32), ("pr_factor", C.c_double),
                 ("pr_start", C.c_int32), ("pr_end", C.c_int32), ("baseline_duty", C.c_double),
-                ("fit_mode", C.c_int32), ("data_f64", C.c_int32)]
+                ("fit_mode", C.c_int32), ("data_f64", C.c_int32), ("dedisp_mode", C.c_int32)]
 
 
 class RunStats(C.Structure):
@@ -135,6 +137,8 @@ def load_library(path: str = LIB_PATH):
     lib.ic_session_create_grouped.argtypes = [C.POINTER(Params), C.c_int, vp, C.c_int, C.POINTER(vp)]
     lib.ic_get_bad_fits.argtypes = [vp, vp, C.c_int]
     lib.ic_fit_profiles.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp]
+    lib.ic_set_delays.argtypes = [vp, vp]
+    lib.ic_rotate_profiles.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp]
     lib.ic_comprehensive_stats.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_double, C.c_double,
                                            vp, vp, vp, vp, vp]
     if lib.ic_abi_version() != ABI_VERSION:
@@ -171,7 +175,8 @@ class GpuSession:
     """One cleaning session on one GPU (wraps ic_session_*)."""
 
     def __init__(self, nsub, nchan, nbin, max_iter=5, chanthresh=5.0, subintthresh=5.0,
-                 pulse_region=(0, 0, 1), baseline_duty=0.15, device=0, fit_mode=FIT_EXACT, data_f64=False):
+                 pulse_region=(0, 0, 1), baseline_duty=0.15, device=0, fit_mode=FIT_EXACT, data_f64=False,
+                 delay=None):
         self.lib = load_library()
         self.shape = (int(nsub), int(nchan), int(nbin))
         self.max_iter = int(max_iter)
@@ -179,13 +184,24 @@ class GpuSession:
         on, fac, a, b = normalise_pulse_region(list(pulse_region), int(nbin))
         self.params = Params(int(nsub), int(nchan), int(nbin), int(max_iter), float(chanthresh),
                              float(subintthresh), on, fac, a, b, float(baseline_duty), self.fit_mode,
-                             1 if data_f64 else 0)
+                             1 if data_f64 else 0, DEDISP_SHIFT if delay is None else DEDISP_FFT)
         self.data_f64 = bool(data_f64)
         h = C.c_void_p()
         rc = self._create(int(device), h)
         if rc != 0:
             raise NativeError("%s: %s (rc=%d)" % (self._create_name, _err(self.lib), rc))
         self.h = h
+        if delay is not None:
+            self._initial_delays(delay)
+
+    def _initial_delays(self, delay):
+        self.set_delays(delay)
+
+    def set_delays(self, delay):
+        """Fractional per-channel delays in bins (this session's channels) of a
+        session created with `delay` (dedisp_mode IC_DEDISP_FFT)."""
+        d = np.ascontiguousarray(delay, dtype=np.float64).reshape(self.shape[1])
+        self._check(self.lib.ic_set_delays(self.h, _ptr(d)), "ic_set_delays")
 
     _create_name = "ic_session_create"
 
@@ -344,6 +360,22 @@ def fit_profiles(profiles, template, fit_mode=FIT_EXACT, device=0):
     return amp, info, R
 
 
+def rotate_profiles(cube, delay, sign=1, device=0):
+    """Fractional dedispersion of a (nsub, nchan, nbin) cube on the GPU: the FFT
+    phase rotation by +delay (sign 1, dedisperse) or -delay (sign -1)."""
+    lib = load_library()
+    cube = np.ascontiguousarray(cube, dtype=np.float32)
+    if cube.ndim != 3:
+        raise ValueError("rotate_profiles: cube must be (nsub, nchan, nbin)")
+    nsub, nchan, nbin = cube.shape
+    d = np.ascontiguousarray(delay, dtype=np.float64).reshape(nchan)
+    out = np.empty_like(cube)
+    rc = lib.ic_rotate_profiles(int(device), nsub, nchan, nbin, _ptr(cube), _ptr(d), int(sign), _ptr(out))
+    if rc != 0:
+        raise NativeError("ic_rotate_profiles: %s (rc=%d)" % (_err(lib), rc))
+    return out
+
+
 def comprehensive_stats(data, weights, chanthresh=5.0, subintthresh=5.0, device=0, diagnostics=False):
     """comprehensive_stats (iterative_cleaner.py:181-226) on the GPU for the
     (nsub, nchan, nbin) data and (nsub, nchan) weights the reference masks and
@@ -449,9 +481,15 @@ class ShardSession(GpuSession):
         self.chan_range = chans[self.rank]
         self.row_range = rows[self.rank]
         self.global_shape = (int(nsub), int(nchan), int(nbin))
+        self._delay = None
         super().__init__(nsub, nchan, nbin, **kw)
         c0, c1 = self.chan_range
         self.shape = (int(nsub), c1 - c0, int(nbin))
+        if self._delay is not None:   # the shard's own channels
+            self.set_delays(self._delay)
+
+    def _initial_delays(self, delay):
+        self._delay = delay
 
     def _create(self, device, h):
         if self.group is not None:

@@ -16,7 +16,10 @@ order so that the HIP kernels can reproduce it bit-for-bit:
 * ``pscrunch``: total intensity = f32(pol0 + pol1) for PPQQ / Coherence data,
   pol 0 (= I) for Stokes data; the state becomes "Intensity";
 * ``dedisperse``/``dededisperse``: integer per-channel rotation by
-  ``dm_shift[c]`` bins, ``ded[i] = raw[(i + shift) % nbin]``;
+  ``dm_shift[c]`` bins, ``ded[i] = raw[(i + shift) % nbin]``; an archive made
+  with fractional delays ``dm_delay[c]`` (f64 bins) rotates instead by
+  psrchive's FFT phase rotation, in the arithmetic order written in
+  :mod:`.phase_rotation` (power-of-two nbin);
 * channel sums (baseline total, fscrunch) use the CANONICAL CHANNEL ORDER
   (:func:`chan_sum`): f64, sequential inside super-blocks of ``SUPER_BLOCK``
   channels; the super-block partials are combined by the halving tree of
@@ -149,7 +152,7 @@ class Archive:
     def __init__(self, data, weights=None, dm_shift=None, dedispersed=False,
                  filename="synthetic.ar", source="J0000+0000",
                  centre_frequency=1400.0, mjd_start=60000.0, mjd_end=60000.01,
-                 baseline_duty=BASELINE_DUTY, state=None):
+                 baseline_duty=BASELINE_DUTY, state=None, dm_delay=None):
         data = np.asarray(data, dtype=np.float32)
         if data.ndim != 4:
             raise ValueError("data must be (nsub, npol, nchan, nbin)")
@@ -166,6 +169,12 @@ class Archive:
         if dm_shift is None:
             dm_shift = np.zeros(nchan, dtype=np.int64)
         self._shift = np.mod(np.asarray(dm_shift, dtype=np.int64), nbin).reshape(nchan)
+        self._delay = None
+        if dm_delay is not None:
+            from .phase_rotation import is_supported
+            if not is_supported(nbin):
+                raise ValueError("fractional dedispersion needs a power-of-two nbin (got %d)" % nbin)
+            self._delay = np.array(dm_delay, dtype=np.float64).reshape(nchan)
         self._dedispersed = bool(dedispersed)
         self._filename = filename
         self._source = source
@@ -196,6 +205,15 @@ class Archive:
 
     def get_dm_shift(self) -> np.ndarray:
         return self._shift.copy()
+
+    def get_dm_delay(self):
+        """Fractional per-channel delays in bins (f64), or None for an archive
+        dedispersed by integer shifts."""
+        return None if self._delay is None else self._delay.copy()
+
+    def _rotate(self, data: np.ndarray, sign: int) -> np.ndarray:
+        from .phase_rotation import phasors, rotate
+        return rotate(data, phasors(self.get_nbin(), self._delay), sign)
 
     def get_dedispersed(self) -> bool:
         return self._dedispersed
@@ -241,6 +259,8 @@ class Archive:
         """Samples in the dedispersed frame (a copy if currently dispersed)."""
         if self._dedispersed:
             return self._data
+        if self._delay is not None:
+            return self._rotate(self._data, +1)
         out = np.empty_like(self._data)
         n = self.get_nbin()
         idx = (np.arange(n)[None, :] + self._shift[:, None]) % n
@@ -254,7 +274,10 @@ class Archive:
             self._dedispersed = True
 
     def dededisperse(self) -> None:
-        if self._dedispersed:
+        if self._dedispersed and self._delay is not None:
+            self._data = self._rotate(self._data, -1)
+            self._dedispersed = False
+        elif self._dedispersed:
             n = self.get_nbin()
             out = np.empty_like(self._data)
             idx = (np.arange(n)[None, :] - self._shift[:, None]) % n
@@ -292,6 +315,8 @@ class Archive:
         self._data = np.ascontiguousarray(prof[:, :, None, :])
         self._weights = wsum.astype(np.float32)[:, None]
         self._shift = np.zeros(1, dtype=np.int64)
+        if self._delay is not None:
+            self._delay = np.zeros(1, dtype=np.float64)
 
     def tscrunch(self) -> None:
         nsub = self.get_nsubint()

@@ -9,7 +9,8 @@ Two formats:
   .fits / .sf / .rf;
 * otherwise an uncompressed ``.npz`` container (no pickles) holding ``data``
   (nsub, npol, nchan, nbin) f32, ``weights`` (nsub, nchan) f32, ``dm_shift``
-  (nchan,) i64, ``dedispersed`` (bool scalar) and a JSON ``meta`` string.
+  (nchan,) i64, ``dedispersed`` (bool scalar), a JSON ``meta`` string and,
+  for an archive with fractional delays, ``dm_delay`` (nchan,) f64.
 
 The extension of the path is kept as given (``*.ar`` works for both).
 """
@@ -41,10 +42,11 @@ def save(ar: Archive, path: str) -> None:
         "baseline_duty": ar.get_baseline_duty(),
         "state": ar.get_state(),
     }
+    extra = {} if ar._delay is None else {"dm_delay": ar._delay}
     with open(path, "wb") as fh:
         np.savez(fh, data=ar._data, weights=ar._weights, dm_shift=ar._shift,
                  dedispersed=np.array(ar.get_dedispersed()),
-                 meta=np.array(json.dumps(meta)))
+                 meta=np.array(json.dumps(meta)), **extra)
 
 
 def _npz_member(path: str, name: str, channels):
@@ -91,6 +93,7 @@ def load(path: str, channels=None) -> Archive:
     with np.load(path, allow_pickle=False) as z:
         meta = json.loads(str(z["meta"]))
         weights, shift = z["weights"], z["dm_shift"]
+        delay = z["dm_delay"] if "dm_delay" in z.files else None
         dedispersed = bool(z["dedispersed"])
         data = z["data"] if channels is None else None
     nchan_total = weights.shape[1]
@@ -100,7 +103,8 @@ def load(path: str, channels=None) -> Archive:
             raise ValueError("%s: channel range %s outside [0, %d)" % (path, (c0, c1), nchan_total))
         data = _npz_member(path, "data", (c0, c1))
         weights, shift = weights[:, c0:c1], shift[c0:c1]
-    ar = Archive(data, weights, shift, dedispersed=dedispersed, filename=path,
+        delay = None if delay is None else delay[c0:c1]
+    ar = Archive(data, weights, shift, dedispersed=dedispersed, filename=path, dm_delay=delay,
                  source=meta.get("source", "J0000+0000"),
                  centre_frequency=meta.get("centre_frequency", 1400.0),
                  mjd_start=meta.get("mjd_start", 60000.0),

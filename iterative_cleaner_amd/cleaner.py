@@ -131,6 +131,15 @@ def _dm_shift(ar) -> np.ndarray:
     return out
 
 
+def _dm_delay(ar):
+    """Fractional per-channel delays in bins when the archive dedisperses by
+    psrchive's FFT phase rotation (stand-in archives made with dm_delay), else
+    None (integer shifts, _dm_shift)."""
+    get = getattr(ar, "get_dm_delay", None)
+    d = get() if get is not None else None
+    return None if d is None else np.asarray(d, dtype=np.float64)
+
+
 def _state(ar) -> str:
     """psrchive polarisation state name ("Intensity", "PPQQ", "Coherence",
     "Stokes"); archives without get_state are taken by their npol."""
@@ -171,13 +180,14 @@ def _device() -> int:
 
 
 def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15, nchan_total=None,
-             data_f64=False):
+             data_f64=False, delay=None):
     """Run the GPU loop on a (nsub, nchan, nbin) f32 cube, or on full-polarisation
     data (nsub, npol, nchan, nbin) that the GPU pscrunches; returns the ic_run dict
     (+ ``residual`` when requested).  Under channel sharding (dist.channel_sharding)
     every rank runs its channel shard and gets the merged result: `cube` is then
     either the whole archive (sliced here) or, with ``nchan_total`` set, already
-    this rank's channel slice (read slice-only from the file)."""
+    this rank's channel slice (read slice-only from the file).  ``delay``:
+    fractional per-channel delays (dedispersion by FFT phase rotation)."""
     pols = cube.ndim == 4
     nsub, nchan, nbin = (cube.shape[0], cube.shape[2], cube.shape[3]) if pols else cube.shape
     from .dist import channel_sharding
@@ -193,17 +203,18 @@ def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_d
             c0, c1 = chans[rank]
             cube = cube[:, :, c0:c1] if pols else cube[:, c0:c1]
             w0, shift = np.asarray(w0)[:, c0:c1], np.asarray(shift)[c0:c1]
+            delay = None if delay is None else np.asarray(delay)[c0:c1]
             nchan_total = nchan
         return sharded.clean_cube_dist(
             np.ascontiguousarray(cube), np.ascontiguousarray(w0), np.asarray(shift), (nsub, nchan_total, nbin),
             dev, want_residual=want_residual,
             max_iter=args.max_iter, chanthresh=args.chanthresh, subintthresh=args.subintthresh,
-            pulse_region=args.pulse_region, baseline_duty=baseline_duty, data_f64=data_f64)
+            pulse_region=args.pulse_region, baseline_duty=baseline_duty, data_f64=data_f64, delay=delay)
     if nchan_total is not None and nchan_total != nchan:
         raise ValueError("a channel slice of an archive needs channel sharding")
     with _native.GpuSession(nsub, nchan, nbin, args.max_iter, args.chanthresh, args.subintthresh,
                             args.pulse_region, baseline_duty,
-                            device=_device() if device is None else device, data_f64=data_f64) as s:
+                            device=_device() if device is None else device, data_f64=data_f64, delay=delay) as s:
         if pols:
             s.upload_pols(cube, w0, shift)
         else:
@@ -290,9 +301,10 @@ def clean(ar, args, arch):
 
     cube = _loop_input(ar)
     shift = _dm_shift(ar)
+    delay = _dm_delay(ar)
     duty = ar.get_baseline_duty() if hasattr(ar, "get_baseline_duty") else 0.15
     out = run_loop(cube, orig_weights, shift, args, want_residual=args.unload_res, baseline_duty=duty,
-                   nchan_total=nchan_total, data_f64=_data_f64(ar))
+                   nchan_total=nchan_total, data_f64=_data_f64(ar), delay=delay)
     del cube
 
     x = 0
@@ -333,13 +345,14 @@ def clean(ar, args, arch):
         if args.pscrunch:
             ar.pscrunch()
         shift = _dm_shift(ar)
+        delay = _dm_delay(ar)
     elif not args.pscrunch and not args.memory:
         ar = backend.Archive_load(arch)
     set_weights_archive(ar, avg_test_results)
     if args.bad_chan != 1 or args.bad_subint != 1:
         ar = find_bad_parts(ar, args)
     if args.unload_res and _side_effects:
-        _residual_archive(ar, out["residual"], orig_weights, shift, backend).unload(
+        _residual_archive(ar, out["residual"], orig_weights, shift, backend, delay).unload(
             "%s_residual_%s.ar" % (ar_name, loops))
     if args.print_zap:
         _plot_zap(avg_test_results, ar_name, args)
@@ -350,10 +363,10 @@ def clean(ar, args, arch):
     return ar
 
 
-def _residual_archive(ar, residual, weights, shift, backend):
+def _residual_archive(ar, residual, weights, shift, backend, delay=None):
     """The pulse-free residual archive of the last loop (ic.py:106-108, :161-162)."""
     from .archive import Archive
-    return Archive(residual[:, None], weights, shift, dedispersed=False,
+    return Archive(residual[:, None], weights, shift, dedispersed=False, dm_delay=delay,
                    filename="residual.ar",
                    source=ar.get_source() if hasattr(ar, "get_source") else "J0000+0000")
 

@@ -63,6 +63,7 @@ enum KernelId {
     K_SHARD_PACK,     // pack / assemble / unpack of shard exchanges
     K_EXCHANGE,       // the collectives themselves (host transport or peer copies)
     K_TNORM,          // fit_mode 1: sum(T*T)
+    K_ROTATE,         // fractional dedispersion (FFT phase rotation)
     K_COUNT
 };
 
@@ -189,6 +190,36 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
                           const double *row_med, const double *row_mad, double chanthresh,
                           double subintthresh, double *test, float *W, float *hist, int iter,
                           int32_t *counters);
+// Fractional dedispersion (dedisp_mode IC_DEDISP_FFT; phase_rotation.py):
+// out[p] = rot(f32(in[p] - base[p])) by the channel's phasors, sign +1 =
+// dedisperse, -1 = dededisperse.  Rows p = s*nchan + c of ld_in / ldo floats;
+// out2 (optional) receives a second copy; flags: only subints with
+// flags[s] != 0.  in may equal out (each row is read whole before it is
+// written).  nbin a power of two, 64 .. 4096.
+struct RotateArgs {
+    const float *in;
+    long ld_in;
+    const float *base;          // [P] or nullptr (0)
+    const double2 *ph;          // [nchan][nbin/2 + 1]: exp(+2 pi i fmod(k s_c, nbin) / nbin)
+    int sign;
+    const double2 *tw;          // [nbin]: exp(-2 pi i q / nbin)
+    const int32_t *flags;       // [nsub] or nullptr (all)
+    int nsub, nchan, nbin;
+    float *out;
+    long ldo;
+    float *out2;
+    long ldo2;
+    // residual input (amp != nullptr): row p is f32(amp[p] * T64[i] - in[i])
+    // (x pr_factor on [pr_start, pr_end)), or 0 when info[p] is outside 1-4
+    // (k_residual's arithmetic); base is then unused
+    const double *T64, *amp;
+    const int32_t *info;
+    int pr_on;
+    double pr_factor;
+    int pr_start, pr_end;
+};
+hipError_t launch_rotate(hipStream_t st, const RotateArgs &a);
+bool rotate_supported(int nbin);
 // D == nullptr: fit-cube rows formed from raw and base (fit_mode 1)
 hipError_t launch_residual(hipStream_t st, const float *D, const float *raw, const float *base, const double *T64,
                            const double *amp, const int32_t *info, const int32_t *shift, int nsub, int nchan,

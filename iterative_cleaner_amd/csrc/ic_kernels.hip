@@ -2307,6 +2307,193 @@ __global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, c
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fractional dedispersion: psrchive's FFT phase rotation in the stand-in's
+// written order (phase_rotation.py; oracle orc_rotate).  One block per
+// profile (persistent grid, channel-major so that the blocks in flight share a
+// channel's phasor row in L2); the N/2 complex points live in LDS.
+//   1. z[j] = (f64(f32(x[2j] - b)), f64(f32(x[2j+1] - b)))
+//   2. Z = FFT_{N/2}(z), radix-2 Stockham, register-staged in place
+//   3. pairs (k, N/2 - k): real spectrum, x phasor, inverse half-spectrum (conj)
+//   4. r = FFT_{N/2}(that); out = f32(r.re / M), f32(-r.im / M)
+// Every f64 operation is separately rounded (-ffp-contract=off), so the result
+// is the oracle's bit for bit; the FFT runs its radix-2 stages three at a time
+// in registers (rot_pass), which changes the data movement, not the arithmetic.
+template <int N>
+struct RotCfg {
+    static constexpr int M = N / 2, H = M / 2;
+    static constexpr int LG = N == 64 ? 5 : N == 128 ? 6 : N == 256 ? 7 : N == 512 ? 8 : N == 1024 ? 9
+                                                                              : N == 2048 ? 10 : 11;   // log2 M
+    static constexpr int TB = M / 8 < 64 ? 64 : (M / 8 > 256 ? 256 : M / 8);
+};
+
+// R consecutive radix-2 Stockham stages (ns = 2^lg .. 2^(lg+R-1)) through
+// registers: group ja < G = M/2^R holds the 2^R points v[ja + q G]; the stages
+// run on them as a local Stockham of size 2^R whose butterfly (l, jl) is the
+// global butterfly with k = (jl mod 2^l) * ns + ja mod ns, and the results land
+// at v[(ja / ns) 2^R ns + ja mod ns + p ns].  Same operations, same operands as
+// R separate stages (phase_rotation._stockham), i.e. the same bits, with one
+// LDS round trip instead of R.
+template <int N, int R>
+__device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__ tw, int t, int lg)
+{
+    using C = RotCfg<N>;
+    constexpr int M = C::M, TB = C::TB, G = M >> R, Q = 1 << R, HALF = Q / 2;
+    constexpr int GPT = (G + TB - 1) / TB;
+    const int ns = 1 << lg;
+    double2 u[GPT][Q];
+#pragma unroll
+    for (int gi = 0; gi < GPT; ++gi) {
+        const int ja = t + TB * gi;
+        if (G % TB == 0 || ja < G) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) u[gi][q] = v[ja + q * G];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int gi = 0; gi < GPT; ++gi) {
+        const int ja = t + TB * gi;
+        if (G % TB == 0 || ja < G) {
+            const int k = ja & (ns - 1);
+#pragma unroll
+            for (int l = 0; l < R; ++l) {
+                const int nsl = 1 << l;
+                double2 w2[Q];
+#pragma unroll
+                for (int jl = 0; jl < HALF; ++jl) {
+                    const int kl = jl & (nsl - 1);
+                    const double2 w = tw[(kl * ns + k) * (N >> (l + lg + 1))];
+                    const double2 a = u[gi][jl], b = u[gi][jl + HALF];
+                    const double tr = w.x * b.x - w.y * b.y;
+                    const double ti = w.x * b.y + w.y * b.x;
+                    const int o = 2 * jl - kl;
+                    w2[o] = make_double2(a.x + tr, a.y + ti);
+                    w2[o + nsl] = make_double2(a.x - tr, a.y - ti);
+                }
+#pragma unroll
+                for (int q = 0; q < Q; ++q) u[gi][q] = w2[q];
+            }
+            const int base = ((ja >> lg) << (lg + R)) + k;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) v[base + q * ns] = u[gi][q];
+        }
+    }
+    __syncthreads();
+}
+
+// the full N/2-point FFT: passes of 3 stages (the last one shorter)
+template <int N, int LG0 = 0>
+__device__ __forceinline__ void rot_fft(double2 *v, const double2 *__restrict__ tw, int t)
+{
+    constexpr int LG = RotCfg<N>::LG;
+    if constexpr (LG0 < LG) {
+        constexpr int R = LG - LG0 >= 3 ? 3 : LG - LG0;
+        rot_pass<N, R>(v, tw, t, LG0);
+        rot_fft<N, LG0 + R>(v, tw, t);
+    }
+}
+
+// real spectrum bin from the half-length transform: za = Z_a, zb = Z_{M-a}, w = W^a
+__device__ __forceinline__ double2 rot_post(double2 za, double2 zb, double2 w)
+{
+    const double er = (za.x + zb.x) * 0.5, ei = (za.y - zb.y) * 0.5;
+    const double dr = za.x - zb.x, di = za.y + zb.y;
+    const double orr = di * 0.5, oi = -(dr * 0.5);
+    return make_double2(er + (w.x * orr - w.y * oi), ei + (w.x * oi + w.y * orr));
+}
+
+// half-length input of the inverse from ya = Y_a, yb = Y_{M-a}, w = W^a
+__device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
+{
+    const double er = (ya.x + yb.x) * 0.5, ei = (ya.y - yb.y) * 0.5;
+    const double hr = (ya.x - yb.x) * 0.5, hi = (ya.y + yb.y) * 0.5;
+    const double orr = hr * w.x + hi * w.y, oi = hi * w.x - hr * w.y;
+    return make_double2(er - oi, ei + orr);
+}
+
+template <int N>
+__global__ __launch_bounds__(RotCfg<N>::TB) void k_rotate(RotateArgs a)
+{
+    using C = RotCfg<N>;
+    constexpr int M = C::M, H = C::H, TB = C::TB;
+    __shared__ double2 v[M];
+    const int t = threadIdx.x;
+    const unsigned nsub = (unsigned)a.nsub, nchan = (unsigned)a.nchan;
+    const size_t P = (size_t)nsub * nchan;
+    const double sg = a.sign > 0 ? 1.0 : -1.0;
+    const double inv = 1.0 / (double)M;
+    for (size_t item = blockIdx.x; item < P; item += gridDim.x) {
+        const unsigned c = (unsigned)(item / nsub), s = (unsigned)(item % nsub);
+        if (a.flags && a.flags[s] == 0) continue;            // uniform over the block
+        const size_t p = (size_t)s * nchan + c;
+        const float *x = a.in + p * (size_t)a.ld_in;
+        if (a.amp) {
+            // the residual of the exact fit (k_residual), formed on the fly
+            const int st = a.info[p];
+            const bool ok = st >= 1 && st <= 4;
+            const double am = a.amp[p];
+            for (int j = t; j < M; j += TB) {
+                const float2 q = *(const float2 *)(x + 2 * j);
+                float r[2] = {0.0f, 0.0f};
+                if (ok) {
+                    const float pv[2] = {q.x, q.y};
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int i = 2 * j + e;
+                        const double uu = am * a.T64[i];
+                        double d = uu - (double)pv[e];
+                        if (a.pr_on && i >= a.pr_start && i < a.pr_end) d = d * a.pr_factor;
+                        r[e] = (float)d;
+                    }
+                }
+                v[j] = make_double2((double)r[0], (double)r[1]);
+            }
+        } else {
+            const float b = a.base ? a.base[p] : 0.0f;
+            for (int j = t; j < M; j += TB) {
+                const float2 q = *(const float2 *)(x + 2 * j);
+                const float x0 = q.x - b, x1 = q.y - b;
+                v[j] = make_double2((double)x0, (double)x1);
+            }
+        }
+        __syncthreads();
+        rot_fft<N>(v, a.tw, t);
+        const double2 *ph = a.ph + (size_t)c * (M + 1);
+        for (int k = t; k <= H; k += TB) {
+            if (k == 0) {
+                const double2 z = v[0];
+                const double X0 = z.x + z.y, XM = z.x - z.y;
+                const double Y0 = X0 * ph[0].x, YM = XM * ph[M].x;
+                v[0] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
+            } else {
+                const int q = M - k;
+                const double2 zk = v[k], zq = v[q];
+                const double2 wk = a.tw[k], wq = a.tw[q];
+                const double2 Xk = rot_post(zk, zq, wk), Xq = rot_post(zq, zk, wq);
+                const double2 pk = ph[k], pq = ph[q];
+                const double pki = sg * pk.y, pqi = sg * pq.y;
+                const double2 Yk = make_double2(Xk.x * pk.x - Xk.y * pki, Xk.x * pki + Xk.y * pk.x);
+                const double2 Yq = make_double2(Xq.x * pq.x - Xq.y * pqi, Xq.x * pqi + Xq.y * pq.x);
+                const double2 Zk = rot_pre(Yk, Yq, wk), Zq = rot_pre(Yq, Yk, wq);
+                v[q] = make_double2(Zq.x, -Zq.y);
+                v[k] = make_double2(Zk.x, -Zk.y);
+            }
+        }
+        __syncthreads();
+        rot_fft<N>(v, a.tw, t);
+        float *o = a.out + p * (size_t)a.ldo;
+        float *o2 = a.out2 ? a.out2 + p * (size_t)a.ldo2 : nullptr;
+        for (int j = t; j < M; j += TB) {
+            const double2 r = v[j];
+            const float2 y = make_float2((float)(r.x * inv), (float)((-r.y) * inv));
+            *(float2 *)(o + 2 * j) = y;
+            if (o2) *(float2 *)(o2 + 2 * j) = y;
+        }
+        __syncthreads();   // v is reused by the block's next profile
+    }
+}
+
 // TT = numpy pairwise sum of T64[i]^2 (fit_mode 1's denominator), one wave
 __global__ __launch_bounds__(64) void k_tnorm(const double *__restrict__ T64, const PwPlan *__restrict__ plan,
                                               double *__restrict__ TT)
@@ -2970,10 +3157,8 @@ static hipError_t launch_p2(hipStream_t st, const DiagArgs &a, size_t P)
         hipLaunchKernelGGL((k_diag_p2<NN, DIAG_EXACT, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     else if (a.mode == DIAG_CLOSED)
         hipLaunchKernelGGL((k_diag_p2<NN, DIAG_CLOSED, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
-    else if (!D64)   // comprehensive_stats alone takes f32 data
-        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_STATS, false>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
-    else
-        return hipErrorInvalidValue;
+    else   // comprehensive_stats of given rows (f64 data: the fractional-dedispersion loop)
+        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_STATS, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     return hipGetLastError();
 }
 
@@ -3070,6 +3255,35 @@ hipError_t launch_residual(hipStream_t st, const float *D, const float *raw, con
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
     hipLaunchKernelGGL(k_residual, dim3(grid), dim3(256), 0, st, D, raw, base, T64, amp, info, shift, P, nchan, nbin,
                        ldD, pr_on, pr_factor, pr_start, pr_end, R);
+    return hipGetLastError();
+}
+
+bool rotate_supported(int nbin)
+{
+    switch (nbin) {
+    case 64: case 128: case 256: case 512: case 1024: case 2048: case 4096: return true;
+    default: return false;
+    }
+}
+
+hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
+{
+    const size_t P = (size_t)a.nsub * a.nchan;
+    if (P == 0) return hipSuccess;
+    if (!rotate_supported(a.nbin) || !a.in || !a.out || !a.ph || !a.tw || a.ld_in < a.nbin || a.ldo < a.nbin ||
+        (a.ld_in & 1) || (a.ldo & 1) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 1))) ||
+        (a.amp && (!a.T64 || !a.info)))
+        return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::min<size_t>(P, 16384);
+#define IC_ROT(NN)                                                                                 \
+    case NN:                                                                                       \
+        hipLaunchKernelGGL(k_rotate<NN>, dim3(grid), dim3(RotCfg<NN>::TB), 0, st, a);              \
+        break;
+    switch (a.nbin) {
+        IC_ROT(64) IC_ROT(128) IC_ROT(256) IC_ROT(512) IC_ROT(1024) IC_ROT(2048) IC_ROT(4096)
+    default: return hipErrorInvalidValue;
+    }
+#undef IC_ROT
     return hipGetLastError();
 }
 

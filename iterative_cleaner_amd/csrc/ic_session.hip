@@ -47,7 +47,7 @@ const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",
                                      "k_fscrunch",      "k_tscrunch",  "k_fit_pass", "k_fit_state",
                                      "k_diag",          "k_linestats", "k_combine",  "k_residual",
                                      "k_fit_tail",      "k_sb_tree",   "k_shard_pack", "exchange",
-                                     "k_tnorm"};
+                                     "k_tnorm",         "k_rotate"};
 
 constexpr int kMaxRounds = 1024;      // lmdif rounds per fit (maxfev = 400 bounds it far below)
 constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
@@ -118,6 +118,14 @@ struct Session {
     long tail_threshold = kTailProfiles;
     ic_run_stats stats{};
     std::vector<int32_t> bad_fits;   // per iteration of the last run: fit statuses outside 1-4
+    // fractional dedispersion (dedisp_mode IC_DEDISP_FFT): the dedispersed raw
+    // cube rot(raw), the template stage's rot(f32(raw - base)) (carried rows),
+    // the residual scratch, zero shifts/levels for the shift-indexed kernels,
+    // and the phasor table [nchan][nbin/2 + 1] of ic_set_delays
+    bool fftded = false, delays_set = false;
+    float *dr = nullptr, *Tc = nullptr, *R = nullptr, *zbase = nullptr;
+    int32_t *zshift = nullptr;
+    double2 *ph = nullptr;
     // timing
     bool timing = false;
     std::vector<Timed> events;
@@ -244,7 +252,7 @@ void free_all(Session *s)
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
-                    s->wflag, s->TT};
+                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     void *rbufs[] = {s->std_r, s->mean_r, s->fft_r, s->ptp_r, s->valid_r};
@@ -393,6 +401,57 @@ int scrunch_stage(Session *s)
     return 0;
 }
 
+// phasors exp(+2 pi i fmod(k s_c, nbin) / nbin), k <= nbin/2, in x87 long double
+// (phase_rotation.py phasors; oracle orc_phasors)
+std::vector<double2> make_phasors(int nbin, int nchan, const double *delay)
+{
+    const long double pi = 3.141592653589793238462643383279502884L;
+    const int m = nbin / 2;
+    std::vector<double2> ph((size_t)nchan * (m + 1));
+    for (int c = 0; c < nchan; ++c)
+        for (int k = 0; k <= m; ++k) {
+            const long double t = fmodl((long double)k * (long double)delay[c], (long double)nbin);
+            const long double ang = 2.0L * pi * t / (long double)nbin;
+            ph[(size_t)c * (m + 1) + k] = make_double2((double)cosl(ang), (double)sinl(ang));
+        }
+    return ph;
+}
+
+RotateArgs rotate_args(Session *s, const float *in, const float *base, int sign, const int32_t *flags, float *out,
+                       long ldo)
+{
+    RotateArgs a{};
+    a.in = in;
+    a.ld_in = s->p.nbin;
+    a.base = base;
+    a.ph = s->ph;
+    a.sign = sign;
+    a.tw = s->tw;
+    a.flags = flags;
+    a.nsub = s->p.nsub;
+    a.nchan = s->nchan;
+    a.nbin = s->p.nbin;
+    a.out = out;
+    a.ldo = ldo;
+    return a;
+}
+
+// the iteration's residual rows f32(a T - D) (remove_profile1d, ic.py:277-288),
+// rotated back to the dispersed frame (dededisperse, ic.py:104) -> s->R
+RotateArgs residual_rotate_args(Session *s, int pr_start, int pr_end)
+{
+    RotateArgs a = rotate_args(s, s->D, nullptr, -1, nullptr, s->R, s->p.nbin);
+    a.ld_in = s->ldD;
+    a.T64 = s->T64;
+    a.amp = s->amp;
+    a.info = s->info;
+    a.pr_on = s->p.pr_on;
+    a.pr_factor = s->p.pr_factor;
+    a.pr_start = pr_start;
+    a.pr_end = pr_end;
+    return a;
+}
+
 // fit-cube preparation (iterative_cleaner.py:96-100): baseline with w0, dedisperse.
 // The w0 baseline (window + per-profile levels) is also the template stage's
 // baseline of the first iteration (W == w0).  A shard also hands the validity
@@ -409,6 +468,25 @@ int prepare(Session *s)
         CM(s, s->comm->alltoallv(s->xd_send, s->vsb.data(), s->xd_recv, s->vrb.data(), s->stream), "valid rows");
         LAUNCH(s, K_SHARD_PACK,
                launch_assemble_rows(s->stream, s->geom, s->xd_recv, nullptr, nullptr, nullptr, nullptr, s->valid_r));
+    }
+    if (s->fftded) {
+        // remove_baseline reads the dedispersed view rot(raw) (archive.py
+        // _ded_view); dedisperse then rotates the data it leaves, f32(raw - base0):
+        // that is the fit cube D and iteration 1's template rows Tc (W == w0)
+        LAUNCH(s, K_ROTATE, launch_rotate(s->stream, rotate_args(s, s->raw, nullptr, +1, nullptr, s->dr, nbin)));
+        LAUNCH(s, K_CHAN_PARTIALS,
+               launch_chan_partials(s->stream, 0, s->dr, s->w0, s->zshift, nullptr, nullptr, nsub, nchan, nbin,
+                                    s->part, nullptr, nullptr));
+        if (int rc = window_stage(s, nullptr)) return rc;
+        LAUNCH(s, K_BASE,
+               launch_base(s->stream, s->dr, s->zshift, s->win, nullptr, nsub, nchan, nbin, s->width, s->base0));
+        RotateArgs ra = rotate_args(s, s->raw, s->base0, +1, nullptr, s->Tc, nbin);
+        ra.out2 = s->D;
+        ra.ldo2 = s->ldD;
+        LAUNCH(s, K_ROTATE, launch_rotate(s->stream, ra));
+        CK(hipMemcpyAsync(s->base, s->base0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
+        CK(hipMemsetAsync(s->wflag + nsub, 0, sizeof(int32_t), s->stream));
+        return 0;
     }
     LAUNCH(s, K_CHAN_PARTIALS,
            launch_chan_partials(s->stream, 0, s->raw, s->w0, s->shift, nullptr, nullptr, nsub, nchan, nbin, s->part,
@@ -434,6 +512,25 @@ int prepare(Session *s)
 int iteration_template(Session *s, int iter)
 {
     const int nsub = s->p.nsub, nchan = s->nchan, nbin = s->p.nbin;
+    if (s->fftded) {
+        // FFT dedispersion: the window totals and levels read rot(raw); the rows
+        // rot(f32(raw - base)) of subints whose window moved are re-rotated, and
+        // the fscrunch partials are taken over those rows (no shift, no level)
+        if (iter > 1) {
+            LAUNCH(s, K_CHAN_PARTIALS,
+                   launch_chan_partials(s->stream, 0, s->dr, s->W, s->zshift, nullptr, nullptr, nsub, nchan, nbin,
+                                        s->part, nullptr, nullptr));
+            if (int rc = window_stage(s, s->wflag)) return rc;
+            LAUNCH(s, K_BASE,
+                   launch_base(s->stream, s->dr, s->zshift, s->win, s->wflag, nsub, nchan, nbin, s->width, s->base));
+            LAUNCH(s, K_ROTATE,
+                   launch_rotate(s->stream, rotate_args(s, s->raw, s->base, +1, s->wflag, s->Tc, nbin)));
+        }
+        LAUNCH(s, K_CHAN_PARTIALS,
+               launch_chan_partials(s->stream, 1, s->Tc, s->W, s->zshift, s->zbase, nullptr, nsub, nchan, nbin,
+                                    nullptr, s->part2, s->wpart));
+        return scrunch_stage(s);
+    }
     if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s; also writes D (exact fit)
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, s->D ? 3 : 1, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan,
@@ -588,6 +685,12 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (p.max_iter < 0) return fail(IC_EINVAL, "max_iter < 0");
     if (p.fit_mode != IC_FIT_EXACT && p.fit_mode != IC_FIT_CLOSED)
         return fail(IC_EINVAL, "fit_mode %d unsupported", p.fit_mode);
+    if (p.dedisp_mode != IC_DEDISP_SHIFT && p.dedisp_mode != IC_DEDISP_FFT)
+        return fail(IC_EINVAL, "dedisp_mode %d unsupported", p.dedisp_mode);
+    if (p.dedisp_mode == IC_DEDISP_FFT && !rotate_supported(p.nbin))
+        return fail(IC_EINVAL, "fractional dedispersion needs a power-of-two nbin in 64..4096 (nbin=%d)", p.nbin);
+    if (p.dedisp_mode == IC_DEDISP_FFT && p.fit_mode != IC_FIT_EXACT)
+        return fail(IC_EINVAL, "fractional dedispersion is implemented for the exact fit (fit_mode 0) only");
     if (diag_lds_bytes(p.nbin) > 160 * 1024)
         return fail(IC_EINVAL, "nbin=%d needs %zu bytes of LDS for the diagnostics (> 160 KiB)", p.nbin,
                     diag_lds_bytes(p.nbin));
@@ -656,6 +759,18 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
             return bail(fail(IC_EHIP, "hipMemset(D) failed"));
     }
     AL(s->TT, 1);
+    s->fftded = p.dedisp_mode == IC_DEDISP_FFT;
+    if (s->fftded) {
+        AL(s->dr, N);
+        AL(s->Tc, N);
+        AL(s->R, N);
+        AL(s->zbase, P);
+        AL(s->zshift, (size_t)nchan);
+        AL(s->ph, (size_t)nchan * (nbin / 2 + 1));
+        if (hipMemset(s->zbase, 0, sizeof(float) * P) != hipSuccess ||
+            hipMemset(s->zshift, 0, sizeof(int32_t) * nchan) != hipSuccess)
+            return bail(fail(IC_EHIP, "hipMemset(zero levels / shifts) failed"));
+    }
     AL(s->slot_w0[0], P);
     s->w0 = s->slot_w0[0];
     AL(s->W, P);
@@ -1032,6 +1147,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         s->ran = false;
     }
     if (!s->uploaded) return fail(IC_ESTATE, "ic_run before ic_upload");
+    if (s->fftded && !s->delays_set) return fail(IC_ESTATE, "ic_run before ic_set_delays (dedisp_mode FFT)");
     const ic_params &p = s->p;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
     int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > nbin ? nbin : p.pr_start);
@@ -1066,6 +1182,14 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             if (int rc = run_fit(s)) return rc;
         } else {
             LAUNCH(s, K_TNORM, launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
+        }
+        if (s->fftded) {
+            // residual in the dedispersed frame, dededispersed by the inverse
+            // rotation (ic.py:101-104), then comprehensive_stats of those rows
+            LAUNCH(s, K_ROTATE, launch_rotate(s->stream, residual_rotate_args(s, pr_start, pr_end)));
+            da.mode = DIAG_STATS;
+            da.D = s->R;
+            da.ldD = nbin;
         }
         LAUNCH(s, K_DIAG, launch_diag(s->stream, da));
         // channel medians are local to a shard; row medians need whole rows
@@ -1143,12 +1267,88 @@ int ic_get_residual(void *session, float *out)
     // temporary output buffer
     float *R = nullptr;
     CK(hipMalloc((void **)&R, sizeof(float) * s->N));
-    hipError_t e = launch_residual(s->stream, s->D, s->raw, s->base0, s->T64, s->amp, s->info, s->shift, p.nsub,
-                                   s->nchan, p.nbin, s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, R);
+    hipError_t e;
+    if (s->fftded) {   // residual + dededisperse (the inverse rotation) in one pass
+        RotateArgs ra = residual_rotate_args(s, pr_start, pr_end);
+        ra.out = R;
+        e = launch_rotate(s->stream, ra);
+    } else {
+        e = launch_residual(s->stream, s->D, s->raw, s->base0, s->T64, s->amp, s->info, s->shift, p.nsub, s->nchan,
+                            p.nbin, s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, R);
+    }
     if (e == hipSuccess) e = hipMemcpyAsync(out, R, sizeof(float) * s->N, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     (void)hipFree(R);
     if (e != hipSuccess) return fail(IC_EHIP, "residual: %s", hipGetErrorString(e));
+    return IC_OK;
+}
+
+int ic_set_delays(void *session, const double *delay_bins)
+{
+    Session *s = (Session *)session;
+    if (!s || !delay_bins) return fail(IC_EINVAL, "null argument");
+    if (!s->fftded) return fail(IC_ESTATE, "ic_set_delays on a session with dedisp_mode %d", s->p.dedisp_mode);
+    for (int c = 0; c < s->nchan; ++c)
+        if (!isfinite(delay_bins[c])) return fail(IC_EINVAL, "delay[%d] is not finite", c);
+    CK(hipSetDevice(s->device));
+    const std::vector<double2> ph = make_phasors(s->p.nbin, s->nchan, delay_bins);
+    CK(hipMemcpyAsync(s->ph, ph.data(), sizeof(double2) * ph.size(), hipMemcpyHostToDevice, s->stream));
+    CK(hipStreamSynchronize(s->stream));
+    s->delays_set = true;
+    return IC_OK;
+}
+
+int ic_rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, const double *delay_bins,
+                       int sign, float *out)
+{
+    if (!in || !delay_bins || !out || nsub <= 0 || nchan <= 0) return fail(IC_EINVAL, "bad argument");
+    if (!rotate_supported(nbin))
+        return fail(IC_EINVAL, "fractional dedispersion needs a power-of-two nbin in 64..4096 (nbin=%d)", nbin);
+    if (sign != 1 && sign != -1) return fail(IC_EINVAL, "sign must be +1 or -1");
+    for (int c = 0; c < nchan; ++c)
+        if (!isfinite(delay_bins[c])) return fail(IC_EINVAL, "delay[%d] is not finite", c);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(IC_EHIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
+    CK(hipSetDevice(device));
+    const size_t N = (size_t)nsub * nchan * nbin;
+    const std::vector<double2> ph = make_phasors(nbin, nchan, delay_bins);
+    std::vector<double2> tw(nbin);
+    for (int q = 0; q < nbin; ++q) {
+        const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)q / (long double)nbin;
+        tw[q] = make_double2((double)cosl(ang), (double)sinl(ang));
+    }
+    float *d = nullptr;
+    double2 *dph = nullptr, *dtw = nullptr;
+    hipStream_t st = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc((void **)&d, sizeof(float) * N);
+    if (e == hipSuccess) e = hipMalloc((void **)&dph, sizeof(double2) * ph.size());
+    if (e == hipSuccess) e = hipMalloc((void **)&dtw, sizeof(double2) * tw.size());
+    if (e == hipSuccess) e = hipMemcpyAsync(d, in, sizeof(float) * N, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(dph, ph.data(), sizeof(double2) * ph.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(dtw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        RotateArgs a{};
+        a.in = d;
+        a.ld_in = nbin;
+        a.ph = dph;
+        a.sign = sign;
+        a.tw = dtw;
+        a.nsub = nsub;
+        a.nchan = nchan;
+        a.nbin = nbin;
+        a.out = d;
+        a.ldo = nbin;
+        e = launch_rotate(st, a);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, sizeof(float) * N, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (d) (void)hipFree(d);
+    if (dph) (void)hipFree(dph);
+    if (dtw) (void)hipFree(dtw);
+    if (st) (void)hipStreamDestroy(st);
+    if (e != hipSuccess) return fail(IC_EHIP, "ic_rotate_profiles: %s", hipGetErrorString(e));
     return IC_OK;
 }
 

@@ -1,0 +1,172 @@
+"""Fractional dedispersion of the archive stand-in: psrchive's FFT phase rotation
+with a written, reproducible arithmetic order.
+
+psrchive dedisperses a profile by rotating it in phase through its Fourier
+transform (Pulsar::Profile::rotate_phase -> fft::shift: forward real FFT,
+multiply harmonic k by exp(i 2 pi k s / nbin), inverse real FFT, 1/nbin).  The
+reference calls it through ``dedisperse()`` / ``dededisperse()``
+(iterative_cleaner.py:91, :100, :104).  psrchive is absent here, so real-data
+parity is unpinned; this module DEFINES the stand-in's rotation so that the
+GPU kernel (k_rotate, ic_kernels.hip), the C restatement the tests check
+against (orc_rotate in the oracle/ directory) and this numpy version agree bit for
+bit.  It equals numpy's
+``irfft(rfft(x) * exp(2j pi k s / N))`` to within one f32 ulp (see
+oracle/restated.py fft_phase_shift and tests/test_phase_rotation.py).
+
+Definition, for a profile x of N = 2M samples (N a power of two) and a delay
+of s bins (``y[j] = x[j + s]`` for integer s; ``dedisperse`` rotates by +s,
+``dededisperse`` by -s):
+
+1. x' = f32(x - base) (base 0 when no baseline is subtracted), then
+   z[j] = (f64(x'[2j]), f64(x'[2j+1])), j < M.
+2. Z = FFT_M(z): radix-2 Stockham autosort, stages Ns = 1, 2, .., M/2; for
+   butterfly j < M/2: k = j mod Ns, a = z[j], b = z[j + M/2],
+   w = tw[k * N/(2 Ns)], t = (w.r b.r - w.i b.i, w.r b.i + w.i b.r),
+   out[2j - k] = a + t, out[2j - k + Ns] = a - t.
+3. For k = 1 .. M/2, q = M - k: the real spectrum X_k and X_q
+   (post(Z_k, Z_q, tw[k]) and post(Z_q, Z_k, tw[q])), the phasors
+   Y = X * (P.r, sign * P.i), then the half-length spectrum of the inverse
+   (pre(Y_k, Y_q, tw[k]), pre(Y_q, Y_k, tw[q])), stored conjugated.
+   DC and Nyquist: X_0 = Z_0.r + Z_0.i, X_M = Z_0.r - Z_0.i (real),
+   Y_0 = X_0 P_0.r, Y_M = X_M P_M.r, stored (Y_0 + Y_M)/2, -((Y_0 - Y_M)/2).
+4. r = FFT_M(stored) (same stages); out[2j] = f32(r[j].r * (1/M)),
+   out[2j+1] = f32((-r[j].i) * (1/M)).
+
+Every step is a single IEEE f64 operation in the written order (no fused
+multiply-add).  Tables: tw[q] = exp(-2 pi i q / N) and
+P_c[k] = exp(+2 pi i fmod(k s_c, N) / N), evaluated in x87 long double
+(cosl/sinl) and rounded to f64, exactly as the C library builds them
+(ic_session.hip).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+__all__ = ["PI_L", "twiddles", "phasors", "rotate", "is_supported"]
+
+PI_L = np.longdouble("3.141592653589793238462643383279502884")
+
+
+def is_supported(nbin: int) -> bool:
+    """The rotation needs a power-of-two nbin (the GPU kernel: 64 .. 4096)."""
+    return nbin >= 4 and (nbin & (nbin - 1)) == 0
+
+
+def twiddles(nbin: int) -> np.ndarray:
+    """(2, nbin) f64: cos / sin of -2 pi q / nbin (long double, then f64)."""
+    q = np.arange(nbin).astype(np.longdouble)
+    ang = (np.longdouble(-2.0) * PI_L) * q / np.longdouble(nbin)
+    return np.stack([np.cos(ang).astype(np.float64), np.sin(ang).astype(np.float64)])
+
+
+def phasors(nbin: int, delays) -> np.ndarray:
+    """(2, nchan, nbin/2 + 1) f64: exp(+2 pi i fmod(k s_c, nbin) / nbin)."""
+    m = nbin // 2
+    k = np.arange(m + 1).astype(np.longdouble)
+    s = np.asarray(delays, dtype=np.float64).reshape(-1).astype(np.longdouble)
+    t = np.fmod(k[None, :] * s[:, None], np.longdouble(nbin))
+    ang = (np.longdouble(2.0) * PI_L) * t / np.longdouble(nbin)
+    return np.stack([np.cos(ang).astype(np.float64), np.sin(ang).astype(np.float64)])
+
+
+def _stockham(vr: np.ndarray, vi: np.ndarray, tw: np.ndarray):
+    m = vr.shape[-1]
+    n = 2 * m
+    h = m // 2
+    j = np.arange(h)
+    ns = 1
+    while ns < m:
+        k = j & (ns - 1)
+        idx = k * (n // (2 * ns))
+        wr, wi = tw[0][idx], tw[1][idx]
+        ar, ai, br, bi = vr[..., :h], vi[..., :h], vr[..., h:], vi[..., h:]
+        tr = wr * br - wi * bi
+        ti = wr * bi + wi * br
+        o = 2 * j - k
+        nr = np.empty_like(vr)
+        ni = np.empty_like(vi)
+        nr[..., o] = ar + tr
+        ni[..., o] = ai + ti
+        nr[..., o + ns] = ar - tr
+        ni[..., o + ns] = ai - ti
+        vr, vi = nr, ni
+        ns *= 2
+    return vr, vi
+
+
+def _post(zar, zai, zbr, zbi, wr, wi):
+    er = (zar + zbr) * 0.5
+    ei = (zai - zbi) * 0.5
+    dr = zar - zbr
+    di = zai + zbi
+    orr = di * 0.5
+    oi = -(dr * 0.5)
+    return er + (wr * orr - wi * oi), ei + (wr * oi + wi * orr)
+
+
+def _pre(yar, yai, ybr, ybi, wr, wi):
+    er = (yar + ybr) * 0.5
+    ei = (yai - ybi) * 0.5
+    hr = (yar - ybr) * 0.5
+    hi = (yai + ybi) * 0.5
+    orr = hr * wr + hi * wi
+    oi = hi * wr - hr * wi
+    return er - oi, ei + orr
+
+
+def rotate(x: np.ndarray, ph: np.ndarray, sign: int, tw: np.ndarray | None = None,
+           base: np.ndarray | None = None) -> np.ndarray:
+    """Rotate profiles x (..., nchan, nbin) f32 by their channel's delay.
+
+    ph: phasors(nbin, delays) for the nchan channels (axis -2 of x); sign +1 =
+    dedisperse (y[j] = x[j + s]), -1 = dededisperse; base (..., nchan) f32 is
+    subtracted first in f32 (remove_baseline's levels)."""
+    x = np.asarray(x, dtype=np.float32)
+    n = x.shape[-1]
+    if not is_supported(n):
+        raise ValueError("fractional dedispersion needs a power-of-two nbin (got %d)" % n)
+    if tw is None:
+        tw = twiddles(n)
+    with np.errstate(invalid="ignore", over="ignore"):   # NaN / Inf samples propagate
+        return _rotate(x, ph, sign, tw, base)
+
+
+def _rotate(x, ph, sign, tw, base):
+    n = x.shape[-1]
+    if base is not None:
+        x = (x - np.asarray(base, dtype=np.float32)[..., None]).astype(np.float32)
+    m = n // 2
+    vr = x[..., 0::2].astype(np.float64)
+    vi = x[..., 1::2].astype(np.float64)
+    vr, vi = _stockham(vr, vi, tw)
+    pr = ph[0]
+    pi = ph[1] if sign > 0 else -ph[1]
+    k = np.arange(1, m // 2 + 1)
+    q = m - k
+    zkr, zki, zqr, zqi = vr[..., k], vi[..., k], vr[..., q], vi[..., q]
+    xkr, xki = _post(zkr, zki, zqr, zqi, tw[0][k], tw[1][k])
+    xqr, xqi = _post(zqr, zqi, zkr, zki, tw[0][q], tw[1][q])
+    ykr = xkr * pr[..., k] - xki * pi[..., k]
+    yki = xkr * pi[..., k] + xki * pr[..., k]
+    yqr = xqr * pr[..., q] - xqi * pi[..., q]
+    yqi = xqr * pi[..., q] + xqi * pr[..., q]
+    zkr2, zki2 = _pre(ykr, yki, yqr, yqi, tw[0][k], tw[1][k])
+    zqr2, zqi2 = _pre(yqr, yqi, ykr, yki, tw[0][q], tw[1][q])
+    x0 = vr[..., 0] + vi[..., 0]
+    xm = vr[..., 0] - vi[..., 0]
+    y0 = x0 * pr[..., 0]
+    ym = xm * pr[..., m]
+    ur = np.empty_like(vr)
+    ui = np.empty_like(vi)
+    ur[..., 0] = (y0 + ym) * 0.5
+    ui[..., 0] = -((y0 - ym) * 0.5)
+    ur[..., q] = zqr2
+    ui[..., q] = -zqi2
+    ur[..., k] = zkr2      # k = M/2 pairs with itself: both expressions agree
+    ui[..., k] = -zki2
+    rr, ri = _stockham(ur, ui, tw)
+    inv = 1.0 / m
+    out = np.empty(x.shape, dtype=np.float32)
+    out[..., 0::2] = (rr * inv).astype(np.float32)
+    out[..., 1::2] = ((-ri) * inv).astype(np.float32)
+    return out

@@ -12,9 +12,11 @@ Samples are int16 with a per-(subint, pol, channel) scale and offset:
 value = f32(f32(DATA) * DAT_SCL + DAT_OFFS), the decoding psrchive applies.
 The stand-in's own metadata rides in extra keywords / one extra column that
 other PSRFITS readers ignore: IC_SHIFT (nchan J, integer dedispersion delays in
-bins), IC_DEDSP (dedispersed flag), IC_DUTY (baseline duty), IC_MJDE (end
-MJD).  Files without IC_SHIFT get integer delays from DM, DAT_FREQ and PERIOD
-(the same integer approximation cleaner._dm_shift makes for real psrchive).
+bins), IC_DELAY (nchan D, fractional delays in bins of an archive dedispersed
+by FFT phase rotation), IC_DEDSP (dedispersed flag), IC_DUTY (baseline duty),
+IC_MJDE (end MJD).  Files without IC_SHIFT get integer delays from DM, DAT_FREQ
+and PERIOD (the same integer approximation cleaner._dm_shift makes for real
+psrchive), or, with IC_DEDISPERSION=fft, the exact fractional delays.
 """
 from __future__ import annotations
 
@@ -140,6 +142,14 @@ def decode(q: np.ndarray, scl: np.ndarray, offs: np.ndarray) -> np.ndarray:
     return (q.astype(np.float32) * scl[..., None] + offs[..., None]).astype(np.float32)
 
 
+def fractional_dedispersion() -> bool:
+    """IC_DEDISPERSION=fft: archives whose delays come from DM / DAT_FREQ /
+    PERIOD are dedispersed by psrchive's FFT phase rotation with the exact
+    fractional delay (phase_rotation.py) instead of the rounded integer shift."""
+    import os
+    return os.environ.get("IC_DEDISPERSION", "").strip().lower() == "fft"
+
+
 # ------------------------------------------------------------------ write
 def save(ar, path: str, stand_in_meta: bool = True) -> None:
     """Write `ar` as fold-mode PSRFITS (stand_in_meta=False: standard columns
@@ -166,8 +176,10 @@ def save(ar, path: str, stand_in_meta: bool = True) -> None:
             ("DATA", "%dI" % (nbin * nchan * npol), "(%d,%d,%d)" % (nbin, nchan, npol),
              (nsub, npol * nchan * nbin), qd.reshape(nsub, -1)),
             ("IC_SHIFT", "%dJ" % nchan, None, (nsub, nchan), np.broadcast_to(ar._shift, (nsub, nchan)))]
+    if getattr(ar, "_delay", None) is not None:
+        cols.append(("IC_DELAY", "%dD" % nchan, None, (nsub, nchan), np.broadcast_to(ar._delay, (nsub, nchan))))
     if not stand_in_meta:
-        cols = cols[:-1]
+        cols = cols[:8]
     fields = []
     for name, form, _, _, _ in cols:
         rep = int(form[:-1] or 1)
@@ -282,11 +294,16 @@ def load(path: str, channels=None):
     period = float(np.asarray(rows["PERIOD"]).reshape(-1)[0]) if "PERIOD" in dt.names else 1.0
     cfreq = float(primary.get("OBSFREQ", 1400.0))
     dm = float(hdr.get("DM", 0.0))
+    frac = None
+    if "IC_DELAY" in dt.names:
+        frac = np.array(rows["IC_DELAY"].reshape(nsub, nchan_total)[0, c0:c1], np.float64)
     if "IC_SHIFT" in dt.names:
         shift = np.array(rows["IC_SHIFT"].reshape(nsub, nchan_total)[0, c0:c1], np.int64)
     elif freqs is not None and dm != 0.0:
         delay = 4.148808e3 * dm * (freqs ** -2 - cfreq ** -2)
         shift = np.rint(delay / period * nbin).astype(np.int64) % nbin
+        if fractional_dedispersion():
+            frac = delay / period * nbin
     else:
         shift = np.zeros(nchan, np.int64)
     mjd0 = float(primary.get("STT_IMJD", 60000)) + (float(primary.get("STT_SMJD", 0))
@@ -300,7 +317,7 @@ def load(path: str, channels=None):
                  filename=path, source=str(primary.get("SRC_NAME", "J0000+0000")),
                  centre_frequency=cfreq, mjd_start=mjd0,
                  mjd_end=float(hdr.get("IC_MJDE", mjd0 + 0.01)),
-                 baseline_duty=float(hdr.get("IC_DUTY", 0.15)), state=state)
+                 baseline_duty=float(hdr.get("IC_DUTY", 0.15)), state=state, dm_delay=frac)
     if channels is not None:
         ar._chan_range = (c0, c1)
         ar._nchan_total = nchan_total

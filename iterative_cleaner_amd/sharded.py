@@ -44,10 +44,13 @@ def clean_cube_local(cube, w0, shift, world, devices=None, want_details=False, f
         raise ValueError("need one device per shard")
     chans, _ = _native.shard_layout(nsub, nchan, world)
     kw = _loop_kwargs(args)
+    delay = args.get("delay")
     results = [None] * world
     errors = []
     with _native.ShardGroup(world) as group:
-        sessions = [_native.ShardSession(nsub, nchan, nbin, r, world, group=group, device=devices[r], **kw)
+        sessions = [_native.ShardSession(nsub, nchan, nbin, r, world, group=group, device=devices[r],
+                                         delay=None if delay is None else np.asarray(delay)[chans[r][0]:chans[r][1]],
+                                         **kw)
                     for r in range(world)]
         try:
             for r, s in enumerate(sessions):
@@ -109,7 +112,8 @@ def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, gro
     """This rank's channel shard of one archive under torch.distributed.
     `cube_slice` etc. are the rank's channel range (``_native.shard_layout``);
     returns the merged full-archive dict on every rank (with want_residual, the
-    full residual cube on rank 0 only)."""
+    full residual cube on rank 0 only).  ``delay`` (in args): the slice's
+    fractional delays (FFT-rotation dedispersion)."""
     import torch.distributed as dist
 
     from .dist import TorchComm
@@ -118,8 +122,8 @@ def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, gro
     world, rank = comm.world, comm.rank
     chans, _ = _native.shard_layout(nsub, nchan, world)
     try:
-        with _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm,
-                                  device=_device_index(device), **_loop_kwargs(args)) as s:
+        with _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm, device=_device_index(device),
+                                  delay=args.get("delay"), **_loop_kwargs(args)) as s:
             if np.ndim(cube_slice) == 4:   # full-pol: pscrunched on the GPU
                 s.upload_pols(cube_slice, w0_slice, shift_slice)
             else:

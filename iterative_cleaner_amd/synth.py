@@ -76,6 +76,16 @@ def fractional_weights(w):
     return w
 
 
+def fractional_delays(shift, nbin):
+    """Deterministic fractional per-channel delays in bins near the integer
+    shifts (dedispersion by FFT phase rotation, phase_rotation.py): shift[c]
+    + 0.45 sin(1.3 c), plus whole turns on every 5th channel (the rotation
+    depends on the delay modulo nbin only)."""
+    c = np.arange(len(shift))
+    return (np.asarray(shift, dtype=np.float64) + 0.45 * np.sin(1.3 * c)
+            + np.where(c % 5 == 4, 3.0 * nbin, 0.0))
+
+
 def make_archive(nsub, nchan, nbin, seed=0, rfi_frac=0.05, npol=1,
                  filename="synthetic.ar", **kw) -> Archive:
     data, weights, shift = make_cube(nsub, nchan, nbin, seed, rfi_frac, npol, **kw)

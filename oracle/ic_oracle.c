@@ -15,6 +15,12 @@
  *   orc_fit_residual  remove_profile_inplace / remove_profile1d, :259-288
  *   orc_diagnostics   comprehensive_stats diagnostics, :206-217
  *   orc_test          scalers + combine, :219-256
+ *   orc_rotate        fractional dedispersion (psrchive's FFT phase rotation,
+ *                     dedisperse / dededisperse at iterative_cleaner.py:91,
+ *                     :100, :104) in the written order of
+ *                     iterative_cleaner_amd/phase_rotation.py; parity with real
+ *                     psrchive UNPINNED (psrchive absent), pinned to numpy's
+ *                     irfft(rfft(x) * phasor) within one f32 ulp
  *   orc_clean_loop    the while loop, :83-146
  *
  * Build: gcc -O2 -fPIC -shared -ffp-contract=off -fno-fast-math (oracle/Makefile)
@@ -415,11 +421,22 @@ void orc_fit_cube(int nsub, int nchan, int n, const float *raw, const float *w0,
 
 /* template (iterative_cleaner.py:88-94): remove_baseline(W), dedisperse,
  * fscrunch, tscrunch, amps * 10000 (f32). */
+static void orc_scrunch(int nsub, int nchan, int n, const float *raw, const float *W,
+                        const int32_t *shift, const float *base, float *T);
+
 void orc_template(int nsub, int nchan, int n, const float *raw, const float *W,
                   const int32_t *shift, double duty, float *T)
 {
     float *base = (float *)malloc(sizeof(float) * (size_t)nsub * nchan);
     orc_baseline(nsub, nchan, n, raw, W, shift, duty, base, NULL);
+    orc_scrunch(nsub, nchan, n, raw, W, shift, base, T);
+    free(base);
+}
+
+/* dedisperse (integer shifts), fscrunch, tscrunch of f32(raw - base), amps * 10000 */
+static void orc_scrunch(int nsub, int nchan, int n, const float *raw, const float *W,
+                        const int32_t *shift, const float *base, float *T)
+{
     const int nsb = (nchan + SUPER_BLOCK - 1) / SUPER_BLOCK;
     double *num = (double *)malloc(sizeof(double) * (size_t)n);
     double *part = (double *)malloc(sizeof(double) * (size_t)n * nsb);
@@ -460,7 +477,143 @@ void orc_template(int nsub, int nchan, int n, const float *raw, const float *W,
         float t = (wt != 0.0) ? (float)(num[i] / wt) : 0.0f;
         T[i] = t * 10000.0f;
     }
-    free(base); free(num); free(part); free(wpart); free(F); free(wf);
+    free(num); free(part); free(wpart); free(F); free(wf);
+}
+
+/* ------------------------------------------- fractional dedispersion (FFT) */
+/* tw[2q], tw[2q+1] = cos, sin of -2 pi q / n (x87 long double, rounded to f64) */
+void orc_twiddles(int n, double *tw)
+{
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int q = 0; q < n; ++q) {
+        const long double ang = -2.0L * pi * (long double)q / (long double)n;
+        tw[2 * q] = (double)cosl(ang);
+        tw[2 * q + 1] = (double)sinl(ang);
+    }
+}
+
+/* ph[(c*(n/2+1) + k)*2 + {0,1}] = cos, sin of 2 pi fmod(k s_c, n) / n */
+void orc_phasors(int n, int nchan, const double *delay, double *ph)
+{
+    const long double pi = 3.141592653589793238462643383279502884L;
+    const int m = n / 2;
+    for (int c = 0; c < nchan; ++c)
+        for (int k = 0; k <= m; ++k) {
+            const long double t = fmodl((long double)k * (long double)delay[c], (long double)n);
+            const long double ang = 2.0L * pi * t / (long double)n;
+            double *o = ph + ((size_t)c * (m + 1) + k) * 2;
+            o[0] = (double)cosl(ang);
+            o[1] = (double)sinl(ang);
+        }
+}
+
+/* radix-2 Stockham FFT of m complex points (re/im interleaved) through `tmp` */
+static void stockham(int m, double *v, double *tmp, const double *tw)
+{
+    const int n = 2 * m, h = m / 2;
+    for (int ns = 1; ns < m; ns <<= 1) {
+        for (int j = 0; j < h; ++j) {
+            const int k = j & (ns - 1);
+            const double *w = tw + 2 * (size_t)(k * (n / (2 * ns)));
+            const double ar = v[2 * j], ai = v[2 * j + 1];
+            const double br = v[2 * (j + h)], bi = v[2 * (j + h) + 1];
+            const double tr = w[0] * br - w[1] * bi;
+            const double ti = w[0] * bi + w[1] * br;
+            const int o = 2 * j - k;
+            tmp[2 * o] = ar + tr;
+            tmp[2 * o + 1] = ai + ti;
+            tmp[2 * (o + ns)] = ar - tr;
+            tmp[2 * (o + ns) + 1] = ai - ti;
+        }
+        memcpy(v, tmp, sizeof(double) * 2 * (size_t)m);
+    }
+}
+
+/* real spectrum bin a from the half-length transform: za = Z_a, zb = Z_{M-a}, w = W^a */
+static void rot_post(const double *za, const double *zb, const double *w, double *x)
+{
+    const double er = (za[0] + zb[0]) * 0.5, ei = (za[1] - zb[1]) * 0.5;
+    const double dr = za[0] - zb[0], di = za[1] + zb[1];
+    const double orr = di * 0.5, oi = -(dr * 0.5);
+    x[0] = er + (w[0] * orr - w[1] * oi);
+    x[1] = ei + (w[0] * oi + w[1] * orr);
+}
+
+/* half-length inverse input Z'_a from ya = Y_a, yb = Y_{M-a}, w = W^a */
+static void rot_pre(const double *ya, const double *yb, const double *w, double *z)
+{
+    const double er = (ya[0] + yb[0]) * 0.5, ei = (ya[1] - yb[1]) * 0.5;
+    const double hr = (ya[0] - yb[0]) * 0.5, hi = (ya[1] + yb[1]) * 0.5;
+    const double orr = hr * w[0] + hi * w[1], oi = hi * w[0] - hr * w[1];
+    z[0] = er - oi;
+    z[1] = ei + orr;
+}
+
+/* One profile: out = rotation of f32(x - b) by the channel phasors p (sign +1:
+ * dedisperse, y[j] = x[j + s]; -1: dededisperse).  work: 4n doubles. */
+static void rotate1(int n, const float *x, float b, const double *p, int sign, const double *tw,
+                    double *work, float *out)
+{
+    const int m = n / 2;
+    double *v = work, *tmp = work + 2 * (size_t)m;
+    for (int j = 0; j < m; ++j) {
+        const float x0 = x[2 * j] - b, x1 = x[2 * j + 1] - b;
+        v[2 * j] = (double)x0;
+        v[2 * j + 1] = (double)x1;
+    }
+    stockham(m, v, tmp, tw);
+    const double sg = sign > 0 ? 1.0 : -1.0;
+    {
+        const double X0 = v[0] + v[1], XM = v[0] - v[1];
+        const double Y0 = X0 * p[0], YM = XM * p[2 * m];
+        v[0] = (Y0 + YM) * 0.5;
+        v[1] = -((Y0 - YM) * 0.5);
+    }
+    for (int k = 1; k <= m / 2; ++k) {
+        const int q = m - k;
+        double zk[2] = {v[2 * k], v[2 * k + 1]}, zq[2] = {v[2 * q], v[2 * q + 1]};
+        double Xk[2], Xq[2], Yk[2], Yq[2], Zk[2], Zq[2];
+        rot_post(zk, zq, tw + 2 * k, Xk);
+        rot_post(zq, zk, tw + 2 * q, Xq);
+        const double pkr = p[2 * k], pki = sg * p[2 * k + 1];
+        const double pqr = p[2 * q], pqi = sg * p[2 * q + 1];
+        Yk[0] = Xk[0] * pkr - Xk[1] * pki;
+        Yk[1] = Xk[0] * pki + Xk[1] * pkr;
+        Yq[0] = Xq[0] * pqr - Xq[1] * pqi;
+        Yq[1] = Xq[0] * pqi + Xq[1] * pqr;
+        rot_pre(Yk, Yq, tw + 2 * k, Zk);
+        rot_pre(Yq, Yk, tw + 2 * q, Zq);
+        v[2 * k] = Zk[0];
+        v[2 * k + 1] = -Zk[1];
+        v[2 * q] = Zq[0];
+        v[2 * q + 1] = -Zq[1];
+    }
+    stockham(m, v, tmp, tw);
+    const double inv = 1.0 / (double)m;
+    for (int j = 0; j < m; ++j) {
+        out[2 * j] = (float)(v[2 * j] * inv);
+        out[2 * j + 1] = (float)((-v[2 * j + 1]) * inv);
+    }
+}
+
+/* Rotate every profile of a (nsub, nchan, n) cube by its channel's delay:
+ * out = rot(f32(in - base)) (base may be NULL = 0).  n a power of two >= 4. */
+void orc_rotate(int nsub, int nchan, int n, const float *in, const float *base, const double *delay,
+                int sign, float *out)
+{
+    const int m = n / 2;
+    double *tw = (double *)malloc(sizeof(double) * 2 * (size_t)n);
+    double *ph = (double *)malloc(sizeof(double) * 2 * (size_t)nchan * (m + 1));
+    double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
+    orc_twiddles(n, tw);
+    orc_phasors(n, nchan, delay, ph);
+    for (int s = 0; s < nsub; ++s)
+        for (int c = 0; c < nchan; ++c) {
+            const size_t k = (size_t)s * nchan + c;
+            rotate1(n, in + k * n, base ? base[k] : 0.0f, ph + (size_t)c * (m + 1) * 2, sign, tw, work,
+                    out + k * n);
+        }
+    free(tw); free(ph); free(work);
 }
 
 /* ------------------------------------------------------ pairwise sums */
@@ -918,6 +1071,7 @@ typedef struct {
     double baseline_duty;
     int32_t fit_mode;   /* 0: exact leastsq (orc_fit_residual), 1: closed form (orc_fit_closed) */
     int32_t data_f64;   /* 1: get_data returns f64 (orc_diagnostics_f64 / orc_test_f64) */
+    int32_t dedisp_mode; /* 0: integer shifts; 1: FFT phase rotation by `delay` (orc_rotate) */
 } orc_params;
 
 /* One full clean loop (iterative_cleaner.py:83-146).
@@ -925,11 +1079,14 @@ typedef struct {
  * Outputs: test (P), weights (P), loops, changed[max_iter], nzero[max_iter];
  * optional (may be NULL): R_last (P*nbin, dispersed frame, unweighted),
  * T_all (max_iter*nbin), amp_last/info_last (P),
- * diag_last: std, mean (P f64), ptp (P, f64 storage: f32 values unless data_f64), fft (P f64). */
+ * diag_last: std, mean (P f64), ptp (P, f64 storage: f32 values unless data_f64), fft (P f64).
+ * dedisp_mode 1: `delay` [nchan] f64 bins; every dedisperse / dededisperse of the
+ * reference is the FFT phase rotation (archive.py with dm_delay), `shift` unused. */
 int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, const int32_t *shift,
                    double *test, float *weights, int32_t *loops_out, int32_t *changed,
                    int32_t *nzero, float *R_last, float *T_all, double *amp_last,
-                   int32_t *info_last, double *std_l, double *mean_l, double *ptp_l, double *fft_l)
+                   int32_t *info_last, double *std_l, double *mean_l, double *ptp_l, double *fft_l,
+                   const double *delay)
 {
     const int nsub = pp->nsub, nchan = pp->nchan, n = pp->nbin;
     const size_t P = (size_t)nsub * nchan, N = P * (size_t)n;
@@ -952,24 +1109,47 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
     memcpy(hist, w0, sizeof(float) * P);
     memcpy(Wcur, w0, sizeof(float) * P);
     int nhist = 1;
-    orc_fit_cube(nsub, nchan, n, raw, w0, shift, pp->baseline_duty, D);
+    const int fftded = pp->dedisp_mode == 1;
+    int32_t *zsh = fftded ? (int32_t *)calloc((size_t)nchan, sizeof(int32_t)) : NULL;
+    float *dr = NULL, *Tc = NULL, *bs = NULL, *Rx = NULL;
+    if (fftded) {
+        /* remove_baseline reads the dedispersed view rot(raw); the data it
+         * leaves, f32(raw - base), is then rotated (dedisperse) */
+        dr = (float *)malloc(sizeof(float) * N);
+        Tc = (float *)malloc(sizeof(float) * N);
+        Rx = (float *)malloc(sizeof(float) * N);
+        bs = (float *)malloc(sizeof(float) * P);
+        orc_rotate(nsub, nchan, n, raw, NULL, delay, 1, dr);
+        orc_baseline(nsub, nchan, n, dr, w0, zsh, pp->baseline_duty, bs, NULL);
+        orc_rotate(nsub, nchan, n, raw, bs, delay, 1, D);
+    } else {
+        orc_fit_cube(nsub, nchan, n, raw, w0, shift, pp->baseline_duty, D);
+    }
     int x = 0, loops = -1;
     while (x < maxit) {
         x += 1;
-        orc_template(nsub, nchan, n, raw, Wcur, shift, pp->baseline_duty, T);
+        if (fftded) {
+            orc_baseline(nsub, nchan, n, dr, Wcur, zsh, pp->baseline_duty, bs, NULL);
+            orc_rotate(nsub, nchan, n, raw, bs, delay, 1, Tc);
+            for (size_t k = 0; k < P; ++k) bs[k] = 0.0f;
+            orc_scrunch(nsub, nchan, n, Tc, Wcur, zsh, bs, T);
+        } else {
+            orc_template(nsub, nchan, n, raw, Wcur, shift, pp->baseline_duty, T);
+        }
         if (T_all) memcpy(T_all + (size_t)(x - 1) * n, T, sizeof(float) * (size_t)n);
         if (pp->fit_mode == 1)
             orc_fit_closed((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
         else
             orc_fit_residual((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
         /* dededisperse + apply_weights */
+        if (fftded) orc_rotate(nsub, nchan, n, Rd, NULL, delay, -1, Rx);
         for (int s = 0; s < nsub; ++s)
             for (int c = 0; c < nchan; ++c) {
                 size_t k = (size_t)s * nchan + c;
-                const float *r = Rd + k * n;
+                const float *r = fftded ? Rx + k * n : Rd + k * n;
                 float *o = X + k * n;
                 float w = w0[k];
-                int sh = shift[c];
+                int sh = fftded ? 0 : shift[c];
                 for (int j = 0; j < n; ++j) {
                     int i = j - sh;
                     if (i < 0) i += n;
@@ -1010,9 +1190,9 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
             for (int c = 0; c < nchan; ++c) {
                 size_t k = (size_t)s * nchan + c;
                 for (int j = 0; j < n; ++j) {
-                    int i = j - shift[c];
+                    int i = j - (fftded ? 0 : shift[c]);
                     if (i < 0) i += n;
-                    R_last[k * n + j] = Rd[k * n + i];
+                    R_last[k * n + j] = fftded ? Rx[k * n + i] : Rd[k * n + i];
                 }
             }
     }
@@ -1025,5 +1205,6 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
     *loops_out = loops;
     free(D); free(Rd); free(X); free(T); free(amp); free(info); free(sd); free(mn);
     free(pt); free(pt64); free(X64); free(ff); free(valid); free(hist); free(Wcur);
+    free(zsh); free(dr); free(Tc); free(bs); free(Rx);
     return 0;
 }

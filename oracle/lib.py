@@ -24,7 +24,8 @@ class OrcParams(C.Structure):
                 ("max_iter", C.c_int32), ("chanthresh", C.c_double),
                 ("subintthresh", C.c_double), ("pr_on", C.c_int32),
                 ("pr_factor", C.c_double), ("pr_start", C.c_int32), ("pr_end", C.c_int32),
-                ("baseline_duty", C.c_double), ("fit_mode", C.c_int32), ("data_f64", C.c_int32)]
+                ("baseline_duty", C.c_double), ("fit_mode", C.c_int32), ("data_f64", C.c_int32),
+                ("dedisp_mode", C.c_int32)]
 
 
 def _p(a):
@@ -55,7 +56,10 @@ def lib():
         _lib.orc_sum_f64.restype = C.c_double
         _lib.orc_sum_f64.argtypes = [C.c_void_p, C.c_int]
         _lib.orc_clean_loop.restype = C.c_int
-        _lib.orc_clean_loop.argtypes = [C.POINTER(OrcParams)] + [C.c_void_p] * 16
+        _lib.orc_clean_loop.argtypes = [C.POINTER(OrcParams)] + [C.c_void_p] * 17
+        _lib.orc_twiddles.argtypes = [C.c_int, C.c_void_p]
+        _lib.orc_phasors.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _lib.orc_rotate.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_int, C.c_void_p]
     return _lib
 
 
@@ -123,6 +127,32 @@ def template(raw, W, shift, duty=0.15):
     return T
 
 
+def twiddles(n):
+    """(2, n) f64 twiddle table of the FFT rotation (orc_twiddles)."""
+    tw = np.empty((n, 2), np.float64)
+    lib().orc_twiddles(n, _p(tw))
+    return np.ascontiguousarray(tw.T)
+
+
+def phasors(n, delay):
+    """(2, nchan, n/2 + 1) f64 phasor table (orc_phasors)."""
+    d = np.ascontiguousarray(delay, np.float64).reshape(-1)
+    ph = np.empty((d.size, n // 2 + 1, 2), np.float64)
+    lib().orc_phasors(n, d.size, _p(d), _p(ph))
+    return np.ascontiguousarray(np.moveaxis(ph, -1, 0))
+
+
+def rotate(cube, delay, sign=1, base=None):
+    """FFT phase rotation (fractional dedispersion) of a (nsub, nchan, n) cube:
+    rot(f32(cube - base)) by +delay (sign 1) or -delay (sign -1)."""
+    cube = f32(cube)
+    nsub, nchan, n = cube.shape
+    out = np.empty_like(cube)
+    lib().orc_rotate(nsub, nchan, n, _p(cube), _p(None if base is None else f32(base)),
+                     _p(np.ascontiguousarray(delay, np.float64)), int(sign), _p(out))
+    return out
+
+
 def diagnostics(X, valid):
     X = f32(X)
     shp = X.shape[:-1]
@@ -159,8 +189,10 @@ def test_values(valid, std, mean, ptp, fft, ct, st):
 
 
 def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pulse_region=None,
-               duty=0.15, want_residual=False, want_details=False, fit_mode=0, data_f64=False):
-    """Whole loop; returns dict(test, weights, loops, changed, nzero, [...])."""
+               duty=0.15, want_residual=False, want_details=False, fit_mode=0, data_f64=False, delay=None):
+    """Whole loop; returns dict(test, weights, loops, changed, nzero, [...]).
+    delay (nchan f64 bins): fractional dedispersion by FFT phase rotation
+    (dedisp_mode 1) instead of the integer `shift`."""
     raw = f32(raw)
     nsub, nchan, n = raw.shape
     P = nsub * nchan
@@ -168,7 +200,9 @@ def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pul
     if pulse_region is not None:
         pr_on, fac, a, b = 1, float(pulse_region[0]), int(pulse_region[1]), int(pulse_region[2])
     prm = OrcParams(nsub, nchan, n, max_iter, float(chanthresh), float(subintthresh), pr_on, fac, a, b, duty,
-                    int(fit_mode), 1 if data_f64 else 0)
+                    int(fit_mode), 1 if data_f64 else 0, 0 if delay is None else 1)
+    if delay is not None:
+        delay = np.ascontiguousarray(delay, np.float64).reshape(nchan)
     test = np.empty((nsub, nchan), np.float64)
     weights = np.empty((nsub, nchan), np.float32)
     loops = np.zeros(1, np.int32)
@@ -184,7 +218,7 @@ def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pul
     ff = np.empty(P, np.float64) if want_details else None
     lib().orc_clean_loop(C.byref(prm), _p(raw), _p(f32(w0)), _p(np.ascontiguousarray(shift, np.int32)),
                          _p(test), _p(weights), _p(loops), _p(changed), _p(nzero), _p(R), _p(T_all),
-                         _p(amp), _p(info), _p(sd), _p(mn), _p(pt), _p(ff))
+                         _p(amp), _p(info), _p(sd), _p(mn), _p(pt), _p(ff), _p(delay))
     out = dict(test=test, weights=weights, loops=int(loops[0]), changed=changed[:max_iter],
                nzero=nzero[:max_iter])
     if want_residual:

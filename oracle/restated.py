@@ -199,3 +199,20 @@ def closed_form_fit(D: np.ndarray, T: np.ndarray):
         R = np.where(info[:, None] == 1, amp[:, None] * T64[None, :] - D64, 0.0).astype(np.float32)
     return amp, info, R
 
+
+
+def fft_phase_shift(x: np.ndarray, delay, sign: int = 1) -> np.ndarray:
+    """psrchive's published dedispersion of a profile (Profile::rotate_phase ->
+    fft::shift): forward real FFT, harmonic k times exp(+-2 pi i k s / N),
+    inverse real FFT, as numpy states it (pocketfft, complex128), rounded to
+    f32.  x (..., nchan, N) f32, delay (nchan,) bins; sign +1 dedisperses
+    (y[j] = x[j + s]), -1 dededisperses.  The stand-in's written-order
+    rotation (iterative_cleaner_amd/phase_rotation.py, orc_rotate, k_rotate)
+    agrees with this to within one f32 ulp; real psrchive (FFTW in f32) is not
+    available, so that parity is UNPINNED."""
+    x = np.asarray(x, dtype=np.float32)
+    n = x.shape[-1]
+    k = np.arange(n // 2 + 1)
+    s = np.asarray(delay, dtype=np.float64)[:, None]
+    X = np.fft.rfft(x.astype(np.float64), axis=-1)
+    return np.fft.irfft(X * np.exp(sign * 2j * np.pi * k * s / n), n=n, axis=-1).astype(np.float32)

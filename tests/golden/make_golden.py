@@ -151,12 +151,13 @@ def _load_f64(path):
 
 def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
                    keep_cubes=True, npol=1, workdir=None, out_dir=HERE, residual_full=True, data_f64=False,
-                   frac_weights=False):
+                   frac_weights=False, frac_delay=False):
     data, weights, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi, npol=npol)
     if frac_weights:
         weights = synth.fractional_weights(weights)
     path = os.path.join(workdir, "%s.ar" % name)
-    ar = ica.Archive(data, weights, shift, filename=path)
+    delay = synth.fractional_delays(shift, nbin) if frac_delay else None
+    ar = ica.Archive(data, weights, shift, filename=path, dm_delay=delay)
     ar.unload(path)
     loader = _load_f64 if data_f64 else ica.Archive_load
     ar = loader(path)
@@ -188,7 +189,7 @@ def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
         "meta": np.array(json.dumps({
             "name": name, "nsub": nsub, "nchan": nchan, "nbin": nbin, "seed": seed,
             "rfi": rfi, "npol": npol, "extra_args": list(extra_args), "data_f64": bool(data_f64),
-            "frac_weights": bool(frac_weights),
+            "frac_weights": bool(frac_weights), "frac_delay": bool(frac_delay),
             "args": {k: v for k, v in vars(args).items() if k != "archive"},
             "numpy": np.__version__, "scipy": scipy.__version__})),
     }
@@ -210,6 +211,8 @@ def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
         else:
             arrays["residual_ded_sha_%d" % k] = np.array(sha(it["residual_ded"]))
             arrays["X_sha_%d" % k] = np.array(sha(it["X"]))
+    if frac_delay:
+        arrays["dm_delay"] = delay
     if "-u" in extra_args:
         # the residual archive the reference unloads (iterative_cleaner.py:106-108, :161-162)
         res = ica.Archive_load("%s_residual_%s.ar" % (path, loops))
@@ -530,7 +533,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--skip-big", action="store_true")
-    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64 (round-2 fixtures only)")
+    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64,fft (round-2 fixtures only)")
     a = ap.parse_args()
     ic = import_reference()
     only = set(filter(None, a.only.split(",")))
@@ -545,6 +548,8 @@ def main():
             run_leastsq_nonfinite(ic, a.out)
         if "f64" in only:
             run_f64_cases(ic, a.out)
+        if "fft" in only:
+            run_fft_cases(ic, a.out)
         return
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s12x48x128", 12, 48, 128, 3, 0.05, workdir=wd, out_dir=a.out)
@@ -569,6 +574,25 @@ def main():
     run_zap_plot_case(ic, a.out)
     run_leastsq_nonfinite(ic, a.out)
     run_f64_cases(ic, a.out)
+    run_fft_cases(ic, a.out)
+
+
+def run_fft_cases(ic, out_dir=HERE):
+    """clean() on archives with fractional delays: every dedisperse /
+    dededisperse (ic.py:91, :100, :104) is the stand-in's FFT phase rotation
+    (iterative_cleaner_amd/phase_rotation.py)."""
+    with tempfile.TemporaryDirectory() as wd:
+        run_clean_case(ic, "s12x48x128_fft", 12, 48, 128, 3, 0.05, frac_delay=True, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s8x32x64_pol4_fft", 8, 32, 64, 8, 0.2, npol=4, extra_args=("-p",),
+                       frac_delay=True, keep_cubes=False, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s6x48x1024_fft_u", 6, 48, 1024, 43, 0.05, extra_args=("-u",), frac_delay=True,
+                       keep_cubes=False, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s12x40x256_fft_pr", 12, 40, 256, 9, 0.1, extra_args=("-r", "0.5", "30", "50"),
+                       frac_delay=True, keep_cubes=False, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s4x32x4096_fft_rfi30", 4, 32, 4096, 47, 0.30, frac_delay=True, keep_cubes=False,
+                       workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s6x48x128_fft_f64", 6, 48, 128, 5, 0.1, frac_delay=True, data_f64=True,
+                       frac_weights=True, keep_cubes=False, workdir=wd, out_dir=out_dir)
 
 
 def run_f64_cases(ic, out_dir=HERE):

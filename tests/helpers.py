@@ -29,6 +29,17 @@ def load_clean_case(path):
     return z, meta, np.ascontiguousarray(raw), w0, shift, meta["args"]
 
 
+def case_delay(z, meta):
+    """The fractional per-channel delays of a fixture made with frac_delay (FFT
+    phase-rotation dedispersion), else None (integer shifts)."""
+    if not meta.get("frac_delay"):
+        return None
+    d = np.asarray(z["dm_delay"], dtype=np.float64)
+    assert np.array_equal(d, synth.fractional_delays(synth.make_cube(1, meta["nchan"], meta["nbin"], 0, 0.0)[2],
+                                                     meta["nbin"])), "delay generator drifted"
+    return d
+
+
 def bits_equal(a, b):
     a = np.ascontiguousarray(a)
     b = np.ascontiguousarray(b)

@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import bits_equal, clean_fixtures, load_clean_case, nan_equal
+from helpers import bits_equal, case_delay, clean_fixtures, load_clean_case, nan_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -20,11 +20,12 @@ TEST_ATOL = 1e-9
 FIT_MODES = {"rounds": 0, "tail": 1 << 40, "default": None}
 
 
-def _session(shape, args, duty=0.15, fit_mode="default", data_f64=False):
+def _session(shape, args, duty=0.15, fit_mode="default", data_f64=False, delay=None):
     from iterative_cleaner_amd import _native
     nsub, nchan, nbin = shape
     s = _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"],
-                           args["subintthresh"], args["pulse_region"], duty, device=0, data_f64=data_f64)
+                           args["subintthresh"], args["pulse_region"], duty, device=0, data_f64=data_f64,
+                           delay=delay)
     if FIT_MODES[fit_mode] is not None:
         s.set_fit_tail(FIT_MODES[fit_mode])
     return s
@@ -51,7 +52,8 @@ def _close_test(a, b):
 def test_loop_matches_reference(path, fit_mode):
     z, meta, raw, w0, shift, args = load_clean_case(path)
     nit = int(z["n_iter"])
-    with _session(raw.shape, args, fit_mode=fit_mode, data_f64=meta.get("data_f64", False)) as s:
+    with _session(raw.shape, args, fit_mode=fit_mode, data_f64=meta.get("data_f64", False),
+                  delay=case_delay(z, meta)) as s:
         s.upload(raw, w0, shift)
         out = s.run()
         T = s.template()
@@ -90,7 +92,7 @@ def test_clean_stdout_matches_reference(path, tmp_path, monkeypatch, capsys):
         w0_ = synth.fractional_weights(w0_)
     monkeypatch.chdir(tmp_path)
     arpath = str(tmp_path / ("%s.ar" % meta["name"]))
-    ica.Archive(data, w0_, shift_, filename=arpath).unload(arpath)
+    ica.Archive(data, w0_, shift_, filename=arpath, dm_delay=case_delay(z, meta)).unload(arpath)
     ar = ica.Archive_load(arpath)
     if meta.get("data_f64"):
         # a binding whose get_data returns f64 (the reference's reload at :150 saw the same)

@@ -1,0 +1,110 @@
+"""Fractional dedispersion (psrchive's FFT phase rotation; reference calls
+dedisperse/dededisperse at iterative_cleaner.py:91, :100, :104).  CPU tests:
+the archive stand-in's written-order rotation (phase_rotation.py) == the C
+oracle's restatement (orc_rotate) bit for bit, both within one f32 ulp of
+numpy's irfft(rfft(x) * phasor) (oracle/restated.py fft_phase_shift), and the
+stand-in's archive plumbing of fractional delays.  Parity against real
+psrchive is UNPINNED (psrchive absent)."""
+import numpy as np
+import pytest
+
+from helpers import nan_equal
+
+
+def _case(n, nchan=9, nsub=4, seed=3):
+    rng = np.random.default_rng(seed + n)
+    d = rng.uniform(-5 * n, 5 * n, nchan)
+    d[0], d[1], d[2] = 0.0, 3.0, 0.5
+    x = (rng.standard_normal((nsub, nchan, n)) * 100).astype(np.float32)
+    x[0, 3, n - 1] = np.nan
+    x[1, 4, :] = 0.0
+    x[2, 5, 1] = np.inf
+    b = rng.standard_normal((nsub, nchan)).astype(np.float32)
+    return x, d, b
+
+
+@pytest.mark.parametrize("n", [4, 8, 64, 128, 256, 1024, 2048, 4096])
+def test_tables_and_rotation_match_c_oracle(n, oracle_lib):
+    from iterative_cleaner_amd import phase_rotation as pr
+    x, d, b = _case(n)
+    assert np.array_equal(pr.twiddles(n), oracle_lib.twiddles(n))
+    ph = pr.phasors(n, d)
+    assert np.array_equal(ph, oracle_lib.phasors(n, d))
+    for sign in (1, -1):
+        for base in (None, b):
+            a = pr.rotate(x, ph, sign, base=base)
+            c = oracle_lib.rotate(x, d, sign, base=base)
+            # NaN payloads/signs are not part of the definition (x86 vs numpy negation)
+            assert nan_equal(a, c) and np.array_equal(np.signbit(a) | np.isnan(a), np.signbit(c) | np.isnan(c))
+
+
+@pytest.mark.parametrize("n", [64, 256, 1024, 4096])
+def test_rotation_within_one_ulp_of_numpy_fft(n, oracle_lib):
+    from oracle.restated import fft_phase_shift
+    rng = np.random.default_rng(n)
+    d = rng.uniform(-3 * n, 3 * n, 16)
+    x = (rng.standard_normal((8, 16, n)) * 10 + 3).astype(np.float32)
+    for sign in (1, -1):
+        got = oracle_lib.rotate(x, d, sign)
+        want = fft_phase_shift(x, d, sign)
+        # one f32 ulp of the value, or the f64 transforms' own error (~ log2(N) eps |profile|)
+        # for samples near zero
+        scale = np.max(np.abs(x), axis=-1, keepdims=True).astype(np.float64)
+        tol = np.spacing(np.abs(want)).astype(np.float64) + 1e-12 * scale
+        assert np.all(np.abs(got.astype(np.float64) - want) <= tol)
+        assert np.mean(got == want) > 0.999
+
+
+def test_integer_and_zero_delays():
+    """A zero delay is the identity and an integer delay the stand-in's roll,
+    to within one ulp (exactly, for these inputs)."""
+    from iterative_cleaner_amd import phase_rotation as pr
+    rng = np.random.default_rng(7)
+    n = 256
+    x = (rng.standard_normal((3, 4, n)) * 5).astype(np.float32)
+    d = np.array([0.0, 5.0, n - 1.0, 2.0 * n + 9])
+    y = pr.rotate(x, pr.phasors(n, d), 1)
+    for c, s in enumerate([0, 5, n - 1, 9]):
+        want = np.roll(x[:, c], -s, axis=-1)
+        assert np.max(np.abs(y[:, c] - want) / np.spacing(np.abs(want))) <= 1.0
+
+
+def test_archive_fft_dedisperse_roundtrip_and_io(tmp_path):
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import archive_io, psrfits, synth
+    from iterative_cleaner_amd import phase_rotation as pr
+    data, w, shift = synth.make_cube(3, 12, 64, 5, 0.1, npol=2)
+    delay = synth.fractional_delays(shift, 64)
+    ar = ica.Archive(data, w, shift, dm_delay=delay)
+    assert np.array_equal(ar.get_dm_delay(), delay)
+    ded = ar._ded_view()
+    assert np.array_equal(ded, pr.rotate(data, pr.phasors(64, delay), 1))
+    ar.dedisperse()
+    ar.dededisperse()
+    back = ar.get_data()
+    assert np.array_equal(back, pr.rotate(ded, pr.phasors(64, delay), -1))
+    for name in ("a.ar", "a.sf"):
+        p = str(tmp_path / name)
+        ica.Archive(data, w, shift, dm_delay=delay).unload(p)
+        br = archive_io.load(p)
+        assert np.array_equal(br.get_dm_delay(), delay)
+        sl = archive_io.load(p, channels=(4, 9))
+        assert np.array_equal(sl.get_dm_delay(), delay[4:9])
+    with pytest.raises(ValueError):
+        ica.Archive(data[..., :48], w, shift, dm_delay=delay)
+    # a foreign PSRFITS file (no stand-in columns): fractional delays from DM only on request
+    fr = ica.Archive(data, w, shift)
+    fr._chan_freqs = 1400.0 + np.arange(12) * 8.0
+    fr._period = 0.05
+    fr._dm = 30.0
+    p = str(tmp_path / "foreign.sf")
+    psrfits.save(fr, p, stand_in_meta=False)
+    assert psrfits.load(p).get_dm_delay() is None
+    import os
+    os.environ["IC_DEDISPERSION"] = "fft"
+    try:
+        fa = psrfits.load(p)
+    finally:
+        del os.environ["IC_DEDISPERSION"]
+    fd = fa.get_dm_delay()
+    assert fd is not None and np.array_equal(np.rint(fd).astype(np.int64) % 64, fa.get_dm_shift())
