@@ -2327,6 +2327,14 @@ struct RotCfg {
     static constexpr int TB = M / 8 < 64 ? 64 : (M / 8 > 256 ? 256 : M / 8);
 };
 
+// LDS address of complex point i: the low 4 bits XOR bits 3..6, so that 16
+// consecutive lanes hit 16 distinct 16-byte bank groups for the contiguous
+// (i = ja + q G) and the strided (i = 8 ja + q, 64 a + b + 8 q) patterns
+#ifndef IC_ROT_SWIZZLE
+#define IC_ROT_SWIZZLE 0
+#endif
+__device__ __forceinline__ int rsw(int i) { return IC_ROT_SWIZZLE ? i ^ ((i >> 3) & 15) : i; }
+
 // R consecutive radix-2 Stockham stages (ns = 2^lg .. 2^(lg+R-1)) through
 // registers: group ja < G = M/2^R holds the 2^R points v[ja + q G]; the stages
 // run on them as a local Stockham of size 2^R whose butterfly (l, jl) is the
@@ -2334,23 +2342,32 @@ struct RotCfg {
 // at v[(ja / ns) 2^R ns + ja mod ns + p ns].  Same operations, same operands as
 // R separate stages (phase_rotation._stockham), i.e. the same bits, with one
 // LDS round trip instead of R.
-template <int N, int R>
-__device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__ tw, int t, int lg)
+template <int N, int R, int LGS>
+__device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__ tw, int t)
 {
     using C = RotCfg<N>;
     constexpr int M = C::M, TB = C::TB, G = M >> R, Q = 1 << R, HALF = Q / 2;
     constexpr int GPT = (G + TB - 1) / TB;
-    const int ns = 1 << lg;
+    constexpr int ns = 1 << LGS;
     double2 u[GPT][Q];
+    // the pass's twiddles first (global/L1 latency overlaps the LDS reads and
+    // the barrier): local stage l uses 2^l distinct ones, w[2^l - 1 + kl]
+    double2 w[GPT][Q - 1];
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
         const int ja = t + TB * gi;
+        const int k = ja & (ns - 1);
         if (G % TB == 0 || ja < G) {
 #pragma unroll
-            for (int q = 0; q < Q; ++q) u[gi][q] = v[ja + q * G];
+            for (int l = 0; l < R; ++l)
+#pragma unroll
+                for (int kl = 0; kl < (1 << l); ++kl)
+                    w[gi][(1 << l) - 1 + kl] = tw[(kl * ns + k) * (N >> (l + LGS + 1))];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) u[gi][q] = v[rsw(ja + q * G)];
         }
     }
-    __syncthreads();
+    gsync<C::TB / 64>();
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
         const int ja = t + TB * gi;
@@ -2363,10 +2380,10 @@ __device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__
 #pragma unroll
                 for (int jl = 0; jl < HALF; ++jl) {
                     const int kl = jl & (nsl - 1);
-                    const double2 w = tw[(kl * ns + k) * (N >> (l + lg + 1))];
+                    const double2 ww = w[gi][nsl - 1 + kl];
                     const double2 a = u[gi][jl], b = u[gi][jl + HALF];
-                    const double tr = w.x * b.x - w.y * b.y;
-                    const double ti = w.x * b.y + w.y * b.x;
+                    const double tr = ww.x * b.x - ww.y * b.y;
+                    const double ti = ww.x * b.y + ww.y * b.x;
                     const int o = 2 * jl - kl;
                     w2[o] = make_double2(a.x + tr, a.y + ti);
                     w2[o + nsl] = make_double2(a.x - tr, a.y - ti);
@@ -2374,12 +2391,12 @@ __device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__
 #pragma unroll
                 for (int q = 0; q < Q; ++q) u[gi][q] = w2[q];
             }
-            const int base = ((ja >> lg) << (lg + R)) + k;
+            const int base = ((ja >> LGS) << (LGS + R)) + k;
 #pragma unroll
-            for (int q = 0; q < Q; ++q) v[base + q * ns] = u[gi][q];
+            for (int q = 0; q < Q; ++q) v[rsw(base + q * ns)] = u[gi][q];
         }
     }
-    __syncthreads();
+    gsync<C::TB / 64>();
 }
 
 // the full N/2-point FFT: passes of 3 stages (the last one shorter)
@@ -2389,7 +2406,7 @@ __device__ __forceinline__ void rot_fft(double2 *v, const double2 *__restrict__ 
     constexpr int LG = RotCfg<N>::LG;
     if constexpr (LG0 < LG) {
         constexpr int R = LG - LG0 >= 3 ? 3 : LG - LG0;
-        rot_pass<N, R>(v, tw, t, LG0);
+        rot_pass<N, R, LG0>(v, tw, t);
         rot_fft<N, LG0 + R>(v, tw, t);
     }
 }
@@ -2413,7 +2430,7 @@ __device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
 }
 
 template <int N>
-__global__ __launch_bounds__(RotCfg<N>::TB) void k_rotate(RotateArgs a)
+__global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 4 : 2) void k_rotate(RotateArgs a)
 {
     using C = RotCfg<N>;
     constexpr int M = C::M, H = C::H, TB = C::TB;
@@ -2429,7 +2446,7 @@ __global__ __launch_bounds__(RotCfg<N>::TB) void k_rotate(RotateArgs a)
         const size_t p = (size_t)s * nchan + c;
         const float *x = a.in + p * (size_t)a.ld_in;
         if (a.amp) {
-            // the residual of the exact fit (k_residual), formed on the fly
+            // the residual of the exact fit (k_residual's arithmetic), formed on the fly
             const int st = a.info[p];
             const bool ok = st >= 1 && st <= 4;
             const double am = a.amp[p];
@@ -2447,28 +2464,28 @@ __global__ __launch_bounds__(RotCfg<N>::TB) void k_rotate(RotateArgs a)
                         r[e] = (float)d;
                     }
                 }
-                v[j] = make_double2((double)r[0], (double)r[1]);
+                v[rsw(j)] = make_double2((double)r[0], (double)r[1]);
             }
         } else {
             const float b = a.base ? a.base[p] : 0.0f;
             for (int j = t; j < M; j += TB) {
                 const float2 q = *(const float2 *)(x + 2 * j);
                 const float x0 = q.x - b, x1 = q.y - b;
-                v[j] = make_double2((double)x0, (double)x1);
+                v[rsw(j)] = make_double2((double)x0, (double)x1);
             }
         }
-        __syncthreads();
+        gsync<TB / 64>();
         rot_fft<N>(v, a.tw, t);
         const double2 *ph = a.ph + (size_t)c * (M + 1);
         for (int k = t; k <= H; k += TB) {
             if (k == 0) {
-                const double2 z = v[0];
+                const double2 z = v[rsw(0)];
                 const double X0 = z.x + z.y, XM = z.x - z.y;
                 const double Y0 = X0 * ph[0].x, YM = XM * ph[M].x;
-                v[0] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
+                v[rsw(0)] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
             } else {
                 const int q = M - k;
-                const double2 zk = v[k], zq = v[q];
+                const double2 zk = v[rsw(k)], zq = v[rsw(q)];
                 const double2 wk = a.tw[k], wq = a.tw[q];
                 const double2 Xk = rot_post(zk, zq, wk), Xq = rot_post(zq, zk, wq);
                 const double2 pk = ph[k], pq = ph[q];
@@ -2476,21 +2493,21 @@ __global__ __launch_bounds__(RotCfg<N>::TB) void k_rotate(RotateArgs a)
                 const double2 Yk = make_double2(Xk.x * pk.x - Xk.y * pki, Xk.x * pki + Xk.y * pk.x);
                 const double2 Yq = make_double2(Xq.x * pq.x - Xq.y * pqi, Xq.x * pqi + Xq.y * pq.x);
                 const double2 Zk = rot_pre(Yk, Yq, wk), Zq = rot_pre(Yq, Yk, wq);
-                v[q] = make_double2(Zq.x, -Zq.y);
-                v[k] = make_double2(Zk.x, -Zk.y);
+                v[rsw(q)] = make_double2(Zq.x, -Zq.y);
+                v[rsw(k)] = make_double2(Zk.x, -Zk.y);
             }
         }
-        __syncthreads();
+        gsync<TB / 64>();
         rot_fft<N>(v, a.tw, t);
         float *o = a.out + p * (size_t)a.ldo;
         float *o2 = a.out2 ? a.out2 + p * (size_t)a.ldo2 : nullptr;
         for (int j = t; j < M; j += TB) {
-            const double2 r = v[j];
+            const double2 r = v[rsw(j)];
             const float2 y = make_float2((float)(r.x * inv), (float)((-r.y) * inv));
             *(float2 *)(o + 2 * j) = y;
             if (o2) *(float2 *)(o2 + 2 * j) = y;
         }
-        __syncthreads();   // v is reused by the block's next profile
+        gsync<TB / 64>();   // v is reused by the block's next profile
     }
 }
 
