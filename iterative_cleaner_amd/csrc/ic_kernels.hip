@@ -1296,6 +1296,51 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
 #define TAIL_CH 256
 #define TAIL_WAVES 4
 
+// s += a[0], s += a[1], ... in order (and t over b, a second chain interleaved
+// with it).  The terms are read from LDS in register blocks of SB, the next
+// block's reads issued before the current block's adds, so the dependent f64
+// adds, not the LDS latency, set the pace of the sequential MINPACK sums.
+template <int SB, bool TWO>
+__device__ __forceinline__ void seq_sums(const double *a, const double *b, int n, double &s, double &t)
+{
+    int q = 0;
+    if (n >= SB) {
+        double ca[SB], cb[SB];
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+            ca[i] = a[i];
+            if (TWO) cb[i] = b[i];
+        }
+        for (q = SB; q + SB <= n; q += SB) {
+            double na[SB], nb[SB];
+#pragma unroll
+            for (int i = 0; i < SB; ++i) {
+                na[i] = a[q + i];
+                if (TWO) nb[i] = b[q + i];
+            }
+#pragma unroll
+            for (int i = 0; i < SB; ++i) {
+                s = s + ca[i];
+                if (TWO) t = t + cb[i];
+            }
+#pragma unroll
+            for (int i = 0; i < SB; ++i) {
+                ca[i] = na[i];
+                if (TWO) cb[i] = nb[i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+            s = s + ca[i];
+            if (TWO) t = t + cb[i];
+        }
+    }
+    for (; q < n; ++q) {
+        s = s + a[q];
+        if (TWO) t = t + b[q];
+    }
+}
+
 __device__ __forceinline__ void tail_sweep_a(const float *__restrict__ p, const double *__restrict__ T64, int nbin,
                                              double xa, double agiant, double (*buf)[TAIL_CH], int lane,
                                              double &fnorm, double &acnorm, double &f0, double &J0)
@@ -1338,20 +1383,19 @@ __device__ __forceinline__ void tail_sweep_a(const float *__restrict__ p, const 
         // formed above, off the dependency chain)
         if (okF && okJ) {   // the usual case: both chains interleaved
             double sF = eF.s2, sJ = eJ.s2;
-            for (int q = 0; q < n; ++q) {
-                sF = sF + buf[2][q];
-                sJ = sJ + buf[3][q];
-            }
+            seq_sums<8, true>(buf[2], buf[3], n, sF, sJ);
             eF.s2 = sF;
             eJ.s2 = sJ;
         } else {
             if (okF) {
-                for (int q = 0; q < n; ++q) eF.s2 = eF.s2 + buf[2][q];
+                double dummy = 0.0;
+                seq_sums<16, false>(buf[2], nullptr, n, eF.s2, dummy);
             } else {
                 for (int q = 0; q < n; ++q) en_add(eF, buf[0][q], agiant);
             }
             if (okJ) {
-                for (int q = 0; q < n; ++q) eJ.s2 = eJ.s2 + buf[3][q];
+                double dummy = 0.0;
+                seq_sums<16, false>(buf[3], nullptr, n, eJ.s2, dummy);
             } else {
                 for (int q = 0; q < n; ++q) en_add(eJ, buf[1][q], agiant);
             }
@@ -1386,7 +1430,8 @@ __device__ __forceinline__ double tail_sweep_b(const float *__restrict__ p, cons
             buf[0][q] = Jn * f;
         }
         wave_sync();
-        for (int q = 0; q < n; ++q) sum = sum + buf[0][q];
+        double dummy = 0.0;
+        seq_sums<16, false>(buf[0], nullptr, n, sum, dummy);
         wave_sync();
     }
     return sum;
