@@ -562,6 +562,7 @@ def main():
                        "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"])
                                                        / per_rank_P / max(1, n_iter), 2),
                        "fit_tail_sweeps": stats["fit_tail_sweeps"] // max(1, n_iter),
+                       "near_threshold_profiles": stats["near_threshold"],
                        "parallelism": parallelism,
                        "loop_hbm_gbs_per_gpu": round(loop_gbs, 1),
                        "loop_hbm_frac": round(loop_gbs / HBM_PEAK_GBS, 4)},

@@ -196,7 +196,9 @@ typedef struct {
     int64_t fit_profile_sweeps;  /* profiles swept by k_fit_pass, summed (x nbin x 4 B = fit bytes) */
     int64_t fit_tail_sweeps;     /* profile sweeps done by k_fit_tail (the last few thousand profiles) */
     int32_t window_moves;        /* subint baseline windows that moved between iterations */
-    int32_t reserved;
+    int32_t near_threshold;      /* last iteration: profiles whose test value lies within 1e-9 of
+                                    the zap threshold 1.0, where fftmax's last bits (not
+                                    bit-identical to numpy's pocketfft) could decide the zap */
 } ic_run_stats;
 int ic_get_run_stats(void *session, ic_run_stats *out);
 

@@ -46,7 +46,7 @@ class Params(C.Structure):
 class RunStats(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("fit_rounds", C.c_int32),
                 ("fit_profile_sweeps", C.c_int64), ("fit_tail_sweeps", C.c_int64),
-                ("window_moves", C.c_int32), ("reserved", C.c_int32)]
+                ("window_moves", C.c_int32), ("near_threshold", C.c_int32)]
 
 
 class KernelTime(C.Structure):
@@ -330,7 +330,7 @@ class GpuSession:
         return dict(iterations=st.iterations, fit_rounds=st.fit_rounds,
                     fit_profile_sweeps=int(st.fit_profile_sweeps),
                     fit_tail_sweeps=int(st.fit_tail_sweeps),
-                    window_moves=int(st.window_moves))
+                    window_moves=int(st.window_moves), near_threshold=int(st.near_threshold))
 
     def kernel_times(self):
         buf = (KernelTime * 32)()

@@ -182,7 +182,8 @@ hipError_t launch_tnorm(hipStream_t st, const double *T64, const PwPlan *plan, i
 // which: bit 0 = column lines (length nsub), bit 1 = row lines (length nchan)
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which = 3);
 // counters: [0] changed, [1] zero weights, [2] fit statuses outside 1-4 (info
-// may be null), [3+h] new weights != history h (iterative_cleaner.py:127-141)
+// may be null), [3] test values within 1e-9 of 1.0, [4+h] new weights !=
+// history h (iterative_cleaner.py:127-141)
 hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *valid, const int32_t *info,
                           const float *w0,
                           const double *std_d, const double *mean_d, const double *ptp_d, int ptp_f32,

@@ -2802,7 +2802,13 @@ __device__ __forceinline__ double nanmax2(double a, double b)
 }
 
 // counters: [0] changed vs hist[iter-1], [1] zero weights, [2] profiles whose
-// fit status is not 1-4 (info may be null: 0), [3+h] != hist[h]
+// fit status is not 1-4 (info may be null: 0), [3] profiles whose test value
+// lies within kNearTie of the zap threshold 1.0 (where the last bits of fftmax,
+// not bit-identical to pocketfft, could decide), [4+h] != hist[h]
+// |test - 1| at or below this counts as a near tie (the fftmax tolerance of
+// the parity tests, DESIGN.md "Numerical semantics")
+constexpr double kNearTie = 1e-9;
+
 __global__ __launch_bounds__(256) void k_combine(
     int nsub, int nchan, const uint8_t *__restrict__ valid, const int32_t *__restrict__ info,
     const float *__restrict__ w0,
@@ -2814,10 +2820,10 @@ __global__ __launch_bounds__(256) void k_combine(
 {
     // grid-stride; the convergence counters are reduced per block (one atomic
     // per counter per block: same-address atomics serialise at the memory side)
-    __shared__ int red[3][4];
+    __shared__ int red[4][4];
     __shared__ unsigned long long dred[4];
     const size_t P = (size_t)nsub * nchan;
-    int changed = 0, zero = 0, bad = 0;
+    int changed = 0, zero = 0, bad = 0, near = 0;
     unsigned long long diff = 0ull;   // bit h: W != hist[h] somewhere (h < 64)
     const int hmax = iter < 64 ? iter : 64;
     for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < P; k += (size_t)gridDim.x * blockDim.x) {
@@ -2852,6 +2858,7 @@ __global__ __launch_bounds__(256) void k_combine(
             t = ((0.0 + S[1]) + S[2]) / 2.0;
         }
         test[k] = t;
+        near += fabs(t - 1.0) <= kNearTie;   // false for NaN
         const float wn = (t >= 1.0) ? 0.0f : w0[k];
         W[k] = wn;
         hist[(size_t)iter * P + k] = wn;
@@ -2865,12 +2872,13 @@ __global__ __launch_bounds__(256) void k_combine(
         for (int h = 0; h < hmax; ++h)
             if (!(wn == hist[(size_t)h * P + k])) diff |= 1ull << h;
         for (int h = 64; h < iter; ++h)
-            if (!(wn == hist[(size_t)h * P + k])) atomicOr(&counters[3 + h], 1);
+            if (!(wn == hist[(size_t)h * P + k])) atomicOr(&counters[4 + h], 1);
     }
     for (int off = 32; off > 0; off >>= 1) {
         changed += __shfl_xor(changed, off);
         zero += __shfl_xor(zero, off);
         bad += __shfl_xor(bad, off);
+        near += __shfl_xor(near, off);
         diff |= __shfl_xor(diff, off);
     }
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -2878,24 +2886,27 @@ __global__ __launch_bounds__(256) void k_combine(
         red[0][wave] = changed;
         red[1][wave] = zero;
         red[2][wave] = bad;
+        red[3][wave] = near;
         dred[wave] = diff;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int ch = 0, ze = 0, bd = 0;
+        int ch = 0, ze = 0, bd = 0, nt = 0;
         unsigned long long df = 0ull;
         for (int w = 0; w < nw; ++w) {
             ch += red[0][w];
             ze += red[1][w];
             bd += red[2][w];
+            nt += red[3][w];
             df |= dred[w];
         }
         // counters[0..1] (changed, zero) as one u64 add: both < 2^32, no carry
         if (ch || ze)
             atomicAdd((unsigned long long *)counters, ((unsigned long long)(unsigned)ze << 32) | (unsigned)ch);
         if (bd) atomicAdd(&counters[2], bd);
+        if (nt) atomicAdd(&counters[3], nt);
         for (int h = 0; h < hmax; ++h)
-            if ((df >> h) & 1ull) atomicOr(&counters[3 + h], 1);
+            if ((df >> h) & 1ull) atomicOr(&counters[4 + h], 1);
     }
 }
 

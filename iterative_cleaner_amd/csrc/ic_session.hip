@@ -1203,15 +1203,16 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
                               la.col_med, la.col_mad, la.row_med, la.row_mad, p.chanthresh, p.subintthresh,
                               s->test, s->W, s->hist, n_iter, s->counters));
         if (s->comm)
-            CM(s, s->comm->allreduce_sum_i32(s->counters, (size_t)(n_iter + 3), s->stream), "convergence counters");
-        CK(hipMemcpyAsync(cnt.data(), s->counters, sizeof(int32_t) * (n_iter + 3), hipMemcpyDeviceToHost,
+            CM(s, s->comm->allreduce_sum_i32(s->counters, (size_t)(n_iter + 4), s->stream), "convergence counters");
+        CK(hipMemcpyAsync(cnt.data(), s->counters, sizeof(int32_t) * (n_iter + 4), hipMemcpyDeviceToHost,
                           s->stream));
         CK(hipStreamSynchronize(s->stream));
         if (changed_out) changed_out[n_iter - 1] = cnt[0];
         if (nzero_out) nzero_out[n_iter - 1] = cnt[1];
         s->bad_fits.push_back(cnt[2]);
+        s->stats.near_threshold = cnt[3];
         for (int h = 0; h < n_iter; ++h)
-            if (cnt[3 + h] == 0) {
+            if (cnt[4 + h] == 0) {
                 loops = x;
                 converged = 1;
                 x = 1000000;
