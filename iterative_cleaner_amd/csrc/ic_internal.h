@@ -194,7 +194,8 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
 // Fractional dedispersion (dedisp_mode IC_DEDISP_FFT; phase_rotation.py):
 // out[p] = rot(f32(in[p] - base[p])) by the channel's phasors, sign +1 =
 // dedisperse, -1 = dededisperse.  Rows p = s*nchan + c of ld_in / ldo floats;
-// out2 (optional) receives a second copy; flags: only subints with
+// out2 (optional) receives a second copy (row strides multiples of 4:
+// 16-byte row accesses); flags: only subints with
 // flags[s] != 0.  in may equal out (each row is read whole before it is
 // written).  nbin a power of two, 64 .. 4096.
 struct RotateArgs {

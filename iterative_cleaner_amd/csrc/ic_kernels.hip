@@ -2495,28 +2495,30 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 4 : 2) void k_rotate(Rot
             const int st = a.info[p];
             const bool ok = st >= 1 && st <= 4;
             const double am = a.amp[p];
-            for (int j = t; j < M; j += TB) {
-                const float2 q = *(const float2 *)(x + 2 * j);
-                float r[2] = {0.0f, 0.0f};
+            for (int j2 = t; j2 < M / 2; j2 += TB) {   // 4 samples = 2 complex points per step
+                const float4 q = *(const float4 *)(x + 4 * j2);
+                float r[4] = {0.0f, 0.0f, 0.0f, 0.0f};
                 if (ok) {
-                    const float pv[2] = {q.x, q.y};
+                    const float pv[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-                    for (int e = 0; e < 2; ++e) {
-                        const int i = 2 * j + e;
+                    for (int e = 0; e < 4; ++e) {
+                        const int i = 4 * j2 + e;
                         const double uu = am * a.T64[i];
                         double d = uu - (double)pv[e];
                         if (a.pr_on && i >= a.pr_start && i < a.pr_end) d = d * a.pr_factor;
                         r[e] = (float)d;
                     }
                 }
-                v[rsw(j)] = make_double2((double)r[0], (double)r[1]);
+                v[rsw(2 * j2)] = make_double2((double)r[0], (double)r[1]);
+                v[rsw(2 * j2 + 1)] = make_double2((double)r[2], (double)r[3]);
             }
         } else {
             const float b = a.base ? a.base[p] : 0.0f;
-            for (int j = t; j < M; j += TB) {
-                const float2 q = *(const float2 *)(x + 2 * j);
-                const float x0 = q.x - b, x1 = q.y - b;
-                v[rsw(j)] = make_double2((double)x0, (double)x1);
+            for (int j2 = t; j2 < M / 2; j2 += TB) {
+                const float4 q = *(const float4 *)(x + 4 * j2);
+                const float x0 = q.x - b, x1 = q.y - b, x2 = q.z - b, x3 = q.w - b;
+                v[rsw(2 * j2)] = make_double2((double)x0, (double)x1);
+                v[rsw(2 * j2 + 1)] = make_double2((double)x2, (double)x3);
             }
         }
         gsync<TB / 64>();
@@ -2546,11 +2548,12 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 4 : 2) void k_rotate(Rot
         rot_fft<N>(v, a.tw, t);
         float *o = a.out + p * (size_t)a.ldo;
         float *o2 = a.out2 ? a.out2 + p * (size_t)a.ldo2 : nullptr;
-        for (int j = t; j < M; j += TB) {
-            const double2 r = v[rsw(j)];
-            const float2 y = make_float2((float)(r.x * inv), (float)((-r.y) * inv));
-            *(float2 *)(o + 2 * j) = y;
-            if (o2) *(float2 *)(o2 + 2 * j) = y;
+        for (int j2 = t; j2 < M / 2; j2 += TB) {
+            const double2 r0 = v[rsw(2 * j2)], r1 = v[rsw(2 * j2 + 1)];
+            const float4 y = make_float4((float)(r0.x * inv), (float)((-r0.y) * inv), (float)(r1.x * inv),
+                                         (float)((-r1.y) * inv));
+            *(float4 *)(o + 4 * j2) = y;
+            if (o2) *(float4 *)(o2 + 4 * j2) = y;
         }
         gsync<TB / 64>();   // v is reused by the block's next profile
     }
@@ -3344,7 +3347,7 @@ hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
     const size_t P = (size_t)a.nsub * a.nchan;
     if (P == 0) return hipSuccess;
     if (!rotate_supported(a.nbin) || !a.in || !a.out || !a.ph || !a.tw || a.ld_in < a.nbin || a.ldo < a.nbin ||
-        (a.ld_in & 1) || (a.ldo & 1) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 1))) ||
+        (a.ld_in & 3) || (a.ldo & 3) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 3))) ||
         (a.amp && (!a.T64 || !a.info)))
         return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<size_t>(P, 16384);
