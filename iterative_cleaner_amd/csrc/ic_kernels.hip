@@ -279,57 +279,71 @@ __global__ __launch_bounds__(kWindowThreads) void k_window(const double *__restr
 }
 
 // base[k] = f32( (sum_{t<width} f64(ded[(win+t)%n])) / width ), sequential in t.
-// One wave per 64 profiles; window chunks of 64 positions are loaded coalesced
-// (one profile row per load instruction) into a transposed LDS tile, then each
-// lane adds its own profile's column in order.
 // Per-profile baseline level: f32(sum_seq f64(x_j) / width) over the subint's
 // window, in the dedispersed frame (Appendix C stand-in; oracle orc_baseline).
-// One wave per profile.  The sequential f64 sum of f32 values is computed in
-// parallel when that is provably exact: every x_j is an integer multiple of
-// 2^(emin-150) and |sum| < width * 2^(emax-126), so when
-// ceil(log2 width) + emax - emin + 24 <= 53 every partial sum, in any order,
-// is representable and the result equals the sequential one bit for bit.
-// Otherwise (rare: values spanning > 2^21, or Inf/NaN) the wave walks the
-// window in order.
+// Four profiles per wave, 16 lanes each: a lane issues its window loads in
+// batches of 8 before adding them, so one memory latency serves four profiles
+// (one profile per wave left the kernel bound by a full latency per profile).
+// The sequential f64 sum of f32 values is computed in parallel when that is
+// provably exact: every x_j is an integer multiple of 2^(emin-150) and
+// |sum| < width * 2^(emax-126), so when ceil(log2 width) + emax - emin + 24 <=
+// 53 every partial sum, in any order, is representable and the result equals
+// the sequential one bit for bit.  Otherwise (rare: values spanning > 2^21, or
+// Inf/NaN) the profile's 16 lanes walk the window in order.
 __global__ __launch_bounds__(256) void k_base(const float *__restrict__ raw, const int32_t *__restrict__ shift,
                                               const int32_t *__restrict__ win, const int32_t *__restrict__ flags,
                                               int nsub, int nchan, int nbin, int width, float *__restrict__ base)
 {
+    constexpr int GL = 16, BATCH = 8;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int grp = lane / GL, gl = lane % GL;
     const long P = (long)nsub * nchan;
     const int lgw = 32 - __clz(max(width - 1, 1));   // ceil(log2(width)), >= 1
-    for (long k = (long)blockIdx.x * 4 + wave; k < P; k += (long)gridDim.x * 4) {
-        if (flags && flags[k / nchan] == 0) continue;   // window unchanged: base unchanged
-        int q0 = win[k / nchan] + shift[k % nchan];
-        if (q0 >= nbin) q0 -= nbin;
-        const float *row = raw + (size_t)k * nbin;
+    for (long k0 = ((long)blockIdx.x * 4 + wave) * 4; k0 < P; k0 += (long)gridDim.x * 16) {
+        const long k = k0 + grp;
+        // window unchanged: base unchanged
+        const bool act = k < P && !(flags && flags[k / nchan] == 0);
         double acc = 0.0;
-        int emax = 0, emin = 255;
-        for (int j = lane; j < width; j += 64) {
-            int q = q0 + j;
-            if (q >= nbin) q -= nbin;
-            const float x = row[q];
-            acc = acc + (double)x;
-            const int be = max((int)((__float_as_uint(x) >> 23) & 0xffu), 1);
-            if (x != 0.0f) {
-                emax = max(emax, be);
-                emin = min(emin, be);
+        int emax = 0, emin = 255, q0 = 0;
+        const float *row = raw + (size_t)(act ? k : 0) * nbin;
+        if (act) {
+            q0 = win[k / nchan] + shift[k % nchan];
+            if (q0 >= nbin) q0 -= nbin;
+            for (int j0 = gl; j0 < width; j0 += GL * BATCH) {
+                float xv[BATCH];
+#pragma unroll
+                for (int u = 0; u < BATCH; ++u) {
+                    const int j = j0 + GL * u;
+                    int q = q0 + j;
+                    if (q >= nbin) q -= nbin;
+                    xv[u] = j < width ? row[q] : 0.0f;
+                }
+#pragma unroll
+                for (int u = 0; u < BATCH; ++u) {
+                    const float x = xv[u];
+                    acc = acc + (double)x;
+                    const int be = max((int)((__float_as_uint(x) >> 23) & 0xffu), 1);
+                    if (x != 0.0f) {
+                        emax = max(emax, be);
+                        emin = min(emin, be);
+                    }
+                }
             }
         }
-        for (int off = 32; off > 0; off >>= 1) {
+        for (int off = GL / 2; off > 0; off >>= 1) {   // within the 16-lane group
             acc = acc + __shfl_xor(acc, off);
             emax = max(emax, __shfl_xor(emax, off));
             emin = min(emin, __shfl_xor(emin, off));
         }
-        if (emax != 0 && lgw + emax - emin + 24 > 53) {
-            acc = 0.0;   // in order (uniform: every lane walks the same values)
+        if (act && emax != 0 && lgw + emax - emin + 24 > 53) {
+            acc = 0.0;   // in order (every lane of the group walks the same values)
             for (int j = 0; j < width; ++j) {
                 int q = q0 + j;
                 if (q >= nbin) q -= nbin;
                 acc = acc + (double)row[q];
             }
         }
-        if (lane == 0) base[k] = (float)(acc / (double)width);
+        if (act && gl == 0) base[k] = (float)(acc / (double)width);
     }
 }
 
@@ -3092,7 +3106,7 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
                        int nsub, int nchan, int nbin, int width, float *base)
 {
     const size_t P = (size_t)nsub * nchan;
-    const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
+    const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 16), 16384);
     hipLaunchKernelGGL(k_base, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
     return hipGetLastError();
 }
