@@ -2818,13 +2818,14 @@ __device__ __forceinline__ double nanmax2(double a, double b)
     return a > b ? a : b;
 }
 
+// |test - 1| at or below this counts as a near tie (the fftmax tolerance of
+// the parity tests, DESIGN.md "Numerical semantics")
+constexpr double kNearTie = 1e-9;
+
 // counters: [0] changed vs hist[iter-1], [1] zero weights, [2] profiles whose
 // fit status is not 1-4 (info may be null: 0), [3] profiles whose test value
 // lies within kNearTie of the zap threshold 1.0 (where the last bits of fftmax,
 // not bit-identical to pocketfft, could decide), [4+h] != hist[h]
-// |test - 1| at or below this counts as a near tie (the fftmax tolerance of
-// the parity tests, DESIGN.md "Numerical semantics")
-constexpr double kNearTie = 1e-9;
 
 __global__ __launch_bounds__(256) void k_combine(
     int nsub, int nchan, const uint8_t *__restrict__ valid, const int32_t *__restrict__ info,
