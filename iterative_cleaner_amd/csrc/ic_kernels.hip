@@ -1245,7 +1245,26 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
     if (slot < nact) {
         k = list ? (long)list[slot] : slot;
         int st = S.mode[k];
-        if (st != ST_DONE) {
+        if (st == ST_B) {
+            // after a B sweep only qtf and the inner-loop start change: read the
+            // fields lm_after_b / lm_after_qtf / lm_start_inner use, write the
+            // ones they set (half the state traffic of a full load/store)
+            LmState L;
+            L.Jn0 = S.Jn0[k]; L.f0 = S.f0[k]; L.fnorm = S.fnorm[k]; L.acnorm = S.acnorm[k]; L.r = S.r[k];
+            L.diag = S.diag[k]; L.delta = S.delta[k]; L.par = S.par[k]; L.x = S.x[k]; L.iter = S.iter[k];
+            L.info = 0;
+            st = lm_after_b(L, S.o_sum[k]);
+            S.qtf[k] = L.qtf; S.gnorm[k] = L.gnorm; S.diag[k] = L.diag; S.par[k] = L.par;
+            S.delta[k] = L.delta; S.wa1[k] = L.wa1; S.x2[k] = L.x2; S.pnorm[k] = L.pnorm;
+            S.mode[k] = st;
+            if (st == ST_A2) S.xa[k] = L.x2;
+            if (st == ST_DONE) {
+                amp_o[k] = L.x;
+                info_o[k] = L.info;
+            } else {
+                still = 1;
+            }
+        } else if (st != ST_DONE) {
             LmState L;
             lm_load(L, S, k);
             if (st == ST_A0) {
@@ -1262,8 +1281,6 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
                 L.J02 = S.o_J0[k];
                 st = lm_after_a2(L, S.o_fnorm[k]);
                 if (L.x == L.x2) S.slow[k] = S.o_exact[k];
-            } else {
-                st = lm_after_b(L, S.o_sum[k]);
             }
             lm_store(L, S, k);
             S.mode[k] = st;
