@@ -62,6 +62,7 @@ CASES = [
     (5, 70, 1024, 18, 0.2, {}),
     (4, 30, 2048, 19, 0.3, {}),
     (6, 40, 4096, 13, 0.1, {}),
+    (4, 3200, 1024, 1, 0.05, {}),             # the C2 channel count: 13 super-blocks
 ]
 
 
