@@ -56,3 +56,29 @@ def test_cli_stokes_archive_cleans_total_intensity(tmp_path, monkeypatch, capsys
     res = ica.Archive_load("iquv_cleaned.ar")
     assert res.get_state() == "Stokes" and res.get_npol() == 4
     assert bits_equal(res.get_weights(), ref["weights"])
+
+
+def test_cli_foreign_psrfits_fractional_dedispersion(tmp_path, monkeypatch, capsys, oracle_lib):
+    """A PSRFITS file without the stand-in's columns, with DM / DAT_FREQ / PERIOD:
+    IC_DEDISPERSION=fft dedisperses by the FFT phase rotation with the exact
+    fractional delays (psrfits.fractional_dedispersion); the zap mask equals the
+    C oracle's loop with those delays."""
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import cleaner, psrfits, synth
+    monkeypatch.chdir(tmp_path)
+    data, w, shift = synth.make_cube(10, 64, 256, 61, 0.2, npol=2)
+    ar = ica.Archive(data, w, np.zeros(64, np.int64), filename="dm.sf")
+    ar._chan_freqs = 1300.0 + np.arange(64) * 3.0
+    ar._period = 0.0125
+    ar._dm = 20.0
+    psrfits.save(ar, "dm.sf", stand_in_meta=False)
+    monkeypatch.setenv("IC_DEDISPERSION", "fft")
+    src = psrfits.load("dm.sf")
+    delay = src.get_dm_delay()
+    assert delay is not None and np.any(delay != np.rint(delay))
+    dec = src.get_data()
+    cube = (dec[:, 0] + dec[:, 1]).astype(np.float32)
+    ref = oracle_lib.clean_loop(cube, src.get_weights(), src.get_dm_shift(), delay=delay)
+    cleaner.main(cleaner.parse_arguments(["-l", "-q", "dm.sf"]))
+    res = ica.Archive_load("dm_cleaned.ar")
+    assert bits_equal(res.get_weights(), ref["weights"])
