@@ -253,13 +253,14 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def fast_mode_summary(_native, cube, w0, shift, shape, device, steps, torch):
+def fast_mode_summary(_native, cube, w0, shift, shape, device, steps, torch, delay=None):
     """fit_mode 1 (closed-form amplitude fused with the diagnostics) on the same
     archive: profiles/s, the loop's SURVEY §8(d) HBM fraction, and (filled in by
     the caller) the zap-mask flips against the exact mode.  Not the reference's
     arithmetic; the headline value stays the exact mode's."""
     nsub, nchan, nbin = shape
-    with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=device, fit_mode=_native.FIT_CLOSED) as s:
+    with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=device, fit_mode=_native.FIT_CLOSED,
+                            delay=delay) as s:
         s.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
         s.run(fetch=False)
         torch.cuda.synchronize()
@@ -375,10 +376,8 @@ def main():
                          "(profiling passes, whose kernel tallies it would mix in)")
     ap.add_argument("--dedisp", choices=("shift", "fft"), default="shift",
                     help="shift: integer dedispersion shifts (default); fft: fractional delays, dedispersed by "
-                         "psrchive's FFT phase rotation (dedisp_mode IC_DEDISP_FFT, exact fit only)")
+                         "psrchive's FFT phase rotation (dedisp_mode IC_DEDISP_FFT)")
     a = ap.parse_args()
-    if a.dedisp == "fft" and a.fit_mode != "exact":
-        raise SystemExit("--dedisp fft needs --fit-mode exact")
 
     import torch
     import torch.distributed as dist
@@ -435,14 +434,14 @@ def main():
     torch.cuda.synchronize()
     sess.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
     fast = None
-    if fit_mode == _native.FIT_EXACT and not sharded and world == 1 and not a.no_fast_summary and delay is None:
+    if fit_mode == _native.FIT_EXACT and not sharded and world == 1 and not a.no_fast_summary:
         # the north star's fast mode on the same archive, beside the exact line
-        fast = fast_mode_summary(_native, cube, w0, shift, (nsub, nchan, nbin), local, a.steps, torch)
+        fast = fast_mode_summary(_native, cube, w0, shift, (nsub, nchan, nbin), local, a.steps, torch, delay)
     flips = None
     if fit_mode == _native.FIT_CLOSED and not sharded and not a.no_flip_check:
         # zap-mask flips of the fast mode against the exact fit on this archive (untimed)
         fres = sess.run()
-        with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local) as ex:
+        with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local, delay=delay) as ex:
             ex.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
             exact = ex.run()
         flips = {"profiles": int(np.count_nonzero(fres["weights"] != exact["weights"])),

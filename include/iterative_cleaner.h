@@ -89,8 +89,8 @@ typedef struct {
  *                    phase_rotation.py (bit-identical to it and to the C oracle;
  *                    within one f32 ulp of numpy's irfft(rfft(x) * phasor);
  *                    parity with real psrchive unpinned).  nbin must be a power of
- *                    two in 64..4096 and fit_mode IC_FIT_EXACT; the shift arrays
- *                    of the uploads are then unused (pass zeros). */
+ *                    two in 64..4096 (either fit_mode); the shift arrays of the
+ *                    uploads are then unused (pass zeros). */
 #define IC_DEDISP_SHIFT 0
 #define IC_DEDISP_FFT 1
 

@@ -154,7 +154,10 @@ hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, lo
 // amplitude sum(T*p)/TT from raw + base (written to amp/info), then the same
 // residual; DIAG_STATS = comprehensive_stats of the rows of D alone (no shift).
 // tw: exp(-2 pi i q/nbin), q < nbin; tw_p2 (power-of-two nbin only): see p2_twiddles()
-enum DiagMode { DIAG_EXACT = 0, DIAG_CLOSED = 1, DIAG_STATS = 2 };
+// DIAG_FIT = the closed-form amplitude alone (amp/info) of the rows of D (no
+// shift, no level): fit_mode 1 with fractional dedispersion, whose residual is
+// then rotated back and measured in DIAG_STATS.
+enum DiagMode { DIAG_EXACT = 0, DIAG_CLOSED = 1, DIAG_STATS = 2, DIAG_FIT = 3 };
 struct DiagArgs {
     int mode;
     const float *D;

@@ -2122,10 +2122,10 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
 #pragma unroll
         for (int u = 0; u < NPT; ++u) tv[u] = T[t + TPP * u];
     }
-    const double TT = mode == DIAG_CLOSED ? *a.TT : 0.0;
-    constexpr bool closed = mode == DIAG_CLOSED;
-    const float *rows = closed ? a.raw : a.D;
-    const size_t ld = closed ? (size_t)N : (size_t)a.ldD;
+    constexpr bool closed = mode == DIAG_CLOSED || mode == DIAG_FIT;
+    const double TT = closed ? *a.TT : 0.0;
+    const float *rows = mode == DIAG_CLOSED ? a.raw : a.D;
+    const size_t ld = mode == DIAG_CLOSED ? (size_t)N : (size_t)a.ldD;
     float pv[NPT];
     unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group);
     // per-profile scalars, loaded one profile ahead as well
@@ -2141,9 +2141,9 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             nx = a.amp[k];
             nst = a.info[k];
         }
-        if (closed) nb = a.base[k];
+        if (mode == DIAG_CLOSED) nb = a.base[k];
         nw = a.w0[k];
-        nsh = mode == DIAG_STATS ? 0 : a.shift[k % (unsigned)nchan];
+        nsh = (mode == DIAG_STATS || mode == DIAG_FIT) ? 0 : a.shift[k % (unsigned)nchan];
     }
     for (; k < P; k += stride) {
         // opaque to the optimiser: the LDS addresses of the FFT stages derive
@@ -2198,6 +2198,14 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             }
             gsync<WPP>();
         }
+        if constexpr (mode == DIAG_FIT) {   // the amplitude is all this mode produces
+            if (PREFETCH && k + stride < P) {
+                const float *pn = rows + (size_t)(k + stride) * ld;
+#pragma unroll
+                for (int u = 0; u < NPT; ++u) pv[u] = pn[t + TPP * u];
+            }
+            continue;
+        }
         const bool ok = st >= 1 && st <= 4;
         // residual -> X (dispersed frame, padded addresses)
         // X = apply_weights(R, w0): f32(R * w), or f64(R) * f64(w) for f64 data
@@ -2239,7 +2247,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
                 nx = a.amp[kn];
                 nst = a.info[kn];
             }
-            if (closed) nb = a.base[kn];
+            if (mode == DIAG_CLOSED) nb = a.base[kn];
             nw = a.w0[kn];
             nsh = mode == DIAG_STATS ? 0 : a.shift[kn % (unsigned)nchan];
         }
@@ -3265,6 +3273,8 @@ static hipError_t launch_p2(hipStream_t st, const DiagArgs &a, size_t P)
         hipLaunchKernelGGL((k_diag_p2<NN, DIAG_EXACT, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     else if (a.mode == DIAG_CLOSED)
         hipLaunchKernelGGL((k_diag_p2<NN, DIAG_CLOSED, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
+    else if (a.mode == DIAG_FIT)   // f32 rows either way (launch_diag passes D64 = false)
+        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_FIT, false>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     else   // comprehensive_stats of given rows (f64 data: the fractional-dedispersion loop)
         hipLaunchKernelGGL((k_diag_p2<NN, DIAG_STATS, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     return hipGetLastError();
@@ -3276,15 +3286,17 @@ hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
     const size_t P = (size_t)a.nsub * a.nchan;
     if (P == 0) return hipSuccess;
     if (a.mode == DIAG_CLOSED ? (!a.raw || !a.base || !a.TT || !a.amp || !a.info)
-                              : (!a.D || a.ldD < nbin || (a.mode == DIAG_EXACT && (!a.amp || !a.info))))
+                              : (!a.D || a.ldD < nbin || (a.mode != DIAG_STATS && (!a.amp || !a.info)) ||
+                                 (a.mode == DIAG_FIT && !a.TT)))
         return hipErrorInvalidValue;
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
-        if (a.data_f64) return launch_p2<NN, true>(st, a, P);                                      \
+        if (a.data_f64 && a.mode != DIAG_FIT) return launch_p2<NN, true>(st, a, P);                \
         return launch_p2<NN, false>(st, a, P);                                                     \
     }
     IC_P2(64) IC_P2(128) IC_P2(256) IC_P2(512) IC_P2(1024) IC_P2(2048) IC_P2(4096)
 #undef IC_P2
+    if (a.mode == DIAG_FIT) return hipErrorInvalidValue;   // power-of-two nbin only
     // nleaf/nops upper bound from nbin: leaves >= 64 samples except tiny n
     const int nleaf_ub = nbin <= 128 ? 1 : (nbin / 64 + 1);
     const DiagLayout lay = diag_layout(nbin, nleaf_ub, nleaf_ub);

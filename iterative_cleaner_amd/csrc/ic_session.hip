@@ -689,8 +689,6 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         return fail(IC_EINVAL, "dedisp_mode %d unsupported", p.dedisp_mode);
     if (p.dedisp_mode == IC_DEDISP_FFT && !rotate_supported(p.nbin))
         return fail(IC_EINVAL, "fractional dedispersion needs a power-of-two nbin in 64..4096 (nbin=%d)", p.nbin);
-    if (p.dedisp_mode == IC_DEDISP_FFT && p.fit_mode != IC_FIT_EXACT)
-        return fail(IC_EINVAL, "fractional dedispersion is implemented for the exact fit (fit_mode 0) only");
     if (diag_lds_bytes(p.nbin) > 160 * 1024)
         return fail(IC_EINVAL, "nbin=%d needs %zu bytes of LDS for the diagnostics (> 160 KiB)", p.nbin,
                     diag_lds_bytes(p.nbin));
@@ -753,7 +751,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     const bool exact = p.fit_mode == IC_FIT_EXACT;
     AL(s->slot_raw[0], N);
     s->raw = s->slot_raw[0];
-    if (exact) {   // the closed-form fit reads the raw cube; no fit cube, no lmdif state
+    // the closed-form fit reads the raw cube (no fit cube, no lmdif state), unless
+    // the dedispersion is the FFT rotation: then the rotated fit cube is kept
+    if (exact || p.dedisp_mode == IC_DEDISP_FFT) {
         AL(s->D, s->Ppad * (size_t)s->ldD);
         if (hipMemset(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD) != hipSuccess)
             return bail(fail(IC_EHIP, "hipMemset(D) failed"));
@@ -1184,6 +1184,11 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             LAUNCH(s, K_TNORM, launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
         }
         if (s->fftded) {
+            if (p.fit_mode == IC_FIT_CLOSED) {   // the closed-form amplitudes of the rotated fit cube
+                DiagArgs fa = da;
+                fa.mode = DIAG_FIT;
+                LAUNCH(s, K_DIAG, launch_diag(s->stream, fa));
+            }
             // residual in the dedispersed frame, dededispersed by the inverse
             // rotation (ic.py:101-104), then comprehensive_stats of those rows
             LAUNCH(s, K_ROTATE, launch_rotate(s->stream, residual_rotate_args(s, pr_start, pr_end)));

@@ -106,6 +106,39 @@ def test_fft_loop_matches_c_oracle(case, fit_tail, oracle_lib):
     assert _same(R, ref["residual"])
 
 
+@pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[4], CASES[6]], ids=lambda c: "%dx%dx%d" % c[:3])
+def test_fft_closed_form_loop_matches_c_oracle(case, oracle_lib):
+    """fit_mode 1 (closed-form amplitude) with fractional dedispersion: the
+    amplitudes of the rotated fit cube (k_diag DIAG_FIT), then the same rotated
+    residual and statistics as the exact fit."""
+    from iterative_cleaner_amd import _native, synth
+    nsub, nchan, nbin, seed, rfi, extra = case
+    data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
+    delay = synth.fractional_delays(shift, nbin)
+    raw = np.ascontiguousarray(data[:, 0])
+    args = dict(max_iter=5, chanthresh=5.0, subintthresh=5.0, pulse_region=[0, 0, 1])
+    args.update(extra)
+    ref = oracle_lib.clean_loop(raw, w0, shift, args["chanthresh"], args["subintthresh"], args["max_iter"],
+                                _pr(args, nbin), want_residual=True, want_details=True, fit_mode=1, delay=delay)
+    with _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"], args["subintthresh"],
+                            args["pulse_region"], device=0, delay=delay, fit_mode=_native.FIT_CLOSED) as s:
+        s.upload(raw, w0, np.zeros(nchan, np.int32))
+        out = s.run()
+        T = s.template()
+        amp, info = s.fit()
+        sd, mn, pt, ff = s.diagnostics()
+        R = s.residual()
+        st = s.run_stats()
+    assert st["fit_rounds"] == 0
+    assert out["loops"] == ref["loops"]
+    assert bits_equal(T, ref["T"][out["n_iter"] - 1])
+    assert bits_equal(amp, ref["amp"]) and bits_equal(info, ref["info"])
+    assert bits_equal(out["weights"], ref["weights"])
+    assert bits_equal(sd, ref["std"]) and bits_equal(mn, ref["mean"]) and bits_equal(pt, ref["ptp"])
+    assert _close(ff, ref["fft"]) and _close(out["test"], ref["test"])
+    assert _same(R, ref["residual"])
+
+
 def test_fft_pols_f64_and_local_shards(oracle_lib):
     """Device pscrunch, f64 data and in-process channel shards in FFT mode."""
     import threading
@@ -157,8 +190,6 @@ def test_fft_mode_argument_errors():
     from iterative_cleaner_amd import _native
     with pytest.raises(_native.NativeError, match="power-of-two"):
         _native.GpuSession(4, 8, 100, device=0, delay=np.zeros(8))
-    with pytest.raises(_native.NativeError, match="exact fit"):
-        _native.GpuSession(4, 8, 64, device=0, delay=np.zeros(8), fit_mode=_native.FIT_CLOSED)
     with pytest.raises(_native.NativeError, match="not finite"):
         _native.GpuSession(4, 8, 64, device=0, delay=np.full(8, np.nan))
     with pytest.raises(_native.NativeError, match="power-of-two"):
