@@ -1942,11 +1942,33 @@ struct P2 {
 };
 
 __device__ __forceinline__ int xaddr(int idx) { return idx + 8 * (idx >> 7); }
+
+// xaddr((j0 + TPP u) mod N) for 0 <= j0 < N, in 3 VALU ops per u: the
+// unwrapped address has compile-time offsets from one base (two for TPP = 64:
+// xaddr(j0 + 64 u) = xaddr(j0) + 64 u + 8 ((u + bit6(j0)) >> 1)), and
+// xaddr(j + N) = xaddr(j) + xaddr(N), so the wrap is an unsigned min
+template <int N, int TPP>
+struct XWrap {
+    int a0, a1;
+    __device__ __forceinline__ explicit XWrap(int j0) : a0(xaddr(j0)), a1(TPP == 64 ? xaddr(j0) + ((j0 >> 3) & 8) : 0) {}
+    __device__ __forceinline__ int operator()(int u) const
+    {
+        constexpr int XN = N + 8 * (N >> 7);
+        const int off = TPP % 128 == 0 ? u * (TPP + TPP / 16) : 64 * u + 8 * (u >> 1);
+        const int au = ((TPP == 64 && (u & 1)) ? a1 : a0) + off;
+        return (int)min((unsigned)au, (unsigned)(au - XN));
+    }
+};
 // complex work array slot of point q: XOR swizzle of the low 3 bits with bits
 // 3-5.  Conflict-free for every access of the kernel: the radix-8 scatters
 // (ds_write_b128, 8-lane groups over 32 banks: low bits (b&7)^r or r^(b&7)) and
 // the contiguous / reversed gathers (ds_read_b128, 16-lane groups over 64 banks).
 __device__ __forceinline__ int cidx(int q) { return q ^ ((q >> 3) & 7); }
+// Address forms with compile-time offsets (the thread index is opaque to the
+// compiler, so it cannot split these itself):
+//   cidx(x + 64 m) = cidx(x) + 64 m                 (the XOR reads bits 3-5 only)
+//   xaddr(x + 8 q) = xaddr(x) + 8 q                 if x % 128 + 8 q < 128
+//   xaddr(x + 128 m) = xaddr(x) + 136 m
 
 // barrier of a profile group: one wave needs only ordering of its LDS ops
 template <int WPP>
@@ -2013,19 +2035,23 @@ __device__ __forceinline__ void p2_stage(double2 *C, const XT *X, double mu, con
     for (int u = 0; u < BPL; ++u) {
         const int b = t + TPP * u;
         if (NB % TPP == 0 || b < NB) {
+            // 2 q = 2 b + 2 r NB: a multiple of 128 apart when NB % 64 == 0
+            const XT *xb = X + xaddr(2 * b);
+            const double2 *cb = C + cidx(b);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int q = b + r * NB;
                 if (FIRST) {
+                    const XT *xq = NB % 64 == 0 ? xb + r * (2 * NB + NB / 8) : X + xaddr(2 * q);
                     if constexpr (sizeof(XT) == 8) {
-                        const double2 xv = *(const double2 *)(X + xaddr(2 * q));
+                        const double2 xv = *(const double2 *)xq;
                         v[u][r] = make_double2(xv.x - mu, xv.y - mu);
                     } else {
-                        const float2 xv = *(const float2 *)(X + xaddr(2 * q));
+                        const float2 xv = *(const float2 *)xq;
                         v[u][r] = make_double2((double)xv.x - mu, (double)xv.y - mu);
                     }
                 } else {
-                    v[u][r] = C[cidx(q)];
+                    v[u][r] = NB % 64 == 0 ? cb[r * NB] : C[cidx(q)];
                 }
             }
         }
@@ -2043,8 +2069,23 @@ __device__ __forceinline__ void p2_stage(double2 *C, const XT *X, double mu, con
             }
             dft_small<R>(v[u]);
             const int idx = (b - k) * R + k;
+            if constexpr (NS % 64 == 0) {
+                double2 *cw = C + cidx(idx);
 #pragma unroll
-            for (int r = 0; r < R; ++r) C[cidx(idx + r * NS)] = v[u][r];
+                for (int r = 0; r < R; ++r) cw[r * NS] = v[u][r];
+            } else if constexpr (NS == 8 && R == 8) {
+                // idx = 64 m + k (k < 8): cidx(idx + 8 r) = 64 m + 8 r + (k ^ r)
+#pragma unroll
+                for (int r = 0; r < R; ++r) C[(idx ^ r) + 8 * r] = v[u][r];
+            } else if constexpr (NS == 1 && R == 8) {
+                // idx = 8 b: cidx(idx + r) = idx + (r ^ (b & 7)) = (idx + (b & 7)) ^ r
+                const int A = idx + (b & 7);
+#pragma unroll
+                for (int r = 0; r < R; ++r) C[A ^ r] = v[u][r];
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) C[cidx(idx + r * NS)] = v[u][r];
+            }
         }
     }
     gsync<TPP / 64>();
@@ -2164,24 +2205,24 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         if (closed) {
             // fit cube row p_i = f32(ded_i - base0), i = (j - sh) mod N: to LDS in
             // the dedispersed order, then a = sum(T*p)/sum(T*T) over the chains
+            const XWrap<N, TPP> xw((t - sh) & (N - 1));
 #pragma unroll
-            for (int u = 0; u < NPT; ++u) {
-                const int j = t + TPP * u;
-                X[xaddr((j - sh) & (N - 1))] = (XT)(pv[u] - bk);
-            }
+            for (int u = 0; u < NPT; ++u) X[xw(u)] = (XT)(pv[u] - bk);
             gsync<WPP>();
             double cs[C::CPL];
-            const bool act = t < C::ACT;
+            const bool act = C::ACT >= TPP || t < C::ACT;   // every thread holds a chain at N >= 512
 #pragma unroll
             for (int sl = 0; sl < C::CPL; ++sl) {
                 const int ch = t + TPP * sl;
                 const int base = (ch >> 3) * C::LEAF + (ch & 7);
                 double r = 0.0;
                 if (act) {
-                    r = T[base] * (double)X[xaddr(base)];
+                    // base % 128 < 8 and 8 q < LEAF <= 128
+                    const XT *xb = X + xaddr(base);
+                    r = T[base] * (double)xb[0];
 #pragma unroll
                     for (int q = 1; q < C::CL; ++q) {
-                        const double pr = T[base + 8 * q] * (double)X[xaddr(base + 8 * q)];
+                        const double pr = T[base + 8 * q] * (double)xb[8 * q];
                         r = r + pr;
                     }
                 }
@@ -2191,7 +2232,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             x = TT != 0.0 ? dot / TT : 0.0;
             st = isfinite(x) ? 1 : 5;
 #pragma unroll
-            for (int u = 0; u < NPT; ++u) pv[u] = (float)X[xaddr(t + TPP * u)];
+            for (int u = 0; u < NPT; ++u) pv[u] = (float)X[TPP % 128 == 0 ? xaddr(t) + u * (TPP + TPP / 16) : xaddr(t + TPP * u)];
             if (t == 0) {
                 a.amp[k] = x;
                 a.info[k] = st;
@@ -2215,8 +2256,9 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         };
         if (mode == DIAG_STATS) {
 #pragma unroll
-            for (int u = 0; u < NPT; ++u) X[xaddr(t + TPP * u)] = weigh(pv[u]);
+            for (int u = 0; u < NPT; ++u) X[TPP % 128 == 0 ? xaddr(t) + u * (TPP + TPP / 16) : xaddr(t + TPP * u)] = weigh(pv[u]);
         } else if (a.pr_on) {
+            const XWrap<N, TPP> xw((t + sh) & (N - 1));
 #pragma unroll
             for (int u = 0; u < NPT; ++u) {
                 const int i = t + TPP * u;
@@ -2224,16 +2266,17 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
                 double e = uu - (double)pv[u];
                 if (i >= a.pr_start && i < a.pr_end) e = e * a.pr_factor;
                 const float R = ok ? (float)e : 0.0f;
-                X[xaddr((i + sh) & (N - 1))] = weigh(R);
+                X[xw(u)] = weigh(R);
             }
         } else {
+            const XWrap<N, TPP> xw((t + sh) & (N - 1));
 #pragma unroll
             for (int u = 0; u < NPT; ++u) {
                 const int i = t + TPP * u;
                 const double uu = x * (TREG ? tv[u] : T[i]);
                 const double e = uu - (double)pv[u];
                 const float R = ok ? (float)e : 0.0f;
-                X[xaddr((i + sh) & (N - 1))] = weigh(R);
+                X[xw(u)] = weigh(R);
             }
         }
         if (k + stride < P) {
@@ -2257,13 +2300,13 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         if (valid) {
             // chain values -> registers
             XT v[C::CPL][C::CL];
-            const bool act = t < C::ACT;
+            const bool act = C::ACT >= TPP || t < C::ACT;   // every thread holds a chain at N >= 512
 #pragma unroll
             for (int sl = 0; sl < C::CPL; ++sl) {
                 const int ch = t + TPP * sl;
                 const int base = (ch >> 3) * C::LEAF + (ch & 7);
 #pragma unroll
-                for (int q = 0; q < C::CL; ++q) v[sl][q] = act ? X[xaddr(base + 8 * q)] : (XT)0;
+                for (int q = 0; q < C::CL; ++q) v[sl][q] = act ? X[xaddr(base) + 8 * q] : (XT)0;
             }
             // mean: pairwise sum in the data dtype (f32, or f64 for f64 data)
             XT fs[C::CPL];
@@ -2294,21 +2337,29 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             sd = sqrt(ss / (double)N);
             // ptp (NaN-propagating), in the data dtype
             XT mx = -INFINITY, mn = INFINITY;
-            int nan = 0;
             if (act) {
 #pragma unroll
                 for (int sl = 0; sl < C::CPL; ++sl)
 #pragma unroll
                     for (int q = 0; q < C::CL; ++q) {
-                        const XT tq = v[sl][q];
-                        nan |= isnan(tq);
-                        mx = OpMaxF()(mx, tq);
-                        mn = OpMinF()(mn, tq);
+                        mx = OpMaxF()(mx, v[sl][q]);
+                        mn = OpMinF()(mn, v[sl][q]);
                     }
             }
             mx = group_tree<WPP, 64>(mx, OpMaxF(), (XT *)(red + 32), wave, lane);
             mn = group_tree<WPP, 64>(mn, OpMinF(), (XT *)(red + 36), wave, lane);
-            nan = group_tree<WPP, 64>(nan, OpOr(), (int *)(red + 40), wave, lane);
+            // a NaN sample makes the pairwise sum s32 NaN; a NaN s32 without one
+            // (inf - inf) is rare, and only then are the samples checked one by one
+            int nan = 0;
+            if (isnan(s32)) {   // group-uniform
+                if (act) {
+#pragma unroll
+                    for (int sl = 0; sl < C::CPL; ++sl)
+#pragma unroll
+                        for (int q = 0; q < C::CL; ++q) nan |= isnan(v[sl][q]);
+                }
+                nan = group_tree<WPP, 64>(nan, OpOr(), (int *)(red + 40), wave, lane);
+            }
             ptp = nan ? (double)NAN : (double)(XT)(mx - mn);
             // rFFT of f64(X) - mean: N/2-point complex Stockham, in place
             p2_fft<C::M, TPP, C::LG, 0, 1, C::M, XT>(Cb, X, mean, tw, t);
@@ -2322,8 +2373,11 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             for (int j = 0; j < (C::M + TPP - 1) / TPP; ++j) {
                 const int kk = t + TPP * j;
                 if (C::M % TPP != 0 && kk >= C::M) continue;   // M = 32 (N = 64)
-                const double2 zk = Cb[cidx(kk)];
-                const double2 zm = Cb[cidx(kk == 0 ? 0 : C::M - kk)];
+                // kk = t + TPP j, M - kk = (TPP - t) + (M - TPP (j + 1)): 64-multiples apart
+                constexpr bool F = TPP % 64 == 0 && C::M % 64 == 0;
+                const double2 zk = F ? Cb[cidx(t) + TPP * j] : Cb[cidx(kk)];
+                const double2 zm = F ? Cb[kk == 0 ? 0 : cidx(TPP - t) + (C::M - TPP * (j + 1))]
+                                     : Cb[cidx(kk == 0 ? 0 : C::M - kk)];
                 const double er = zk.x + zm.x, ei = zk.y - zm.y;
                 const double orr = zk.y + zm.y, oi = zm.x - zk.x;
                 const double2 wv = tw[kk];
@@ -2411,13 +2465,19 @@ struct RotCfg {
     static constexpr int TB = M / 8 < 64 ? 64 : (M / 8 > 256 ? 256 : M / 8);
 };
 
-// LDS address of complex point i: the low 4 bits XOR bits 3..6, so that 16
-// consecutive lanes hit 16 distinct 16-byte bank groups for the contiguous
-// (i = ja + q G) and the strided (i = 8 ja + q, 64 a + b + 8 q) patterns
-#ifndef IC_ROT_SWIZZLE
-#define IC_ROT_SWIZZLE 0
+// LDS slot of complex point i: one pad slot after every 8 points.
+// ds_write_b128 serves 8 contiguous lanes per LDS cycle on the 8 16-byte slots
+// of a 128-B row, so unpadded the first pass's stores (lane ja -> points
+// 8 ja + q) are 8-way on one slot; padded, every store pattern of the passes
+// (8 ja + q, 64 a + b + 8 q, 512 a + b + 64 q) is conflict-free, the
+// contiguous ds_read_b128 reads are 2-way, and the addresses keep their
+// per-q immediate offsets (an XOR swizzle, conflict-free on both, needs an
+// address register per q and spills at N = 1024).
+#ifndef IC_ROT_PAD
+#define IC_ROT_PAD 1
 #endif
-__device__ __forceinline__ int rsw(int i) { return IC_ROT_SWIZZLE ? i ^ ((i >> 3) & 15) : i; }
+__device__ __forceinline__ constexpr int rsw(int i) { return IC_ROT_PAD ? i + (i >> 3) : i; }
+template <int M> constexpr int rot_lds_slots() { return IC_ROT_PAD ? M + M / 8 : M; }
 
 // R consecutive radix-2 Stockham stages (ns = 2^lg .. 2^(lg+R-1)) through
 // registers: group ja < G = M/2^R holds the 2^R points v[ja + q G]; the stages
@@ -2426,8 +2486,20 @@ __device__ __forceinline__ int rsw(int i) { return IC_ROT_SWIZZLE ? i ^ ((i >> 3
 // at v[(ja / ns) 2^R ns + ja mod ns + p ns].  Same operations, same operands as
 // R separate stages (phase_rotation._stockham), i.e. the same bits, with one
 // LDS round trip instead of R.
+// 16-byte loads of the twiddle / phasor tables through a buffer descriptor:
+// a 32-bit per-lane offset plus an immediate, instead of a 64-bit address
+// register per table entry kept live across the profile loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rot_rsrc(const double2 *p, unsigned entries)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(p), 0, (int)(16u * entries), 0x00020000);
+}
+__device__ __forceinline__ double2 rot_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
+{
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
 template <int N, int R, int LGS>
-__device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__ tw, int t)
+__device__ __forceinline__ void rot_pass(double2 *v, __amdgpu_buffer_rsrc_t twr, int t)
 {
     using C = RotCfg<N>;
     constexpr int M = C::M, TB = C::TB, G = M >> R, Q = 1 << R, HALF = Q / 2;
@@ -2443,12 +2515,22 @@ __device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__
         const int k = ja & (ns - 1);
         if (G % TB == 0 || ja < G) {
 #pragma unroll
-            for (int l = 0; l < R; ++l)
+            for (int l = 0; l < R; ++l) {
+                // tw[(kl ns + k) S], S = N / 2^(l + LGS + 1)
+                constexpr unsigned S0 = 16u * (N >> (LGS + 1));
+                const unsigned kb = ((unsigned)k * S0) >> l;
 #pragma unroll
                 for (int kl = 0; kl < (1 << l); ++kl)
-                    w[gi][(1 << l) - 1 + kl] = tw[(kl * ns + k) * (N >> (l + LGS + 1))];
+                    w[gi][(1 << l) - 1 + kl] = rot_ld(twr, kb, (unsigned)(kl * ns) * (S0 >> l));
+            }
+            if constexpr (G % 8 == 0) {
+                const double2 *vj = v + rsw(ja);    // rsw(ja + q G) = rsw(ja) + rsw(q G)
 #pragma unroll
-            for (int q = 0; q < Q; ++q) u[gi][q] = v[rsw(ja + q * G)];
+                for (int q = 0; q < Q; ++q) u[gi][q] = vj[rsw(q * G)];
+            } else {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) u[gi][q] = v[rsw(ja + q * G)];
+            }
         }
     }
     gsync<C::TB / 64>();
@@ -2476,8 +2558,15 @@ __device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__
                 for (int q = 0; q < Q; ++q) u[gi][q] = w2[q];
             }
             const int base = ((ja >> LGS) << (LGS + R)) + k;
+            if constexpr (ns == 1 || ns % 8 == 0) {
+                // ns = 1: base is a multiple of Q <= 8, so base + q stays in base's 8-block
+                double2 *vb = v + rsw(base);
 #pragma unroll
-            for (int q = 0; q < Q; ++q) v[rsw(base + q * ns)] = u[gi][q];
+                for (int q = 0; q < Q; ++q) vb[ns == 1 ? q : rsw(q * ns)] = u[gi][q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) v[rsw(base + q * ns)] = u[gi][q];
+            }
         }
     }
     gsync<C::TB / 64>();
@@ -2485,13 +2574,13 @@ __device__ __forceinline__ void rot_pass(double2 *v, const double2 *__restrict__
 
 // the full N/2-point FFT: passes of 3 stages (the last one shorter)
 template <int N, int LG0 = 0>
-__device__ __forceinline__ void rot_fft(double2 *v, const double2 *__restrict__ tw, int t)
+__device__ __forceinline__ void rot_fft(double2 *v, __amdgpu_buffer_rsrc_t twr, int t)
 {
     constexpr int LG = RotCfg<N>::LG;
     if constexpr (LG0 < LG) {
         constexpr int R = LG - LG0 >= 3 ? 3 : LG - LG0;
-        rot_pass<N, R, LG0>(v, tw, t);
-        rot_fft<N, LG0 + R>(v, tw, t);
+        rot_pass<N, R, LG0>(v, twr, t);
+        rot_fft<N, LG0 + R>(v, twr, t);
     }
 }
 
@@ -2513,36 +2602,76 @@ __device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
     return make_double2(er - oi, ei + orr);
 }
 
+// A/B knobs: waves per SIMD at N <= 1024; prefetch of the post step's
+// twiddles/phasors one pair ahead; prefetch of the next profile's rows
+#ifndef IC_ROT_OCC
+#define IC_ROT_OCC 4
+#endif
+#ifndef IC_ROT_POSTPF
+#define IC_ROT_POSTPF 0
+#endif
+#ifndef IC_ROT_NEXTPF
+#define IC_ROT_NEXTPF 0
+#endif
 template <int N>
-__global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 4 : 2) void k_rotate(RotateArgs a)
+__global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_rotate(RotateArgs a)
 {
     using C = RotCfg<N>;
     constexpr int M = C::M, H = C::H, TB = C::TB;
-    __shared__ double2 v[M];
+    constexpr int NJ = (M / 2 + TB - 1) / TB;    // float4 rows per lane (4 samples = 2 points)
+    constexpr int NK = H / TB + 1;               // spectrum pairs (k, M - k) per lane, k <= H
+    __shared__ double2 v[rot_lds_slots<M>()];
     const int t = threadIdx.x;
     const unsigned nsub = (unsigned)a.nsub, nchan = (unsigned)a.nchan;
     const size_t P = (size_t)nsub * nchan;
     const double sg = a.sign > 0 ? 1.0 : -1.0;
     const double inv = 1.0 / (double)M;
+    const __amdgpu_buffer_rsrc_t twr = rot_rsrc(a.tw, N);
+    // every global load of a profile in flight at once: one memory latency
+    // per profile, not one per row (or per flag / fit lookup)
+    auto load_rows = [&](size_t it, float4 (&xr)[NJ]) {
+        const unsigned c = (unsigned)(it / nsub), s = (unsigned)(it % nsub);
+        const float *x = a.in + ((size_t)s * nchan + c) * (size_t)a.ld_in;
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) {
+            const int j2 = t + u * TB;
+            if ((M / 2) % TB == 0 || j2 < M / 2) xr[u] = *(const float4 *)(x + 4 * j2);
+        }
+    };
+    float4 xnext[NJ];
+    if (IC_ROT_NEXTPF && blockIdx.x < P) load_rows(blockIdx.x, xnext);
     for (size_t item = blockIdx.x; item < P; item += gridDim.x) {
         const unsigned c = (unsigned)(item / nsub), s = (unsigned)(item % nsub);
-        if (a.flags && a.flags[s] == 0) continue;            // uniform over the block
         const size_t p = (size_t)s * nchan + c;
-        const float *x = a.in + p * (size_t)a.ld_in;
+        float4 xin[NJ];
+        if constexpr (IC_ROT_NEXTPF) {
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) xin[u] = xnext[u];
+            if (item + gridDim.x < P) load_rows(item + gridDim.x, xnext);   // lands during this profile
+        } else {
+            load_rows(item, xin);
+        }
+        if (a.flags && a.flags[s] == 0) continue;            // uniform over the block
         if (a.amp) {
             // the residual of the exact fit (k_residual's arithmetic), formed on the fly
             const int st = a.info[p];
             const bool ok = st >= 1 && st <= 4;
             const double am = a.amp[p];
-            for (int j2 = t; j2 < M / 2; j2 += TB) {   // 4 samples = 2 complex points per step
-                const float4 q = *(const float4 *)(x + 4 * j2);
+            const __amdgpu_buffer_rsrc_t t64r = rot_rsrc((const double2 *)a.T64, M);
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) {
+                const int j2 = t + u * TB;
+                if ((M / 2) % TB != 0 && j2 >= M / 2) break;
                 float r[4] = {0.0f, 0.0f, 0.0f, 0.0f};
                 if (ok) {
-                    const float pv[4] = {q.x, q.y, q.z, q.w};
+                    const float pv[4] = {xin[u].x, xin[u].y, xin[u].z, xin[u].w};
+                    const double2 ta = rot_ld(t64r, 32u * (unsigned)t, 32u * (unsigned)(u * TB));
+                    const double2 tb = rot_ld(t64r, 32u * (unsigned)t, 32u * (unsigned)(u * TB) + 16u);
+                    const double tv[4] = {ta.x, ta.y, tb.x, tb.y};
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int i = 4 * j2 + e;
-                        const double uu = am * a.T64[i];
+                        const double uu = am * tv[e];
                         double d = uu - (double)pv[e];
                         if (a.pr_on && i >= a.pr_start && i < a.pr_end) d = d * a.pr_factor;
                         r[e] = (float)d;
@@ -2553,41 +2682,68 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 4 : 2) void k_rotate(Rot
             }
         } else {
             const float b = a.base ? a.base[p] : 0.0f;
-            for (int j2 = t; j2 < M / 2; j2 += TB) {
-                const float4 q = *(const float4 *)(x + 4 * j2);
-                const float x0 = q.x - b, x1 = q.y - b, x2 = q.z - b, x3 = q.w - b;
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) {
+                const int j2 = t + u * TB;
+                if ((M / 2) % TB != 0 && j2 >= M / 2) break;
+                const float x0 = xin[u].x - b, x1 = xin[u].y - b, x2 = xin[u].z - b, x3 = xin[u].w - b;
                 v[rsw(2 * j2)] = make_double2((double)x0, (double)x1);
                 v[rsw(2 * j2 + 1)] = make_double2((double)x2, (double)x3);
             }
         }
         gsync<TB / 64>();
-        rot_fft<N>(v, a.tw, t);
-        const double2 *ph = a.ph + (size_t)c * (M + 1);
-        for (int k = t; k <= H; k += TB) {
-            if (k == 0) {
-                const double2 z = v[rsw(0)];
-                const double X0 = z.x + z.y, XM = z.x - z.y;
-                const double Y0 = X0 * ph[0].x, YM = XM * ph[M].x;
-                v[rsw(0)] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
-            } else {
-                const int q = M - k;
-                const double2 zk = v[rsw(k)], zq = v[rsw(q)];
-                const double2 wk = a.tw[k], wq = a.tw[q];
-                const double2 Xk = rot_post(zk, zq, wk), Xq = rot_post(zq, zk, wq);
-                const double2 pk = ph[k], pq = ph[q];
-                const double pki = sg * pk.y, pqi = sg * pq.y;
-                const double2 Yk = make_double2(Xk.x * pk.x - Xk.y * pki, Xk.x * pki + Xk.y * pk.x);
-                const double2 Yq = make_double2(Xq.x * pq.x - Xq.y * pqi, Xq.x * pqi + Xq.y * pq.x);
-                const double2 Zk = rot_pre(Yk, Yq, wk), Zq = rot_pre(Yq, Yk, wq);
-                v[rsw(q)] = make_double2(Zq.x, -Zq.y);
-                v[rsw(k)] = make_double2(Zk.x, -Zk.y);
+        rot_fft<N>(v, twr, t);
+        const __amdgpu_buffer_rsrc_t phr = rot_rsrc(a.ph + (size_t)c * (M + 1), M + 1);
+        // the post step's twiddles and phasors: pair u + 1's loads in flight
+        // while pair u computes (IC_ROT_POSTPF; else loaded at their use)
+        auto ld = [&](int u, double2 (&w4)[4]) {
+            const int k = t + u * TB;
+            if (k <= H) {
+                w4[0] = rot_ld(twr, 16u * (unsigned)(k & (M - 1)), 0);
+                w4[1] = rot_ld(twr, 16u * (unsigned)((M - k) & (M - 1)), 0);
+                w4[2] = rot_ld(phr, 16u * (unsigned)k, 0);
+                w4[3] = rot_ld(phr, 16u * (unsigned)(M - k), 0);
+            }
+        };
+        double2 cw[4], nw[4];
+        if (IC_ROT_POSTPF) ld(0, cw);
+#pragma unroll
+        for (int u = 0; u < NK; ++u) {
+            if (!IC_ROT_POSTPF) ld(u, cw);
+            else if (u + 1 < NK) ld(u + 1, nw);
+            const int k = t + u * TB;
+            if (k <= H) {
+                const double2 wk = cw[0], wq = cw[1], pk = cw[2], pq = cw[3];
+                if (k == 0) {
+                    const double2 z = v[rsw(0)];
+                    const double X0 = z.x + z.y, XM = z.x - z.y;
+                    const double Y0 = X0 * pk.x, YM = XM * pq.x;
+                    v[rsw(0)] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
+                } else {
+                    const int q = M - k;
+                    const double2 zk = v[rsw(k)], zq = v[rsw(q)];
+                    const double2 Xk = rot_post(zk, zq, wk), Xq = rot_post(zq, zk, wq);
+                    const double pki = sg * pk.y, pqi = sg * pq.y;
+                    const double2 Yk = make_double2(Xk.x * pk.x - Xk.y * pki, Xk.x * pki + Xk.y * pk.x);
+                    const double2 Yq = make_double2(Xq.x * pq.x - Xq.y * pqi, Xq.x * pqi + Xq.y * pq.x);
+                    const double2 Zk = rot_pre(Yk, Yq, wk), Zq = rot_pre(Yq, Yk, wq);
+                    v[rsw(q)] = make_double2(Zq.x, -Zq.y);
+                    v[rsw(k)] = make_double2(Zk.x, -Zk.y);
+                }
+            }
+            if (IC_ROT_POSTPF) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) cw[e] = nw[e];
             }
         }
         gsync<TB / 64>();
-        rot_fft<N>(v, a.tw, t);
+        rot_fft<N>(v, twr, t);
         float *o = a.out + p * (size_t)a.ldo;
         float *o2 = a.out2 ? a.out2 + p * (size_t)a.ldo2 : nullptr;
-        for (int j2 = t; j2 < M / 2; j2 += TB) {
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) {
+            const int j2 = t + u * TB;
+            if ((M / 2) % TB != 0 && j2 >= M / 2) break;
             const double2 r0 = v[rsw(2 * j2)], r1 = v[rsw(2 * j2 + 1)];
             const float4 y = make_float4((float)(r0.x * inv), (float)((-r0.y) * inv), (float)(r1.x * inv),
                                          (float)((-r1.y) * inv));
