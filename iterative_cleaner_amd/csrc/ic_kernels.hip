@@ -714,56 +714,73 @@ __device__ int lm_after_a2(LmState &L, double fnorm1)
 }
 
 // Exact fast path.  enorm: while every component is 0 or inside
-// (RDWARF, agiant) MINPACK's enorm reduces to sqrt(sum_seq a*a); that range is
-// verified per lane with integer compares on the high words of the SQUARES
-// a*a, which the sum needs anyway (no |a| masking): RN is monotone, so
-// hi(RN(a^2)) < hi(RN(agiant^2)) implies |a| < agiant and, for a != 0,
-// hi(RN(a^2)) > hi(RN(RDWARF^2)) implies |a| > RDWARF (conservatively: equal
-// high words count as out of range).  A nonzero a whose square underflowed to
-// 0 would slip through, so the A sweep takes this path only for
-// |x| in [2^-100, 2^100]: there every nonzero f = RN(RN(x t) - p) (t, p from
-// f32) is >= 2^-301 and every nonzero J >= 2^-427 in magnitude, |J| <= 2^355,
-// and all squares are normal.  Division: q = RN(a/b) from the
-// correctly rounded reciprocal y = RN(1/b) with two FMA corrections; after
-// the first, q1 is within one ulp, so the second (Markstein) correction is
-// exactly RN(a/b) barring over/underflow — which would push J out of the
-// verified enorm range and send the lane to the exact pass.
+// (RDWARF, agiant) MINPACK's enorm reduces to sqrt(sum_seq a*a).  The range is
+// verified per lane without per-sample work after the first 32 samples:
+//  * upper: the sequential sum of the nonnegative squares bounds every square
+//    (RN is monotone), so hi(RN(s2)) < hi(RN(agiant^2)) at the end implies
+//    |a| < agiant for every component (NaN/Inf fail the compare);
+//  * lower: over the first 32 samples (the peeled first tile pair) every
+//    nonzero square is checked, hi(RN(a^2)) > hi(RN(RDWARF^2)) implies
+//    |a| > RDWARF (equal high words count as out of range); after them the
+//    running sum must be >= 2^-40.  A later component with |a| <= RDWARF then
+//    adds RN(a^2) <= 2^-129 < ulp(s2)/2 to s2, a no-op, exactly as MINPACK
+//    leaves it out of s2; MINPACK's final factor 1 + (x3max/s2)(x3max s3) <=
+//    1 + n RDWARF^2 / 2^-40 rounds to 1 for any n < 2^50, and s2 >= x3max, so
+//    its result is sqrt(s2) as well.
+// A nonzero a whose square underflowed to 0 would slip through the first-tile
+// check, so the A sweep takes this path only for |x| in [2^-100, 2^100]:
+// there every nonzero f = RN(RN(x t) - p) (t, p from f32) is >= 2^-301 and
+// every nonzero J >= 2^-427 in magnitude, |J| <= 2^355, and all squares are
+// normal.  Division q = RN(a/b): y = RN(1/b) and ylo = RN((1 - b y) y) (1 - b y
+// is exact) approximate 1/b to 2^-105 relative, so q0 = RN(a y + RN(a ylo)) is
+// within 2^-104 |a/b| + ulp/2, i.e. faithful, and one Markstein correction
+// q = RN(q0 + RN(a - b q0) y) (the remainder exact) is RN(a/b), barring
+// over/underflow — which would push J out of the verified enorm range and send
+// the lane to the exact pass.
 struct FastAcc {
     double s2;
-    uint32_t maxhi, minhm1;
+    uint32_t minhm1;
 };
 
 __device__ __forceinline__ void fa_zero(FastAcc &a)
 {
     a.s2 = 0.0;
-    a.maxhi = 0u;
     a.minhm1 = 0xffffffffu;
 }
 
+template <bool CHK>
 __device__ __forceinline__ void fa_add(FastAcc &a, double v)
 {
     const double sq = v * v;   // == RN(|v| * |v|)
     a.s2 = a.s2 + sq;
-    const uint32_t hi = (uint32_t)((unsigned long long)__double_as_longlong(sq) >> 32);
-    a.maxhi = max(a.maxhi, hi);
-    a.minhm1 = min(a.minhm1, hi - 1u);   // zero -> 0xffffffff
+    if (CHK) {
+        const uint32_t hi = (uint32_t)((unsigned long long)__double_as_longlong(sq) >> 32);
+        a.minhm1 = min(a.minhm1, hi - 1u);   // zero -> 0xffffffff
+    }
 }
 
-__device__ __forceinline__ bool fa_ok(const FastAcc &a, uint32_t hr1, uint32_t hg)
+// after the checked samples: no nonzero square at or below RDWARF^2, and the
+// running sum large enough to absorb any later one
+__device__ __forceinline__ bool fa_lo_ok(const FastAcc &a, uint32_t hr1)
 {
-    const bool lo_ok = (a.minhm1 == 0xffffffffu) || (a.minhm1 + 1u >= hr1);
-    return lo_ok && (a.maxhi < hg);
+    return ((a.minhm1 == 0xffffffffu) || (a.minhm1 + 1u >= hr1)) && a.s2 >= 0x1p-40;
+}
+
+__device__ __forceinline__ bool fa_hi_ok(const FastAcc &a, uint32_t hg)
+{
+    return (uint32_t)((unsigned long long)__double_as_longlong(a.s2) >> 32) < hg;
 }
 
 __device__ __forceinline__ double fa_fin(const FastAcc &a) { return a.s2 != 0.0 ? sqrt(a.s2) : 0.0; }
 
-__device__ __forceinline__ double mdiv(double a, double b, double y)
+// low part of 1/b given y = RN(1/b)
+__device__ __forceinline__ double recip_lo(double b, double y) { return fma(-b, y, 1.0) * y; }
+
+__device__ __forceinline__ double mdiv(double a, double b, double y, double ylo)
 {
-    const double q0 = a * y;
+    const double q0 = fma(a, y, a * ylo);
     const double r0 = fma(-b, q0, a);
-    const double q1 = fma(r0, y, q0);
-    const double r1 = fma(-b, q1, a);
-    return fma(r1, y, q1);
+    return fma(r0, y, q0);
 }
 
 __device__ __forceinline__ bool x_in_fast_range(double x)
@@ -825,36 +842,49 @@ __device__ __forceinline__ void read_tile(const DmaTiles &d, fv4 (&v)[4])
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
 }
 
+// one pair of tiles (t, t + 1); CHK: the body runs its per-sample range checks
+template <bool CHK, typename Body>
+__device__ __forceinline__ void sweep_pair(const DmaTiles &d, int t, int nt, Body &body)
+{
+    fv4 v[4];
+    dma_tile(d, d.lds + FIT_BUF, (t + 1) * FIT_TB);
+    body.load_T(t * FIT_TB);   // scalar loads issued ahead of the waits
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    read_tile<0>(d, v);
+    body.template run<CHK>(t * FIT_TB, v);
+    body.fence();   // keep tile t's arithmetic ahead of the next wait
+    body.load_T((t + 1) * FIT_TB);
+    if (t + 2 < nt) {
+        dma_tile(d, d.lds, (t + 2) * FIT_TB);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    read_tile<FIT_BUF>(d, v);
+    body.template run<CHK>((t + 1) * FIT_TB, v);
+    body.fence();
+}
+
+// Body::kPeel: the first pair (32 samples) is peeled with the checks on, then
+// body.checked()
 template <typename Body>
 __device__ __forceinline__ void sweep_dma(const DmaTiles &d, int ldD, Body &body)
 {
-    const int nt = ldD / FIT_TB;   // even
+    const int nt = ldD / FIT_TB;   // even, >= 2
     dma_tile(d, d.lds, 0);
-    for (int t = 0; t < nt; t += 2) {
-        fv4 v[4];
-        dma_tile(d, d.lds + FIT_BUF, (t + 1) * FIT_TB);
-        body.load_T(t * FIT_TB);   // scalar loads issued ahead of the waits
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        read_tile<0>(d, v);
-        body(t * FIT_TB, v);
-        body.fence();   // keep tile t's arithmetic ahead of the next wait
-        body.load_T((t + 1) * FIT_TB);
-        if (t + 2 < nt) {
-            dma_tile(d, d.lds, (t + 2) * FIT_TB);
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        read_tile<FIT_BUF>(d, v);
-        body((t + 1) * FIT_TB, v);
-        body.fence();
+    int t = 0;
+    if constexpr (Body::kPeel) {
+        sweep_pair<true>(d, 0, nt, body);
+        body.checked();
+        t = 2;
     }
+    for (; t < nt; t += 2) sweep_pair<false>(d, t, nt, body);
 }
 
 struct PassIn {
     bool A, B;                   // lane takes part in pass A / B
-    double xa, xha, ha, yha;     // A: f(xa) and J(xa)
-    double xb, xhb, hb, yhb, ajb, yaj;  // B: sum Jn*f at xb
+    double xa, xha, ha, yha, yla;  // A: f(xa) and J(xa)
+    double xb, xhb, hb, yhb, ylb, ajb, yaj, ylj;  // B: sum Jn*f at xb
 };
 
 struct PassOut {
@@ -868,45 +898,29 @@ struct PassOut {
 // no-ops: f = J = 0 adds nothing to either norm, and Jn*f = 0 to the dot.
 template <bool DA, bool DB>
 struct FastBody {
+    static constexpr bool kPeel = true;
     const PassIn &in;
     const double *__restrict__ T64;
     FastAcc fF, fJ;
     double fa0, Ja0, sum;
+    int lo_ok;
 
     __device__ __forceinline__ FastBody(const PassIn &i, const double *T) : in(i), T64(T)
     {
         fa_zero(fF);
         fa_zero(fJ);
         fa0 = Ja0 = sum = 0.0;
+        lo_ok = 1;
     }
 
-    __device__ __forceinline__ void sample(double t, double pv, bool first)
+    // the flag is materialised here (empty asm): otherwise the compiler sinks
+    // the per-sample minima below the sweep loop and keeps the squares live
+    __device__ __forceinline__ void checked()
     {
         if (DA) {
-            const double u = in.xa * t;
-            const double f = u - pv;
-            const double uh = in.xha * t;
-            const double wa = uh - pv;
-            const double d = wa - f;
-            fa_add(fF, f);
-            const double J = mdiv(d, in.ha, in.yha);
-            fa_add(fJ, J);
-            if (first) {
-                fa0 = f;
-                Ja0 = J;
-            }
-        }
-        if (DB) {
-            const double u = in.xb * t;
-            const double f = u - pv;
-            const double uh = in.xhb * t;
-            const double wa = uh - pv;
-            const double d = wa - f;
-            const double J = mdiv(d, in.hb, in.yhb);
-            double Jn = mdiv(J, in.ajb, in.yaj);
-            if (first) Jn = Jn + 1.0;
-            const double pr = Jn * f;
-            sum = sum + pr;
+            const uint32_t hr1 = (uint32_t)((unsigned long long)__double_as_longlong(kRdwarf * kRdwarf) >> 32) + 1u;
+            lo_ok = (fa_lo_ok(fF, hr1) && fa_lo_ok(fJ, hr1)) ? 1 : 0;
+            asm volatile("" : "+v"(lo_ok));
         }
     }
 
@@ -914,8 +928,7 @@ struct FastBody {
     // arithmetic below the following s_waitcnt (asm statements keep their order)
     __device__ __forceinline__ void fence()
     {
-        asm volatile("" : "+v"(fF.s2), "+v"(fF.maxhi), "+v"(fF.minhm1), "+v"(fJ.s2), "+v"(fJ.maxhi),
-                     "+v"(fJ.minhm1), "+v"(sum));
+        asm volatile("" : "+v"(fF.s2), "+v"(fJ.s2), "+v"(sum), "+v"(fF.minhm1), "+v"(fJ.minhm1));
     }
 
     double tv[FIT_TB];   // the tile's template values (wave-uniform: SGPRs)
@@ -926,9 +939,12 @@ struct FastBody {
     }
 
     // Four samples at a time, stage by stage: the four dependent chains (the
-    // products, the differences, the five-step division) are interleaved so
+    // products, the differences, the four-step divisions) are interleaved so
     // that every f64 op has independent neighbours to hide its latency behind;
-    // the accumulations still run in sample order.  Same IEEE ops as sample().
+    // the accumulations still run in sample order.  Per sample: A = f(x),
+    // f(x + h), J = RN((f(x + h) - f(x))/h), f^2 and J^2 summed; B = the same f
+    // and J, Jn = RN(J/ajnorm) (+1 on sample 0), sum += Jn f.
+    template <bool CHK>
     __device__ __forceinline__ void group4(const double (&t)[4], const fv4 &pv4, bool first)
     {
         const float pf[4] = {pv4.x, pv4.y, pv4.z, pv4.w};
@@ -947,21 +963,19 @@ struct FastBody {
             for (int k = 0; k < 4; ++k) d[k] = d[k] - p[k];
 #pragma unroll
             for (int k = 0; k < 4; ++k) d[k] = d[k] - f[k];
-            // J = mdiv(d, ha, yha), stage-interleaved
+            // J = mdiv(d, ha, yha, yla), stage-interleaved
 #pragma unroll
-            for (int k = 0; k < 4; ++k) q[k] = d[k] * in.yha;
+            for (int k = 0; k < 4; ++k) q[k] = d[k] * in.yla;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) r[k] = fma(-in.ha, q[k], d[k]);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yha, q[k]);
+            for (int k = 0; k < 4; ++k) q[k] = fma(d[k], in.yha, q[k]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) r[k] = fma(-in.ha, q[k], d[k]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yha, q[k]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                fa_add(fF, f[k]);
-                fa_add(fJ, q[k]);
+                fa_add<CHK>(fF, f[k]);
+                fa_add<CHK>(fJ, q[k]);
             }
             if (first) {
                 fa0 = f[0];
@@ -980,24 +994,20 @@ struct FastBody {
             for (int k = 0; k < 4; ++k) d[k] = d[k] - p[k];
 #pragma unroll
             for (int k = 0; k < 4; ++k) d[k] = d[k] - f[k];
-            // J = mdiv(d, hb, yhb)
+            // J = mdiv(d, hb, yhb, ylb)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) q[k] = d[k] * in.yhb;
+            for (int k = 0; k < 4; ++k) q[k] = d[k] * in.ylb;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) r[k] = fma(-in.hb, q[k], d[k]);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yhb, q[k]);
+            for (int k = 0; k < 4; ++k) q[k] = fma(d[k], in.yhb, q[k]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) r[k] = fma(-in.hb, q[k], d[k]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yhb, q[k]);
-            // Jn = mdiv(J, ajb, yaj)
+            // Jn = mdiv(J, ajb, yaj, ylj)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) d[k] = q[k] * in.yaj;
+            for (int k = 0; k < 4; ++k) d[k] = q[k] * in.ylj;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) r[k] = fma(-in.ajb, d[k], q[k]);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) d[k] = fma(r[k], in.yaj, d[k]);
+            for (int k = 0; k < 4; ++k) d[k] = fma(q[k], in.yaj, d[k]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) r[k] = fma(-in.ajb, d[k], q[k]);
 #pragma unroll
@@ -1010,18 +1020,20 @@ struct FastBody {
         }
     }
 
-    __device__ __forceinline__ void operator()(int b0, const fv4 (&v)[4])
+    template <bool CHK>
+    __device__ __forceinline__ void run(int b0, const fv4 (&v)[4])
     {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const double t4[4] = {tv[4 * c], tv[4 * c + 1], tv[4 * c + 2], tv[4 * c + 3]};
-            group4(t4, v[c], c == 0 && b0 == 0);
+            group4<CHK>(t4, v[c], CHK && c == 0 && b0 == 0);
         }
     }
 };
 
 // Exact sweep body: MINPACK's branchy enorm and true divisions, per lane.
 struct ExactBody {
+    static constexpr bool kPeel = false;
     const PassIn &in;
     const double *__restrict__ T64;
     double agiant;
@@ -1067,8 +1079,8 @@ struct ExactBody {
 
     __device__ __forceinline__ void fence() {}
     __device__ __forceinline__ void load_T(int) {}
-
-    __device__ void operator()(int b0, const fv4 (&v)[4])
+    template <bool CHK>
+    __device__ void run(int b0, const fv4 (&v)[4])
     {
         for (int c = 0; c < 4; ++c) {
             const int i = b0 + 4 * c;
@@ -1086,14 +1098,13 @@ __device__ __forceinline__ void fast_sweep(const DmaTiles &d, int ldD, const Pas
 {
     FastBody<DA, DB> body(in, T64);
     sweep_dma(d, ldD, body);
-    const uint32_t hr1 = (uint32_t)((unsigned long long)__double_as_longlong(kRdwarf * kRdwarf) >> 32) + 1u;
     const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant * agiant) >> 32);
     out.f0 = body.fa0;
     out.J0 = body.Ja0;
     out.sum = body.sum;
     out.fnorm = fa_fin(body.fF);
     out.acnorm = fa_fin(body.fJ);
-    out.bad = DA && in.A && !(fa_ok(body.fF, hr1, hg) && fa_ok(body.fJ, hr1, hg));
+    out.bad = DA && in.A && !(body.lo_ok && fa_hi_ok(body.fF, hg) && fa_hi_ok(body.fJ, hg));
 }
 
 // ---- split lmdif: state machine (k_fit_state) <-> data sweeps (k_fit_pass) ----
@@ -1173,13 +1184,16 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     if (in.ha == 0.0) in.ha = eps;
     in.xha = in.xa + in.ha;
     in.yha = 1.0 / in.ha;
+    in.yla = recip_lo(in.ha, in.yha);
     in.xb = reqB ? S.x[k] : 1.0;
     in.hb = eps * fabs(in.xb);
     if (in.hb == 0.0) in.hb = eps;
     in.xhb = in.xb + in.hb;
     in.yhb = 1.0 / in.hb;
+    in.ylb = recip_lo(in.hb, in.yhb);
     in.ajb = reqB ? S.aj[k] : 1.0;
     in.yaj = 1.0 / in.ajb;
+    in.ylj = recip_lo(in.ajb, in.yaj);
     const bool slow = reqB && S.slow[k];
     const bool fastA = reqA && x_in_sq_range(in.xa);
     const bool fastB = reqB && !slow && x_in_fast_range(in.xb) && x_in_fast_range(in.ajb);
