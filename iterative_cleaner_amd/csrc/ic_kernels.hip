@@ -2378,35 +2378,42 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             // rFFT of f64(X) - mean: N/2-point complex Stockham, in place
             p2_fft<C::M, TPP, C::LG, 0, 1, C::M, XT>(Cb, X, mean, tw, t);
             // X_k = E_k + w^k O_k, computed as 2 X_k (the 1/2 factors are exact
-            // powers of two, applied once to the maximum)
-            // k = 0 .. M-1 on all threads; the Nyquist term k = M (w = -1, Z_M = Z_0)
-            // reduces to (Re 2Z_0 - Im 2Z_0)^2 and is added by thread 0 from k = 0
-            double best2 = 0.0;
-            int nanf = 0;
-#pragma unroll 2
-            for (int j = 0; j < (C::M + TPP - 1) / TPP; ++j) {
-                const int kk = t + TPP * j;
-                if (C::M % TPP != 0 && kk >= C::M) continue;   // M = 32 (N = 64)
-                // kk = t + TPP j, M - kk = (TPP - t) + (M - TPP (j + 1)): 64-multiples apart
-                constexpr bool F = TPP % 64 == 0 && C::M % 64 == 0;
-                const double2 zk = F ? Cb[cidx(t) + TPP * j] : Cb[cidx(kk)];
-                const double2 zm = F ? Cb[kk == 0 ? 0 : cidx(TPP - t) + (C::M - TPP * (j + 1))]
-                                     : Cb[cidx(kk == 0 ? 0 : C::M - kk)];
+            // powers of two, applied once to the maximum).  Bins pair up: with
+            // E_k, O_k from Z_k and Z_(M-k), E_(M-k) = conj E_k, O_(M-k) = conj O_k
+            // and w^(M-k) = -conj w^k, so X_(M-k) = conj(E_k - w^k O_k): one
+            // product t = w^k O_k serves X_k = E + t and X_(M-k).  Pairs k = 0 ..
+            // M/2 cover every bin: k = 0 gives DC (E + O) and Nyquist (E - O), k = M/2
+            // pairs with itself.  NaN: the a2 are >= 0 or NaN, so their sum is NaN
+            // iff one of them is.
+            constexpr int H = C::M / 2;
+            constexpr int JF = H / TPP;   // pair tasks every thread holds
+            double best2 = 0.0, nsum = 0.0;
+            auto post = [&](const double2 zk, const double2 zm, const double2 wv) {
                 const double er = zk.x + zm.x, ei = zk.y - zm.y;
                 const double orr = zk.y + zm.y, oi = zm.x - zk.x;
-                const double2 wv = tw[kk];
-                const double re = er + __builtin_fma(orr, wv.x, -(oi * wv.y));
-                const double im = ei + __builtin_fma(orr, wv.y, oi * wv.x);
+                const double tr = __builtin_fma(orr, wv.x, -(oi * wv.y));
+                const double ti = __builtin_fma(orr, wv.y, oi * wv.x);
+                const double re = er + tr, im = ei + ti;
+                const double rm = er - tr, imm = ti - ei;
                 const double a2 = __builtin_fma(re, re, im * im);
-                nanf |= isnan(a2);
-                best2 = fmax(best2, a2);
-                if (j == 0 && t == 0) {
-                    const double rn = er - orr;
-                    const double an = rn * rn;
-                    nanf |= isnan(an);
-                    best2 = fmax(best2, an);
-                }
+                const double b2 = __builtin_fma(rm, rm, imm * imm);
+                nsum = nsum + a2;
+                nsum = nsum + b2;
+                best2 = fmax(best2, fmax(a2, b2));
+            };
+#pragma unroll
+            for (int j = 0; j < JF; ++j) {
+                // kk = t + TPP j, M - kk = (TPP - t) + (M - TPP (j + 1)): 64-multiples apart
+                const int kk = t + TPP * j;
+                const double2 zk = Cb[cidx(t) + TPP * j];
+                const double2 zm = Cb[kk == 0 ? 0 : cidx(TPP - t) + (C::M - TPP * (j + 1))];
+                post(zk, zm, tw[kk]);
             }
+            {
+                const int kk = t + TPP * JF;   // the rest: kk <= M/2 (one thread at N >= 256)
+                if (kk <= H) post(Cb[cidx(kk)], Cb[cidx(kk == 0 ? 0 : C::M - kk)], tw[kk]);
+            }
+            int nanf = isnan(nsum);
             best2 = group_tree<WPP, 64>(best2, OpMaxF(), red + 44, wave, lane);
             nanf = group_tree<WPP, 64>(nanf, OpOr(), (int *)(red + 48), wave, lane);
             fftv = nanf ? NAN : 0.5 * sqrt(best2);
