@@ -9,6 +9,10 @@ namespace icgpu {
 constexpr int kSuperBlock = 256;    // canonical channel super-block (archive.py SUPER_BLOCK)
 constexpr int kMaxLeaves = 256;     // pairwise-sum leaves (nbin <= 32768)
 constexpr int kFitTile = 32;        // bins per k_fit_pass LDS tile (fit cube row padding)
+#ifndef IC_FIT_PAD_DEFAULT
+#define IC_FIT_PAD_DEFAULT 0
+#endif
+constexpr int kFitPad = IC_FIT_PAD_DEFAULT;   // extra bins per fit-cube row when ldD % 1024 == 0
 
 // Canonical combine of super-block partials (archive.py sb_tree): the halving
 // tree over n leaves, evaluated as a post-order stack program: push leaf j,

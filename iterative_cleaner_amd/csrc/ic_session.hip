@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -727,6 +728,14 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     s->rows_own = rr[2 * rank + 1] - rr[2 * rank];
     s->rows_pad = (p.nsub + world - 1) / world;
     s->ldD = ((p.nbin + kFitTile - 1) / kFitTile) * kFitTile;
+    // row stride of the fit cube: off a multiple of 4 KiB (a fit sweep reads
+    // one 64-B piece of 64 consecutive rows at a time; at a 4-KiB stride those
+    // land on the same HBM channels).  IC_FIT_PAD: bins of padding (A/B knob).
+    {
+        const char *e = getenv("IC_FIT_PAD");
+        const int pad = e ? atoi(e) : kFitPad;
+        if (pad > 0 && pad % 4 == 0 && (s->ldD % 1024) == 0) s->ldD += pad;
+    }
     s->Ppad = ((s->P + 63) / 64) * 64;
     s->width = (int)(p.baseline_duty * (double)p.nbin);
     if (s->width < 1) s->width = 1;
