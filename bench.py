@@ -530,11 +530,25 @@ def main():
             v = valu.get(dom)
             if v:
                 g = v["valu_insts_per_launch"] / avg_s / 1e9
-                # the dominant kernel is f64-VALU-bound: that is its roof
-                roof.update({"bound": "valu", "achieved": round(g, 1), "peak": VALU_PEAK_G,
-                             "unit": "G wave64 VALU inst/s", "frac": round(g / VALU_PEAK_G, 4),
-                             "insts_per_launch": v["valu_insts_per_launch"],
-                             "f64_share": v["f64_share_of_valu"], "valu_source": vsrc})
+                roof["valu"] = {"achieved": round(g, 1), "peak": VALU_PEAK_G, "unit": "G wave64 VALU inst/s",
+                                "frac": round(g / VALU_PEAK_G, 4), "insts_per_launch": v["valu_insts_per_launch"],
+                                "f64_share": v["f64_share_of_valu"], "source": vsrc}
+        if traffic:
+            # measured HBM bytes (PMC) per launch over the launch time: what the
+            # kernel actually moves, re-sweeps and refetches included
+            tg = traffic / avg_s / 1e9
+            roof["traffic_gbs"] = round(tg, 1)
+            roof["traffic_frac"] = round(tg / HBM_PEAK_GBS, 4)
+        # the roof that binds is the larger measured fraction: PMC traffic
+        # against HBM peak, or VALU issue against its peak
+        vf = roof.get("valu", {}).get("frac")
+        if vf is not None and vf > roof.get("traffic_frac", 0.0):
+            roof["bound"] = "valu"
+            roof["bound_note"] = "VALU issue (%.2f of peak) exceeds measured HBM traffic (%s of peak)" % (
+                vf, roof.get("traffic_frac"))
+        elif "traffic_frac" in roof:
+            roof["bound_note"] = ("measured HBM traffic %.2f of peak (re-sweeps included); frac/achieved use "
+                                  "SURVEY §8(d) algorithmic bytes" % roof["traffic_frac"])
         roof["per_kernel"] = per_kernel
         iter_bytes = 8 * per_rank_P * nbin + 64 * per_rank_P    # SURVEY §8(d) B_iter, one GPU's share
         loop_gbs = iter_bytes * n_iter / (elapsed / a.steps) / 1e9
