@@ -188,6 +188,10 @@ typedef struct {
 int ic_get_kernel_times(void *session, ic_kernel_time *out, int n);
 const char *ic_kernel_name(int kernel);
 int ic_set_timing(void *session, int enabled);
+/* Restrict the timing to one kernel id (ic_kernel_name ids; -1 = every kernel,
+ * the default): two HIP events per launch cost ~5 us, so a timed region that
+ * must stay representative times only the kernel it prices. */
+int ic_set_timing_kernel(void *session, int kernel);
 
 /* Statistics of the last ic_run (measurement; see DESIGN.md roofline). */
 typedef struct {

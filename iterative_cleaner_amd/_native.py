@@ -23,7 +23,8 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_shard_layout", "ic_session_create_shard", "ic_group_create", "ic_group_destroy",
            "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free",
            "ic_upload_pols", "ic_comprehensive_stats", "ic_get_bad_fits",
-           "ic_fit_profiles", "ic_get_diagnostics_f64", "ic_set_delays", "ic_rotate_profiles")
+           "ic_fit_profiles", "ic_get_diagnostics_f64", "ic_set_delays", "ic_rotate_profiles",
+           "ic_set_timing_kernel")
 
 FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)
 FIT_CLOSED = 1   # IC_FIT_CLOSED: closed-form amplitude fused with the diagnostics (fast mode)
@@ -121,6 +122,7 @@ def load_library(path: str = LIB_PATH):
     lib.ic_get_diagnostics_f64.argtypes = [vp, vp, vp, vp, vp]
     lib.ic_get_kernel_times.argtypes = [vp, C.POINTER(KernelTime), C.c_int]
     lib.ic_set_timing.argtypes = [vp, C.c_int]
+    lib.ic_set_timing_kernel.argtypes = [vp, C.c_int]
     lib.ic_get_run_stats.argtypes = [vp, C.POINTER(RunStats)]
     lib.ic_set_fit_tail.argtypes = [vp, C.c_int64]
     lib.ic_upload_async.argtypes = [vp, vp, vp, vp]
@@ -317,7 +319,16 @@ class GpuSession:
                         "ic_get_diagnostics")
         return sd, mn, pt, ff
 
-    def set_timing(self, on: bool):
+    def set_timing(self, on: bool, only: str | None = None):
+        """Per-kernel HIP-event timing of the following runs; `only`: one kernel
+        name (the others run without events)."""
+        kid = -1
+        if only is not None:
+            names = [self.lib.ic_kernel_name(q).decode() for q in range(64)]
+            if only not in names:
+                raise ValueError("unknown kernel %r" % only)
+            kid = names.index(only)
+        self._check(self.lib.ic_set_timing_kernel(self.h, kid), "ic_set_timing_kernel")
         self._check(self.lib.ic_set_timing(self.h, 1 if on else 0), "ic_set_timing")
 
     def set_fit_tail(self, threshold: int):

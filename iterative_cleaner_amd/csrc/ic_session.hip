@@ -129,7 +129,10 @@ struct Session {
     double2 *ph = nullptr;
     // timing
     bool timing = false;
+    int timing_only = -1;            // >= 0: time only this kernel id
     std::vector<Timed> events;
+    std::vector<hipEvent_t> epool;   // reused across runs: no hipEventCreate in the timed region
+    size_t enext = 0;
     double kms[K_COUNT] = {0};
     int klaunch[K_COUNT] = {0};
 };
@@ -180,16 +183,31 @@ int make_plan(int n, PwPlan *pl)
     return 0;
 }
 
+// timing events come from a per-session pool (created on first use, reused
+// once collect_timing has read them)
+static hipError_t take_event(Session *s, hipEvent_t *e)
+{
+    if (s->enext == s->epool.size()) {
+        hipEvent_t n = nullptr;
+        const hipError_t rc = hipEventCreate(&n);
+        if (rc != hipSuccess) return rc;
+        s->epool.push_back(n);
+    }
+    *e = s->epool[s->enext++];
+    return hipSuccess;
+}
+
 #define LAUNCH(S, KID, CALL)                                                   \
     do {                                                                       \
         Timed t_{KID, nullptr, nullptr};                                       \
-        if ((S)->timing) {                                                     \
-            CK(hipEventCreate(&t_.a));                                         \
-            CK(hipEventCreate(&t_.b));                                         \
+        const bool tm_ = (S)->timing && ((S)->timing_only < 0 || (S)->timing_only == (KID)); \
+        if (tm_) {                                                             \
+            CK(take_event((S), &t_.a));                                        \
+            CK(take_event((S), &t_.b));                                        \
             CK(hipEventRecord(t_.a, (S)->stream));                             \
         }                                                                      \
         CK(CALL);                                                              \
-        if ((S)->timing) {                                                     \
+        if (tm_) {                                                             \
             CK(hipEventRecord(t_.b, (S)->stream));                             \
             (S)->events.push_back(t_);                                         \
         }                                                                      \
@@ -233,10 +251,9 @@ int collect_timing(Session *s)
         CK(hipEventElapsedTime(&ms, e.a, e.b));
         s->kms[e.kid] += ms;
         s->klaunch[e.kid] += 1;
-        (void)hipEventDestroy(e.a);
-        (void)hipEventDestroy(e.b);
     }
     s->events.clear();
+    s->enext = 0;
     return 0;
 }
 
@@ -271,10 +288,9 @@ void free_all(Session *s)
     if (s->h_rcount) (void)hipHostFree(s->h_rcount);
     for (auto &e : s->rev)
         if (e) (void)hipEventDestroy(e);
-    for (auto &e : s->events) {
-        (void)hipEventDestroy(e.a);
-        (void)hipEventDestroy(e.b);
-    }
+    for (auto &e : s->epool) (void)hipEventDestroy(e);
+    s->epool.clear();
+    s->events.clear();
     if (s->stream) (void)hipStreamDestroy(s->stream);
 }
 
@@ -292,13 +308,14 @@ __global__ void k_valid(const float *w0, uint8_t *valid, float *W, float *hist0,
 #define CM(S, call, what)                                                                         \
     do {                                                                                          \
         Timed t_{K_EXCHANGE, nullptr, nullptr};                                                   \
-        if ((S)->timing) {                                                                        \
-            CK(hipEventCreate(&t_.a));                                                            \
-            CK(hipEventCreate(&t_.b));                                                            \
+        const bool tm_ = (S)->timing && ((S)->timing_only < 0 || (S)->timing_only == K_EXCHANGE); \
+        if (tm_) {                                                                                \
+            CK(take_event((S), &t_.a));                                                           \
+            CK(take_event((S), &t_.b));                                                           \
             CK(hipEventRecord(t_.a, (S)->stream));                                                \
         }                                                                                         \
         const int rc_ = (call);                                                                   \
-        if ((S)->timing) {                                                                        \
+        if (tm_) {                                                                                \
             CK(hipEventRecord(t_.b, (S)->stream));                                                \
             (S)->events.push_back(t_);                                                            \
         }                                                                                         \
@@ -1072,6 +1089,15 @@ int ic_host_alloc(size_t bytes, void **ptr)
 void ic_host_free(void *ptr)
 {
     if (ptr) (void)hipHostFree(ptr);
+}
+
+int ic_set_timing_kernel(void *session, int kernel)
+{
+    Session *s = (Session *)session;
+    if (!s) return fail(IC_EINVAL, "null session");
+    if (kernel >= K_COUNT) return fail(IC_EINVAL, "kernel id %d >= %d", kernel, (int)K_COUNT);
+    s->timing_only = kernel < 0 ? -1 : kernel;
+    return IC_OK;
 }
 
 int ic_set_timing(void *session, int enabled)
