@@ -14,6 +14,21 @@ constexpr int kFitTile = 32;        // bins per k_fit_pass LDS tile (fit cube ro
 #endif
 constexpr int kFitPad = IC_FIT_PAD_DEFAULT;   // extra bins per fit-cube row when ldD % 1024 == 0
 
+// Tiled fit cube (dtiled): profiles in groups of 64 (one k_fit_pass wave),
+// each group stored as ldD/32 tiles of [64 profiles][32 bins] (8 KiB), so a
+// wave's 32-bin step of its 64 rows is one contiguous 8-KiB block instead of
+// 64 lines 4 KiB apart.  Element (k, i) of a cube with row length ldD
+// (a multiple of 32, profiles padded to a multiple of 64):
+__host__ __device__ inline size_t dt_ofs(size_t k, int i, int ldD)
+{
+    return (((k >> 6) * (size_t)(ldD >> 5) + (size_t)(i >> 5)) << 11) + ((k & 63) << 5) + (size_t)(i & 31);
+}
+// element (k, i) of the fit cube in either layout
+__host__ __device__ inline size_t d_ofs(size_t k, int i, int ldD, int dtiled)
+{
+    return dtiled ? dt_ofs(k, i, ldD) : k * (size_t)ldD + (size_t)i;
+}
+
 // Canonical combine of super-block partials (archive.py sb_tree): the halving
 // tree over n leaves, evaluated as a post-order stack program: push leaf j,
 // then merge the two top entries merges[j] times.  n <= kMaxSbLeaves (nchan <=
@@ -96,7 +111,8 @@ struct LineStatsArgs {
 // flags: only subints with flags[s] != 0 (nullptr: all)
 hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, const float *W, const int32_t *shift,
                                 const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
-                                double *part, double *part2, double *wpart, float *D = nullptr, int ldD = 0);
+                                double *part, double *part2, double *wpart, float *D = nullptr, int ldD = 0,
+                                int dtiled = 0);
 // flags != nullptr: flags[s] = window of subint s moved (win updated in place)
 // element (s, leaf, i) of `part` is part[s*ss + leaf*sl + i]; the leaves are
 // combined with `plan` (single device: the nsb super-blocks; sharded: the
@@ -142,7 +158,8 @@ hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
 // list == nullptr: all P profiles; else list[0 .. *nlist) with *nlist <= bound
 // (the host sizes grids from a count it already knows: counts only shrink).
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S);
+                           int dtiled, const int32_t *list, const int32_t *nlist, long bound,
+                           const FitStateArrays &S);
 // ctr: zeroed device counter, finished blocks << 32 | survivors (its low word,
 // little-endian, is the next round's list length); host_n: host-mapped int the
 // last block writes the final count to
@@ -150,7 +167,7 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
                             const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
                             unsigned long long *ctr, int32_t *host_n);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
+                           int dtiled, const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
                            double *amp, int32_t *info, unsigned long long *sweeps);
 // Diagnostics kernels (k_diag_p2<N> for power-of-two nbin 64..4096, k_diag
 // otherwise).  mode: DIAG_EXACT = residual from the exact fit's amp/info and
@@ -180,6 +197,7 @@ struct DiagArgs {
     int pr_start, pr_end;
     double *std_o, *mean_o, *fft_o, *ptp_o;
     int data_f64;      // psrchive get_data returns f64: X = f64(R) * f64(w), f64 mean and ptp
+    int dtiled;        // D is the tiled fit cube (dt_ofs); DIAG_STATS inputs are row-major
 };
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a);
 // dynamic LDS the generic k_diag needs for one wave (0 for the power-of-two kernels)
@@ -232,6 +250,7 @@ bool rotate_supported(int nbin);
 // D == nullptr: fit-cube rows formed from raw and base (fit_mode 1)
 hipError_t launch_residual(hipStream_t st, const float *D, const float *raw, const float *base, const double *T64,
                            const double *amp, const int32_t *info, const int32_t *shift, int nsub, int nchan,
-                           int nbin, int ldD, int pr_on, double pr_factor, int pr_start, int pr_end, float *R);
+                           int nbin, int ldD, int dtiled, int pr_on, double pr_factor, int pr_start, int pr_end,
+                           float *R);
 
 }  // namespace icgpu

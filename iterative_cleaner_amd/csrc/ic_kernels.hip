@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void k_chan_partials(
     const float *__restrict__ raw, const float *__restrict__ W, const int32_t *__restrict__ shift,
     const float *__restrict__ base, const int32_t *__restrict__ flags, int nsub, int nchan, int nbin, int nsb,
     double *__restrict__ part, double *__restrict__ part2, double *__restrict__ wpart, float *__restrict__ D,
-    int ldD)
+    int ldD, int dtiled)
 {
     constexpr bool A = MODE == 0 || MODE == 2, F = MODE != 0, WD = MODE == 3;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void k_chan_partials(
                 const float d = xv[q] - bv[q];
                 if (A) acc = acc + w * (double)xv[q];
                 if (F) acc2 = acc2 + w * (double)d;
-                if (WD) D[(krow + c + q) * (size_t)ldD + i] = d;
+                if (WD) D[d_ofs(krow + c + q, i, ldD, dtiled)] = d;
             }
         }
         for (; c < c1; ++c) {
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void k_chan_partials(
             const float d = F ? x - base[k] : 0.0f;
             if (A) acc = acc + w * (double)x;
             if (F) acc2 = acc2 + w * (double)d;
-            if (WD) D[k * (size_t)ldD + i] = d;
+            if (WD) D[d_ofs(k, i, ldD, dtiled)] = d;
         }
         if (A) part[((size_t)s * nsb + sb) * nbin + i] = acc;
         if (F) part2[((size_t)s * nsb + sb) * nbin + i] = acc2;
@@ -817,6 +817,7 @@ typedef float fv4 __attribute__((ext_vector_type(4)));
 
 struct DmaTiles {
     const float *src[4];   // this lane's DMA source for instruction m at bin 0
+    int tiled;             // fit cube layout (dt_ofs): bin b0 of a row is at + (b0/32) 2048 + b0 % 32
     uint32_t rd[4];        // LDS byte address of this lane's chunk c in buffer 0
     char *lds;             // buffer 0 (buffer 1 at +FIT_BUF)
 };
@@ -828,9 +829,10 @@ __device__ __forceinline__ uint32_t lds_u32(const void *p)
 
 __device__ __forceinline__ void dma_tile(const DmaTiles &d, char *buf, int b0)
 {
+    const int off = d.tiled ? ((b0 >> 5) << 11) + (b0 & 31) : b0;
 #pragma unroll
     for (int m = 0; m < 4; ++m)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(d.src[m] + b0),
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(d.src[m] + off),
                                          (__attribute__((address_space(3))) void *)(buf + m * 1024), 16, 0, 0);
 }
 
@@ -1155,7 +1157,7 @@ __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
 // list == nullptr: profiles [0, P) in order (first round); else list[0..nlist).
 // One wave per block (the LDS buffers are private to the wave: no barriers).
 __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, const double *__restrict__ T64,
-                                                 long P, int nbin, int ldD, int nsw,
+                                                 long P, int nbin, int ldD, int nsw, int dtiled,
                                                  const int32_t *__restrict__ list,
                                                  const int32_t *__restrict__ nlist, FitStateArrays S)
 {
@@ -1172,6 +1174,7 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     if (!__any(reqA || reqB)) return;
     DmaTiles dt;
     dt.lds = lbuf;
+    dt.tiled = dtiled;
     {
         const int c = (lane & 3) ^ ((lane >> 4) & 3);
 #pragma unroll
@@ -1182,7 +1185,7 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 #if IC_FIT_ROWPROBE   // A/B probe only: every wave sweeps rows 0..63 (L2-resident data, VALU-only time)
             kr = m * 16 + (lane >> 2);
 #endif
-            dt.src[m] = D + (size_t)kr * ldD + 4 * c;
+            dt.src[m] = D + d_ofs(kr, 4 * c, ldD, dtiled);
         }
         const uint32_t base = lds_u32(lbuf) + 16u * (uint32_t)(64 * (lane >> 4) + 4 * (lane & 15));
         const int g = (lane >> 2) & 3;
@@ -1399,7 +1402,15 @@ __device__ __forceinline__ void seq_sums(const double *a, const double *b, int n
     }
 }
 
-__device__ __forceinline__ void tail_sweep_a(const float *__restrict__ p, const double *__restrict__ T64, int nbin,
+// one fit-cube row in either layout (d_ofs)
+struct RowRef {
+    const float *D;
+    size_t k;
+    int ldD, tiled;
+    __device__ __forceinline__ float operator[](int i) const { return D[d_ofs(k, i, ldD, tiled)]; }
+};
+
+__device__ __forceinline__ void tail_sweep_a(const RowRef &p, const double *__restrict__ T64, int nbin,
                                              double xa, double agiant, double (*buf)[TAIL_CH], int lane,
                                              double &fnorm, double &acnorm, double &f0, double &J0)
 {
@@ -1464,7 +1475,7 @@ __device__ __forceinline__ void tail_sweep_a(const float *__restrict__ p, const 
     acnorm = en_fin(eJ);
 }
 
-__device__ __forceinline__ double tail_sweep_b(const float *__restrict__ p, const double *__restrict__ T64, int nbin,
+__device__ __forceinline__ double tail_sweep_b(const RowRef &p, const double *__restrict__ T64, int nbin,
                                                double x, double aj, double (*buf)[TAIL_CH], int lane)
 {
     const double eps = sqrt(DBL_EPSILON);
@@ -1497,7 +1508,7 @@ __device__ __forceinline__ double tail_sweep_b(const float *__restrict__ p, cons
 
 __global__ __launch_bounds__(64 * TAIL_WAVES) void k_fit_tail(const float *__restrict__ D,
                                                               const double *__restrict__ T64, long P, int nbin,
-                                                              int ldD, const int32_t *__restrict__ list,
+                                                              int ldD, int dtiled, const int32_t *__restrict__ list,
                                                               const int32_t *__restrict__ nlist, FitStateArrays S,
                                                               double *__restrict__ amp_o,
                                                               int32_t *__restrict__ info_o,
@@ -1516,7 +1527,8 @@ __global__ __launch_bounds__(64 * TAIL_WAVES) void k_fit_tail(const float *__res
         LmState L;
         lm_load(L, S, k);
         double xa = S.xa[k];
-        const float *p = D + (size_t)k * ldD;
+        // the row's samples are contiguous in runs of 32 (tiled) or whole
+        const RowRef p{D, (size_t)k, ldD, dtiled};
         while (st != ST_DONE) {
             ++nsw;
             if (st == ST_B) {
@@ -1786,6 +1798,8 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
             }
             p = a.D + k * (size_t)a.ldD;
         }
+        const bool tr = a.dtiled && mode == DIAG_EXACT;   // the tiled fit cube (dt_ofs)
+        auto prow = [&](int i) -> float { return tr ? a.D[dt_ofs(k, i, a.ldD)] : p[i]; };
         const bool ok = stt >= 1 && stt <= 4;
         // residual -> X (dispersed frame): X[j] = f32(f32(r[i]) * w), j = (i + sh) mod n
         // (f64(f32(r[i])) * f64(w) for f64 data)
@@ -1795,7 +1809,7 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
                 R = p[i];
             } else if (ok) {
                 const double u = x * T64[i];
-                double e = u - (double)p[i];
+                double e = u - (double)prow(i);
                 if (a.pr_on && i >= a.pr_start && i < a.pr_end) e = e * a.pr_factor;
                 R = (float)e;
             }
@@ -2192,9 +2206,18 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
     }
     constexpr bool closed = mode == DIAG_CLOSED || mode == DIAG_FIT;
     const double TT = closed ? *a.TT : 0.0;
-    const float *rows = mode == DIAG_CLOSED ? a.raw : a.D;
-    const size_t ld = mode == DIAG_CLOSED ? (size_t)N : (size_t)a.ldD;
+    // DIAG_EXACT reads the raw row, not the fit cube: the cube's value is
+    // D_i = f32(raw_j - base0), j = (i + sh) mod N (k_chan_partials mode 3), and
+    // the raw rows are contiguous whatever the cube's layout (dt_ofs)
+    constexpr bool fromraw = mode == DIAG_CLOSED || mode == DIAG_EXACT;
+    const float *rows = fromraw ? a.raw : a.D;
+    const size_t ld = fromraw ? (size_t)N : (size_t)a.ldD;
     float pv[NPT];
+    auto loadrow = [&](unsigned kk) {
+        const float *pn = rows + (size_t)kk * ld;
+#pragma unroll
+        for (int u = 0; u < NPT; ++u) pv[u] = pn[t + TPP * u];
+    };
     unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group);
     // per-profile scalars, loaded one profile ahead as well
     double nx = 0.0;
@@ -2202,14 +2225,13 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
     float nw = 0.0f, nb = 0.0f;
     if (k < P) {
         if (PREFETCH) {
-#pragma unroll
-            for (int u = 0; u < NPT; ++u) pv[u] = rows[(size_t)k * ld + t + TPP * u];
+            loadrow(k);
         }
         if (mode == DIAG_EXACT) {
             nx = a.amp[k];
             nst = a.info[k];
         }
-        if (mode == DIAG_CLOSED) nb = a.base[k];
+        if (fromraw) nb = a.base[k];
         nw = a.w0[k];
         nsh = (mode == DIAG_STATS || mode == DIAG_FIT) ? 0 : a.shift[k % (unsigned)nchan];
     }
@@ -2225,8 +2247,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         const int sh = nsh;
         const float bk = nb;
         if (!PREFETCH) {
-#pragma unroll
-            for (int u = 0; u < NPT; ++u) pv[u] = rows[(size_t)k * ld + t + TPP * u];
+            loadrow(k);
         }
         gsync<WPP>();
         if (closed) {
@@ -2267,11 +2288,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             gsync<WPP>();
         }
         if constexpr (mode == DIAG_FIT) {   // the amplitude is all this mode produces
-            if (PREFETCH && k + stride < P) {
-                const float *pn = rows + (size_t)(k + stride) * ld;
-#pragma unroll
-                for (int u = 0; u < NPT; ++u) pv[u] = pn[t + TPP * u];
-            }
+            if (PREFETCH && k + stride < P) loadrow(k + stride);
             continue;
         }
         const bool ok = st >= 1 && st <= 4;
@@ -2284,6 +2301,33 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         if (mode == DIAG_STATS) {
 #pragma unroll
             for (int u = 0; u < NPT; ++u) X[TPP % 128 == 0 ? xaddr(t) + u * (TPP + TPP / 16) : xaddr(t + TPP * u)] = weigh(pv[u]);
+        } else if (mode == DIAG_EXACT) {
+            // sample j = t + TPP u of the raw row (dispersed frame) is the
+            // dedispersed sample i = (j - sh) mod N: residual f32(x T_i - D_i)
+            // with D_i = f32(raw_j - base0), written to X[j]
+            const int i0 = (t - sh) & (N - 1);
+            double tg[NPT];   // the template gathered at i: all loads issued before the first use
+#pragma unroll
+            for (int u = 0; u < NPT; ++u) tg[u] = T[(i0 + TPP * u) & (N - 1)];
+            if (a.pr_on) {
+#pragma unroll
+                for (int u = 0; u < NPT; ++u) {
+                    const int i = (i0 + TPP * u) & (N - 1);
+                    const float pj = pv[u] - bk;
+                    double e = x * tg[u] - (double)pj;
+                    if (i >= a.pr_start && i < a.pr_end) e = e * a.pr_factor;
+                    const float R = ok ? (float)e : 0.0f;
+                    X[TPP % 128 == 0 ? xaddr(t) + u * (TPP + TPP / 16) : xaddr(t + TPP * u)] = weigh(R);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < NPT; ++u) {
+                    const float pj = pv[u] - bk;
+                    const double e = x * tg[u] - (double)pj;
+                    const float R = ok ? (float)e : 0.0f;
+                    X[TPP % 128 == 0 ? xaddr(t) + u * (TPP + TPP / 16) : xaddr(t + TPP * u)] = weigh(R);
+                }
+            }
         } else if (a.pr_on) {
             const XWrap<N, TPP> xw((t + sh) & (N - 1));
 #pragma unroll
@@ -2308,16 +2352,12 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         }
         if (k + stride < P) {
             const unsigned kn = k + stride;
-            if (PREFETCH) {
-                const float *pn = rows + (size_t)kn * ld;
-#pragma unroll
-                for (int u = 0; u < NPT; ++u) pv[u] = pn[t + TPP * u];
-            }
+            if (PREFETCH) loadrow(kn);
             if (mode == DIAG_EXACT) {
                 nx = a.amp[kn];
                 nst = a.info[kn];
             }
-            if (mode == DIAG_CLOSED) nb = a.base[kn];
+            if (fromraw) nb = a.base[kn];
             nw = a.w0[kn];
             nsh = mode == DIAG_STATS ? 0 : a.shift[kn % (unsigned)nchan];
         }
@@ -2453,8 +2493,8 @@ __global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, c
                                                   const float *__restrict__ base, const double *__restrict__ T64,
                                                   const double *__restrict__ amp, const int32_t *__restrict__ info,
                                                   const int32_t *__restrict__ shift, size_t P, int nchan, int nbin,
-                                                  int ldD, int pr_on, double pr_factor, int pr_start, int pr_end,
-                                                  float *__restrict__ R)
+                                                  int ldD, int dtiled, int pr_on, double pr_factor, int pr_start,
+                                                  int pr_end, float *__restrict__ R)
 {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (size_t k = (size_t)blockIdx.x * 4 + wave; k < P; k += (size_t)gridDim.x * 4) {
@@ -2468,7 +2508,7 @@ __global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, c
             if (j >= nbin) j -= nbin;
             float v = 0.0f;
             if (ok) {
-                const float p = D ? D[k * ldD + i] : raw[k * nbin + j] - b;
+                const float p = D ? D[d_ofs(k, i, ldD, dtiled)] : raw[k * nbin + j] - b;
                 const double u = a * T64[i];
                 double e = u - (double)p;
                 if (pr_on && i >= pr_start && i < pr_end) e = e * pr_factor;
@@ -3285,15 +3325,15 @@ static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) 
 
 hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, const float *W, const int32_t *shift,
                                 const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
-                                double *part, double *part2, double *wpart, float *D, int ldD)
+                                double *part, double *part2, double *wpart, float *D, int ldD, int dtiled)
 {
     const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
     dim3 grid(cdiv(nbin, bs), nsb, nsub);
-    if (mode == 3 && (!D || ldD < nbin)) return hipErrorInvalidValue;
+    if (mode == 3 && (!D || ldD < nbin || (dtiled && ldD % 32 != 0))) return hipErrorInvalidValue;
 #define IC_CP(M)                                                                                                  \
     hipLaunchKernelGGL(k_chan_partials<M>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin, \
-                       nsb, part, part2, wpart, D, ldD)
+                       nsb, part, part2, wpart, D, ldD, dtiled)
     if (mode == 0)
         IC_CP(0);
     else if (mode == 1)
@@ -3418,15 +3458,17 @@ hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P)
 }
 
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S)
+                           int dtiled, const int32_t *list, const int32_t *nlist, long bound,
+                           const FitStateArrays &S)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
     // sweep length: nbin rounded up to whole tile pairs (sweep_dma); the row
     // stride ldD may be longer (padding off the power-of-two stride)
     const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
-    if (ldD % 4 != 0 || ldD < nsw) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_fit_pass, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, list, nlist, S);
+    if (ldD % 4 != 0 || ldD < nsw || (dtiled && ldD % 32 != 0)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_fit_pass, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled, list,
+                       nlist, S);
     return hipGetLastError();
 }
 
@@ -3442,13 +3484,13 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
 }
 
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
+                           int dtiled, const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
                            double *amp, int32_t *info, unsigned long long *sweeps)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min<long>(cdiv(n, TAIL_WAVES), 65536);
-    hipLaunchKernelGGL(k_fit_tail, dim3(grid), dim3(64 * TAIL_WAVES), 0, st, D, T64, P, nbin, ldD, list, nlist,
+    hipLaunchKernelGGL(k_fit_tail, dim3(grid), dim3(64 * TAIL_WAVES), 0, st, D, T64, P, nbin, ldD, dtiled, list, nlist,
                        S, amp, info, sweeps);
     return hipGetLastError();
 }
@@ -3561,13 +3603,14 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
 
 hipError_t launch_residual(hipStream_t st, const float *D, const float *raw, const float *base, const double *T64,
                            const double *amp, const int32_t *info, const int32_t *shift, int nsub, int nchan,
-                           int nbin, int ldD, int pr_on, double pr_factor, int pr_start, int pr_end, float *R)
+                           int nbin, int ldD, int dtiled, int pr_on, double pr_factor, int pr_start, int pr_end,
+                           float *R)
 {
     const size_t P = (size_t)nsub * nchan;
     if (!D && (!raw || !base)) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
     hipLaunchKernelGGL(k_residual, dim3(grid), dim3(256), 0, st, D, raw, base, T64, amp, info, shift, P, nchan, nbin,
-                       ldD, pr_on, pr_factor, pr_start, pr_end, R);
+                       ldD, dtiled, pr_on, pr_factor, pr_start, pr_end, R);
     return hipGetLastError();
 }
 

@@ -124,6 +124,7 @@ struct Session {
     // the residual scratch, zero shifts/levels for the shift-indexed kernels,
     // and the phasor table [nchan][nbin/2 + 1] of ic_set_delays
     bool fftded = false, delays_set = false;
+    int dtiled = 0;                  // fit cube D in the tiled layout (dt_ofs)
     float *dr = nullptr, *Tc = nullptr, *R = nullptr, *zbase = nullptr;
     int32_t *zshift = nullptr;
     double2 *ph = nullptr;
@@ -552,7 +553,7 @@ int iteration_template(Session *s, int iter)
     if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s; also writes D (exact fit)
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, s->D ? 3 : 1, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan,
-                                    nbin, nullptr, s->part2, s->wpart, s->D, s->ldD));
+                                    nbin, nullptr, s->part2, s->wpart, s->D, s->ldD, s->dtiled));
     } else {
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, 2, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
@@ -621,13 +622,14 @@ int run_fit(Session *s)
     for (int r = 0;; ++r) {
         if (r >= kMaxRounds) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", r);
         if (bound <= s->tail_threshold) {
-            LAUNCH(s, K_FIT_TAIL, launch_fit_tail(s->stream, s->D, s->T64, P, nbin, s->ldD, cur, cin, bound,
+            LAUNCH(s, K_FIT_TAIL, launch_fit_tail(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
                                                   s->fs, s->amp, s->info, tail_sweeps));
             tail = true;
             break;
         }
         int32_t *next = bufs[r & 1];
-        LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, cur, cin, bound, s->fs));
+        LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
+                                                s->fs));
         s->h_rcount[r] = -1;
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
                                                 ctr + r, s->d_h_rcount + r));
@@ -786,6 +788,12 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     }
     AL(s->TT, 1);
     s->fftded = p.dedisp_mode == IC_DEDISP_FFT;
+    // the fit cube written by k_chan_partials mode 3 is tiled (k_rotate's, in
+    // the FFT mode, is row-major); IC_FIT_TILED=0: row-major (A/B knob)
+    {
+        const char *e = getenv("IC_FIT_TILED");
+        s->dtiled = (!s->fftded && !(e && atoi(e) == 0)) ? 1 : 0;
+    }
     if (s->fftded) {
         AL(s->dr, N);
         AL(s->Tc, N);
@@ -1139,6 +1147,7 @@ DiagArgs diag_args(Session *s, int pr_start, int pr_end)
     a.mode = p.fit_mode == IC_FIT_EXACT ? DIAG_EXACT : DIAG_CLOSED;
     a.D = s->D;
     a.ldD = s->ldD;
+    a.dtiled = s->dtiled;
     a.raw = s->raw;
     a.base = s->base0;
     a.T64 = s->T64;
@@ -1230,6 +1239,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             da.mode = DIAG_STATS;
             da.D = s->R;
             da.ldD = nbin;
+            da.dtiled = 0;
         }
         LAUNCH(s, K_DIAG, launch_diag(s->stream, da));
         // channel medians are local to a shard; row medians need whole rows
@@ -1315,7 +1325,7 @@ int ic_get_residual(void *session, float *out)
         e = launch_rotate(s->stream, ra);
     } else {
         e = launch_residual(s->stream, s->D, s->raw, s->base0, s->T64, s->amp, s->info, s->shift, p.nsub, s->nchan,
-                            p.nbin, s->ldD, p.pr_on, p.pr_factor, pr_start, pr_end, R);
+                            p.nbin, s->ldD, s->dtiled, p.pr_on, p.pr_factor, pr_start, pr_end, R);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(out, R, sizeof(float) * s->N, hipMemcpyDeviceToHost, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
@@ -1589,6 +1599,7 @@ int ic_fit_profiles(int device, int nprof, int nbin, const float *T, const float
         Session *s;
         ~Guard() { ic_session_destroy(s); }
     } guard{s};
+    s->dtiled = 0;   // D is filled row by row below
     const size_t P = s->P, row = sizeof(float) * (size_t)nbin;
     std::vector<double> t64(s->ldD, 0.0);
     for (int i = 0; i < nbin; ++i) t64[i] = (double)T[i];
@@ -1616,7 +1627,7 @@ int ic_fit_profiles(int device, int nprof, int nbin, const float *T, const float
         float *R = nullptr;
         CK(hipMalloc((void **)&R, sizeof(float) * s->N));
         hipError_t e = launch_residual(s->stream, s->D, s->raw, s->base0, s->T64, s->amp, s->info, s->shift, p.nsub,
-                                       s->nchan, nbin, s->ldD, 0, 1.0, 0, 0, R);
+                                       s->nchan, nbin, s->ldD, s->dtiled, 0, 1.0, 0, 0, R);
         if (e == hipSuccess) e = hipMemcpyAsync(resid_out, R, row * nprof, hipMemcpyDeviceToHost, s->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
         (void)hipFree(R);
