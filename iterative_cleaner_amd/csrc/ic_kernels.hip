@@ -2307,8 +2307,16 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             // with D_i = f32(raw_j - base0), written to X[j]
             const int i0 = (t - sh) & (N - 1);
             double tg[NPT];   // the template gathered at i: all loads issued before the first use
+            {
+                // byte offsets (8 i0 + 8 TPP u) mod 8N through a buffer descriptor: two VALU per load
+                const __amdgpu_buffer_rsrc_t tr =
+                    __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(T), 0, 8 * N, 0x00020000);
+                const unsigned b0 = 8u * (unsigned)i0;
 #pragma unroll
-            for (int u = 0; u < NPT; ++u) tg[u] = T[(i0 + TPP * u) & (N - 1)];
+                for (int u = 0; u < NPT; ++u)
+                    tg[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                           tr, (b0 + 8u * TPP * u) & (8u * N - 1u), 0, 0));
+            }
             if (a.pr_on) {
 #pragma unroll
                 for (int u = 0; u < NPT; ++u) {
