@@ -565,9 +565,11 @@ def main():
         # against HBM peak, or VALU issue against its peak
         vf = roof.get("valu", {}).get("frac")
         if vf is not None and vf > roof.get("traffic_frac", 0.0):
-            roof["bound"] = "valu"
-            roof["bound_note"] = "VALU issue (%.2f of peak) exceeds measured HBM traffic (%s of peak)" % (
-                vf, roof.get("traffic_frac"))
+            vv = roof["valu"]
+            roof.update({"bound": "valu", "achieved": vv["achieved"], "peak": vv["peak"], "unit": vv["unit"],
+                         "frac": vv["frac"]})
+            roof["bound_note"] = ("VALU issue (%.2f of peak) exceeds measured HBM traffic (%s of peak); the HBM "
+                                  "fraction in SURVEY §8(d) bytes is hbm_frac_s8d" % (vf, roof.get("traffic_frac")))
         elif "traffic_frac" in roof:
             roof["bound_note"] = ("measured HBM traffic %.2f of peak (re-sweeps included); frac/achieved use "
                                   "SURVEY §8(d) algorithmic bytes" % roof["traffic_frac"])
