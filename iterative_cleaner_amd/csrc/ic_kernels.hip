@@ -1270,6 +1270,15 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
     __shared__ int woff[FIT_STATE_BS / 64];
     const long slot = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long nact = list ? (long)*nlist : P;
+    // the grid is sized from an upper bound: blocks past the list return at
+    // once, and only the nblk blocks with work take part in the append (a
+    // same-address atomic each, ~12 ns apiece, serialised)
+    const long nblk = (nact + blockDim.x - 1) / blockDim.x;
+    if ((long)blockIdx.x >= nblk) {
+        if (nblk == 0 && blockIdx.x == 0 && threadIdx.x == 0)   // empty list: the count is 0
+            __hip_atomic_store(host_n, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     int still = 0;
     long k = 0;
     if (slot < nact) {
@@ -1338,7 +1347,7 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             woff[w] = base;
             base += wcnt[w];
         }
-        if ((old >> 32) == (unsigned long long)gridDim.x - 1)   // last block: base is the final count
+        if ((old >> 32) == (unsigned long long)nblk - 1)   // last block with work: base is the final count
             __hip_atomic_store(host_n, base, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
