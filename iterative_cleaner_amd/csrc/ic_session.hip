@@ -111,6 +111,8 @@ struct Session {
     int32_t *lists = nullptr;   // two active-profile lists of P entries
     int32_t *rcount = nullptr;  // u64 per round (blocks done << 32 | survivors) + tail sweep counter
     int32_t *h_rcount = nullptr;  // host-mapped mirror, written by k_fit_state's last block
+    int32_t *h_small = nullptr;   // pinned readback of the per-iteration counters and run stats
+                                  // (a pageable D2H copy is staged synchronously, ~30 us each)
     int32_t *d_h_rcount = nullptr;  // its device address
     hipEvent_t rev[2] = {nullptr, nullptr};
     void *fs_block = nullptr;   // one allocation backing fs
@@ -133,6 +135,7 @@ struct Session {
     int timing_only = -1;            // >= 0: time only this kernel id
     std::vector<Timed> events;
     std::vector<hipEvent_t> epool;   // reused across runs: no hipEventCreate in the timed region
+    hipEvent_t sev = nullptr;        // spin_sync's marker
     size_t enext = 0;
     double kms[K_COUNT] = {0};
     int klaunch[K_COUNT] = {0};
@@ -198,6 +201,17 @@ static hipError_t take_event(Session *s, hipEvent_t *e)
     return hipSuccess;
 }
 
+// wait for the stream by polling an event (the blocking wait's wake-up cost
+// ~0.1 ms per iteration boundary on the MI355X hosts)
+static hipError_t spin_sync(Session *s)
+{
+    hipError_t e = hipEventRecord(s->sev, s->stream);
+    if (e != hipSuccess) return e;
+    while ((e = hipEventQuery(s->sev)) == hipErrorNotReady) {
+    }
+    return e;
+}
+
 #define LAUNCH(S, KID, CALL)                                                   \
     do {                                                                       \
         Timed t_{KID, nullptr, nullptr};                                       \
@@ -245,7 +259,7 @@ std::vector<double2> p2_twiddles(int N)
 
 int collect_timing(Session *s)
 {
-    if (!s->timing) return 0;
+    if (s->events.empty()) return 0;
     CK(hipStreamSynchronize(s->stream));
     for (auto &e : s->events) {
         float ms = 0.f;
@@ -287,8 +301,10 @@ void free_all(Session *s)
         s->comm = nullptr;
     }
     if (s->h_rcount) (void)hipHostFree(s->h_rcount);
+    if (s->h_small) (void)hipHostFree(s->h_small);
     for (auto &e : s->rev)
         if (e) (void)hipEventDestroy(e);
+    if (s->sev) (void)hipEventDestroy(s->sev);
     for (auto &e : s->epool) (void)hipEventDestroy(e);
     s->epool.clear();
     s->events.clear();
@@ -639,7 +655,10 @@ int run_fit(Session *s)
         cin = (const int32_t *)(ctr + r);   // low word: the survivor count
         if (r >= 1) {
             // count after round r-1 (= input of round r) bounds the count after round r
-            CK(hipEventSynchronize(s->rev[(r - 1) & 1]));
+            hipError_t qe;
+            while ((qe = hipEventQuery(s->rev[(r - 1) & 1])) == hipErrorNotReady) {
+            }
+            CK(qe);
             const long c = s->h_rcount[r - 1];
             if (c == 0) break;   // round r had nothing to do
             bound = c;
@@ -900,6 +919,10 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     for (auto &e : s->rev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
             return bail(fail(IC_EHIP, "hipEventCreate failed"));
+    if (hipEventCreateWithFlags(&s->sev, hipEventDisableTiming) != hipSuccess)
+        return bail(fail(IC_EHIP, "hipEventCreate failed"));
+    if (hipHostMalloc((void **)&s->h_small, sizeof(int32_t) * ((size_t)p.max_iter + 16)) != hipSuccess)
+        return bail(fail(IC_ENOMEM, "hipHostMalloc(readback) failed"));
     if (exact) {
         // fit state: 23 double arrays + 5 int arrays, each padded to 256 B
         const size_t dstride = ((P * 8 + 255) / 256) * 256, istride = ((P * 4 + 255) / 256) * 256;
@@ -1113,6 +1136,8 @@ int ic_set_timing(void *session, int enabled)
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null session");
     s->timing = enabled != 0;
+    s->events.clear();   // events of earlier runs are discarded unread
+    s->enext = 0;
     for (int q = 0; q < K_COUNT; ++q) {
         s->kms[q] = 0.0;
         s->klaunch[q] = 0;
@@ -1124,6 +1149,7 @@ int ic_get_kernel_times(void *session, ic_kernel_time *out, int n)
 {
     Session *s = (Session *)session;
     if (!s || (!out && n > 0)) return fail(IC_EINVAL, "null argument");
+    if (int rc = collect_timing(s)) return rc;
     int m = 0;
     for (int q = 0; q < K_COUNT && m < n; ++q) {
         out[m].kernel = q;
@@ -1212,7 +1238,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     la.col_mad = s->lstat + 4 * nchan;
     la.row_med = s->lstat + 8 * nchan;
     la.row_mad = s->lstat + 8 * nchan + 4 * nsub;
-    std::vector<int32_t> cnt(p.max_iter + 5);
+    int32_t *cnt = s->h_small;   // [max_iter + 5] counters, then the run stats (pinned)
     s->bad_fits.clear();
     int x = 0, loops = -1, n_iter = 0, converged = 0;
     // k_fit_tail's sweep counter (after the per-round counters): one run's total
@@ -1254,9 +1280,9 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
                               s->test, s->W, s->hist, n_iter, s->counters));
         if (s->comm)
             CM(s, s->comm->allreduce_sum_i32(s->counters, (size_t)(n_iter + 4), s->stream), "convergence counters");
-        CK(hipMemcpyAsync(cnt.data(), s->counters, sizeof(int32_t) * (n_iter + 4), hipMemcpyDeviceToHost,
+        CK(hipMemcpyAsync(cnt, s->counters, sizeof(int32_t) * (n_iter + 4), hipMemcpyDeviceToHost,
                           s->stream));
-        CK(hipStreamSynchronize(s->stream));
+        CK(spin_sync(s));
         if (changed_out) changed_out[n_iter - 1] = cnt[0];
         if (nzero_out) nzero_out[n_iter - 1] = cnt[1];
         s->bad_fits.push_back(cnt[2]);
@@ -1274,16 +1300,17 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         CK(hipMemcpyAsync(test_out, s->test, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
     if (weights_out)
         CK(hipMemcpyAsync(weights_out, s->W, sizeof(float) * s->P, hipMemcpyDeviceToHost, s->stream));
-    CK(hipStreamSynchronize(s->stream));
     {
-        int32_t moves = 0;
-        CK(hipMemcpy(&moves, s->wflag + nsub, sizeof moves, hipMemcpyDeviceToHost));
-        s->stats.window_moves = moves;
-        unsigned long long tsw = 0;
-        CK(hipMemcpy(&tsw, (unsigned long long *)s->rcount + kMaxRounds, sizeof tsw, hipMemcpyDeviceToHost));
-        s->stats.fit_tail_sweeps += (int64_t)tsw;
+        int32_t *moves = s->h_small + p.max_iter + 6;                               // pinned
+        unsigned long long *tsw = (unsigned long long *)(s->h_small + ((p.max_iter + 9) & ~1));   // 8-B aligned
+        CK(hipMemcpyAsync(moves, s->wflag + nsub, sizeof *moves, hipMemcpyDeviceToHost, s->stream));
+        CK(hipMemcpyAsync(tsw, (unsigned long long *)s->rcount + kMaxRounds, sizeof *tsw, hipMemcpyDeviceToHost,
+                          s->stream));
+        CK(spin_sync(s));
+        s->stats.window_moves = *moves;
+        s->stats.fit_tail_sweeps += (int64_t)*tsw;
     }
-    if (int rc = collect_timing(s)) return rc;
+    // timing events are read when asked for (ic_get_kernel_times), not here
     if (loops_out) *loops_out = loops;
     if (n_iter_out) *n_iter_out = n_iter;
     s->stats.iterations = n_iter;
