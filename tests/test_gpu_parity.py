@@ -244,3 +244,27 @@ def test_extreme_amplitudes_match_c_oracle(fit_mode, oracle_lib):
     assert bits_equal(out["weights"], ref["weights"])
     assert bits_equal(amp, ref["amp"]) and bits_equal(info, ref["info"])
     assert bits_equal(sd, ref["std"]) and bits_equal(mn, ref["mean"])
+
+
+@pytest.mark.parametrize("path", [p for p in clean_fixtures() if "fft" not in os.path.basename(p)][:4],
+                         ids=lambda p: os.path.basename(p)[6:-4])
+def test_row_major_fit_cube_matches_tiled(path, monkeypatch):
+    """The fit cube's two layouts (IC_FIT_TILED, read at session creation:
+    tiled by default, row-major as the A/B baseline) give the same bits, and
+    both the reference's: layout moves bytes, never arithmetic."""
+    z, meta, raw, w0, shift, args = load_clean_case(path)
+    nit = int(z["n_iter"])
+    outs = []
+    for tiled in ("1", "0"):
+        monkeypatch.setenv("IC_FIT_TILED", tiled)
+        with _session(raw.shape, args, data_f64=meta.get("data_f64", False)) as s:
+            s.upload(raw, w0, shift)
+            out = s.run()
+            amp, info = s.fit()
+            resid = s.residual()
+        outs.append((out, amp, info, resid))
+    (o1, a1, i1, r1), (o0, a0, i0, r0) = outs
+    assert bits_equal(o1["weights"], z["weights_%d" % nit]) and bits_equal(o0["weights"], o1["weights"])
+    assert o1["loops"] == o0["loops"] == int(z["loops"])
+    assert bits_equal(a1, a0) and bits_equal(i1, i0)
+    assert nan_equal(r1, r0)
