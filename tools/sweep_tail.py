@@ -1,4 +1,4 @@
-"""Sweep the k_fit_tail hand-over threshold on the C2 bench workload (one GPU).
+"""Sweep the k_fit_tail hand-over threshold on a bench workload (one GPU; C2 by default).
 
 Prints one line per threshold: ms per clean (mean of --steps runs after one
 warm-up) and the per-kernel times of the fit kernels.
@@ -23,10 +23,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--thresholds", default="0,4096,8192,16384,32768,65536")
+    ap.add_argument("--workload", default="C2", choices=sorted(bench.WORKLOADS))
     a = ap.parse_args()
     _native.load_library()
     dev = torch.device("cuda:0")
-    nsub, nchan, nbin, seed, rfi = bench.WORKLOADS["C2"]
+    nsub, nchan, nbin, seed, rfi = bench.WORKLOADS[a.workload]
     cube, w0, shift = bench.make_cube_device(nsub, nchan, nbin, seed, rfi, dev)
     sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=0)
     torch.cuda.synchronize()
