@@ -123,6 +123,20 @@ struct OpOr {
 //           (iteration 1: base = base0, W = w0: the fit cube of ic.py:96-100 comes
 //           out of the same read of the cube)
 // flags != nullptr: only subints with flags[s] != 0 (a moved window) run.
+#ifndef IC_NT_FITCUBE
+#define IC_NT_FITCUBE 1
+#endif
+#ifndef IC_NT_RAW
+#define IC_NT_RAW 0
+#endif
+// the fit cube is written once and read by the next kernels' sweeps, not by
+// this one: non-temporal stores keep the write stream out of the way (A/B knob)
+__device__ __forceinline__ void st_fitcube(float *p, float v)
+{
+    if (IC_NT_FITCUBE) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k_chan_partials(
     const float *__restrict__ raw, const float *__restrict__ W, const int32_t *__restrict__ shift,
@@ -150,7 +164,8 @@ __global__ __launch_bounds__(256) void k_chan_partials(
             for (int q = 0; q < B; ++q) {
                 int j = i + shift[c + q];
                 if (j >= nbin) j -= nbin;
-                xv[q] = raw[(krow + c + q) * nbin + j];
+                xv[q] = IC_NT_RAW ? __builtin_nontemporal_load(&raw[(krow + c + q) * nbin + j])
+                                  : raw[(krow + c + q) * nbin + j];
                 wv[q] = W[krow + c + q];
                 bv[q] = F ? base[krow + c + q] : 0.0f;
             }
@@ -160,7 +175,7 @@ __global__ __launch_bounds__(256) void k_chan_partials(
                 const float d = xv[q] - bv[q];
                 if (A) acc = acc + w * (double)xv[q];
                 if (F) acc2 = acc2 + w * (double)d;
-                if (WD) D[d_ofs(krow + c + q, i, ldD, dtiled)] = d;
+                if (WD) st_fitcube(D + d_ofs(krow + c + q, i, ldD, dtiled), d);
             }
         }
         for (; c < c1; ++c) {
@@ -172,7 +187,7 @@ __global__ __launch_bounds__(256) void k_chan_partials(
             const float d = F ? x - base[k] : 0.0f;
             if (A) acc = acc + w * (double)x;
             if (F) acc2 = acc2 + w * (double)d;
-            if (WD) D[d_ofs(k, i, ldD, dtiled)] = d;
+            if (WD) st_fitcube(D + d_ofs(k, i, ldD, dtiled), d);
         }
         if (A) part[((size_t)s * nsb + sb) * nbin + i] = acc;
         if (F) part2[((size_t)s * nsb + sb) * nbin + i] = acc2;
@@ -808,6 +823,9 @@ __device__ __forceinline__ bool x_in_sq_range(double x)
 // all 64 lanes hits 16 distinct 16-B slots in each 16-lane bank group.
 // D is padded to [roundup(P,64)][ldD], ldD a multiple of 32: no guards.
 #define FIT_TB 16
+#ifndef IC_NT_SWEEP
+#define IC_NT_SWEEP 0
+#endif
 #ifndef IC_FIT_ROWPROBE
 #define IC_FIT_ROWPROBE 0
 #endif
@@ -833,7 +851,8 @@ __device__ __forceinline__ void dma_tile(const DmaTiles &d, char *buf, int b0)
 #pragma unroll
     for (int m = 0; m < 4; ++m)
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(d.src[m] + off),
-                                         (__attribute__((address_space(3))) void *)(buf + m * 1024), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void *)(buf + m * 1024), 16, 0,
+                                         IC_NT_SWEEP ? 2 : 0);   // cache policy: 2 = nt (A/B knob)
 }
 
 // ds_read in asm: the compiler would otherwise order every LDS read behind a
