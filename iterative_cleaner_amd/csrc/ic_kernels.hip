@@ -1534,7 +1534,10 @@ __device__ __forceinline__ double tail_sweep_b(const RowRef &p, const double *__
     return sum;
 }
 
-__global__ __launch_bounds__(64 * TAIL_WAVES) void k_fit_tail(const float *__restrict__ D,
+#ifndef IC_TAIL_MINW
+#define IC_TAIL_MINW 3   // waves per SIMD the register allocation must allow (A/B: 1 = 2 waves, 0.1 ms/clean slower)
+#endif
+__global__ __launch_bounds__(64 * TAIL_WAVES, IC_TAIL_MINW) void k_fit_tail(const float *__restrict__ D,
                                                               const double *__restrict__ T64, long P, int nbin,
                                                               int ldD, int dtiled, const int32_t *__restrict__ list,
                                                               const int32_t *__restrict__ nlist, FitStateArrays S,
