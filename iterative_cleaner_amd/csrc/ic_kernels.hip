@@ -1277,7 +1277,7 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 // profiles), and the last block to finish publishes the final count to
 // host-mapped memory (host_n), so the host needs no copy dispatch to learn it.
 #ifndef FIT_STATE_BS
-#define FIT_STATE_BS 256
+#define FIT_STATE_BS 512
 #endif
 __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
                                                             const int32_t *__restrict__ nlist,
@@ -1322,18 +1322,39 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             } else {
                 still = 1;
             }
+        } else if (st == ST_A0) {
+            // the first transition: the state is k_fit_init's (x = 1, par = 0,
+            // iter = 1) and lm_outer reads nothing else; on the usual way out (a B
+            // request) only the fields it set are written
+            LmState L;
+            L.x = 1.0; L.par = 0.0; L.iter = 1; L.info = 0;
+            L.acn2 = 0.0; L.J02 = 0.0; L.f02 = 0.0;
+            L.fnorm = S.o_fnorm[k];
+            L.nfev = 1;
+            L.acnorm = S.o_acnorm[k];
+            L.f0 = S.o_f0[k];
+            L.J0 = S.o_J0[k];
+            S.slow[k] = S.o_exact[k];
+            st = lm_outer(L);
+            if (st == ST_B) {
+                S.fnorm[k] = L.fnorm; S.nfev[k] = L.nfev; S.acnorm[k] = L.acnorm; S.f0[k] = L.f0;
+                S.J0[k] = L.J0; S.Jn0[k] = L.Jn0; S.aj[k] = L.aj; S.r[k] = L.r; S.diag[k] = L.diag;
+                S.xnorm[k] = L.xnorm; S.delta[k] = L.delta;
+            } else {
+                lm_store(L, S, k);
+            }
+            S.mode[k] = st;
+            if (st == ST_A2) S.xa[k] = L.x2;
+            if (st == ST_DONE) {
+                amp_o[k] = L.x;
+                info_o[k] = L.info;
+            } else {
+                still = 1;
+            }
         } else if (st != ST_DONE) {
             LmState L;
             lm_load(L, S, k);
-            if (st == ST_A0) {
-                L.fnorm = S.o_fnorm[k];
-                L.nfev = 1;
-                L.acnorm = S.o_acnorm[k];
-                L.f0 = S.o_f0[k];
-                L.J0 = S.o_J0[k];
-                S.slow[k] = S.o_exact[k];
-                st = lm_outer(L);
-            } else if (st == ST_A2) {
+            if (st == ST_A2) {
                 L.acn2 = S.o_acnorm[k];
                 L.f02 = S.o_f0[k];
                 L.J02 = S.o_J0[k];
