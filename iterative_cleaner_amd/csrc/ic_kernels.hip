@@ -3092,6 +3092,209 @@ __global__ __launch_bounds__(256) void k_linestats(LineStatsArgs a, int rows, in
     }
 }
 
+// ---- long lines: W waves per line -------------------------------------------
+// The rows (length nchan, a few thousand) are too few for one wave each to fill
+// the chip (4*nsub waves), and early radix digits put most keys of a wave in
+// one bin, so the LDS atomics serialise.  Here a block of W waves owns a line:
+// wave w gathers its own slice of the line into its own key segment, the 256
+// bins are shared by the block, and min/max/count/NaN flags are block
+// reductions.  Order statistics do not depend on where a key sits, so the
+// result is the one k_linestats computes.
+
+template <int W> struct GrpRed {
+    unsigned long long *s;   // 2*W slots
+    int wave, lane;
+    __device__ unsigned long long min_u64(unsigned long long v)
+    {
+        v = wave_min_u64(v);
+        if (lane == 0) s[wave] = v;
+        __syncthreads();
+        unsigned long long r = s[0];
+#pragma unroll
+        for (int i = 1; i < W; ++i) r = s[i] < r ? s[i] : r;
+        __syncthreads();
+        return r;
+    }
+    __device__ unsigned long long max_u64(unsigned long long v)
+    {
+        v = wave_max_u64(v);
+        if (lane == 0) s[wave] = v;
+        __syncthreads();
+        unsigned long long r = s[0];
+#pragma unroll
+        for (int i = 1; i < W; ++i) r = s[i] > r ? s[i] : r;
+        __syncthreads();
+        return r;
+    }
+    // min and max in one round trip
+    __device__ void minmax_u64(unsigned long long &lo, unsigned long long &hi)
+    {
+        lo = wave_min_u64(lo);
+        hi = wave_max_u64(hi);
+        if (lane == 0) {
+            s[wave] = lo;
+            s[W + wave] = hi;
+        }
+        __syncthreads();
+        lo = s[0];
+        hi = s[W];
+#pragma unroll
+        for (int i = 1; i < W; ++i) {
+            lo = s[i] < lo ? s[i] : lo;
+            hi = s[W + i] > hi ? s[W + i] : hi;
+        }
+        __syncthreads();
+    }
+    __device__ int sum_i(int v) { return sum_uniform(wave_sum_i(v)); }
+    // v already uniform across the wave
+    __device__ int sum_uniform(int v)
+    {
+        if (lane == 0) s[wave] = (unsigned long long)(unsigned)v;
+        __syncthreads();
+        int r = 0;
+#pragma unroll
+        for (int i = 0; i < W; ++i) r += (int)(unsigned)s[i];
+        __syncthreads();
+        return r;
+    }
+};
+
+// r-th smallest (0-based) over every wave's segment keys[0, n): uniform result
+template <int W>
+__device__ unsigned long long grp_select(GrpRed<W> &g, const unsigned long long *keys, int n, int r, unsigned *hist)
+{
+    const int lane = g.lane;
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int j = lane; j < n; j += 64) {
+        const unsigned long long k = keys[j];
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+    g.minmax_u64(lo, hi);
+    if (lo == hi) return lo;
+    const int top = 63 - __clzll((long long)(lo ^ hi));
+    int shift = (top / 8) * 8;
+    unsigned long long prefix = shift + 8 >= 64 ? 0ull : (lo & (~0ull << (shift + 8)));
+    for (; shift >= 0; shift -= 8) {
+        const unsigned long long hmask = shift + 8 >= 64 ? 0ull : (~0ull << (shift + 8));
+        for (int t = threadIdx.x; t < 256; t += 64 * W) hist[t] = 0u;
+        __syncthreads();
+        for (int j = lane; j < n; j += 64) {
+            const unsigned long long k = keys[j];
+            if ((k & hmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        const uint4 c4 = *(const uint4 *)&hist[lane * 4];
+        const int sl = (int)(c4.x + c4.y + c4.z + c4.w);
+        const int incl = wave_incl_scan(sl);
+        const unsigned long long over = __ballot(incl > r);
+        const int L = __ffsll((long long)over) - 1;
+        int below = __shfl(incl - sl, L);
+        const uint4 cl = *(const uint4 *)&hist[L * 4];
+        int bin = L * 4;
+        if (r - below >= (int)cl.x) {
+            below += cl.x;
+            ++bin;
+            if (r - below >= (int)cl.y) {
+                below += cl.y;
+                ++bin;
+                if (r - below >= (int)cl.z) {
+                    below += cl.z;
+                    ++bin;
+                }
+            }
+        }
+        r -= below;
+        prefix |= (unsigned long long)bin << shift;
+        __syncthreads();   // every wave has read the bins before the next zeroing
+    }
+    return prefix;
+}
+
+// median over the block's keys (ntot > 0 in total, no NaN), dtype arithmetic
+template <int W>
+__device__ double grp_median(GrpRed<W> &g, const unsigned long long *keys, int n, int ntot, bool f32, unsigned *hist)
+{
+    const int idx = ntot / 2;
+    if (ntot % 2) {
+        const double m = unkey64(grp_select<W>(g, keys, n, idx, hist));
+        return f32 ? (double)(0.0f + (float)m) : 0.0 + m;
+    }
+    const unsigned long long klo = grp_select<W>(g, keys, n, idx - 1, hist);
+    int le = 0;
+    unsigned long long nxt = ~0ull;
+    for (int j = g.lane; j < n; j += 64) {
+        const unsigned long long k = keys[j];
+        le += k <= klo;
+        if (k > klo && k < nxt) nxt = k;
+    }
+    le = g.sum_i(le);
+    nxt = g.min_u64(nxt);
+    const unsigned long long khi = le > idx ? klo : nxt;
+    const double lo = unkey64(klo), hi = unkey64(khi);
+    if (f32) {
+        const float t = (0.0f + (float)lo) + (float)hi;
+        return (double)(t / 2.0f);
+    }
+    const double t = (0.0 + lo) + hi;
+    return t / 2.0;
+}
+
+// one block of W waves per line; LDS: 256 bins, 2*W reduction slots, len keys
+template <int W> __global__ __launch_bounds__(64 * W) void k_linestats_grp(LineStatsArgs a, int rows, int len)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lsm[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    unsigned *hist = (unsigned *)lsm;
+    GrpRed<W> g{(unsigned long long *)(lsm + 1024), wave, lane};
+    const int nline = rows ? a.nsub : a.nchan;
+    const int line = blockIdx.x;
+    const int diag = line / nline, idx = line % nline;
+    const bool f32 = diag == 2 && a.ptp_f32, plain = diag == 3;
+    const int seg = (((len + W - 1) / W) + 63) & ~63;
+    const int q0w = wave * seg, q1w = min(len, q0w + seg);
+    unsigned long long *keys = (unsigned long long *)(lsm + 1024 + 16 * W) + q0w;
+    int cnt = 0, nan = 0;
+    for (int q0 = q0w; q0 < q1w; q0 += 64) {
+        const int q = q0 + lane;
+        double d = 0.0;
+        bool v = false;
+        if (q < q1w) {
+            const size_t kk = rows ? (size_t)idx * a.nchan + q : (size_t)q * a.nchan + idx;
+            v = plain ? true : (a.valid[kk] != 0);
+            d = diag == 0 ? a.std_d[kk] : diag == 1 ? a.mean_d[kk] : diag == 2 ? a.ptp_d[kk] : a.fft_d[kk];
+        }
+        const unsigned long long m = __ballot(v);
+        if (v) keys[cnt + __popcll(m & ((1ull << lane) - 1ull))] = key64(d);
+        nan |= v && isnan(d);
+        cnt += __popcll(m);
+    }
+    nan = g.sum_uniform(__any(nan) ? 1 : 0);   // the barrier also publishes the keys
+    const int ntot = g.sum_uniform(cnt);
+    double med = NAN, mad = NAN;
+    if (ntot > 0 && !nan) {
+        med = grp_median<W>(g, keys, cnt, ntot, f32, hist);
+        int rnan = 0;
+        for (int j = lane; j < cnt; j += 64) {
+            const double d = unkey64(keys[j]);
+            const double r = f32 ? (double)fabsf((float)d - (float)med) : fabs(d - med);
+            rnan |= isnan(r);
+            keys[j] = key64(r);
+        }
+        rnan = g.sum_uniform(__any(rnan) ? 1 : 0);
+        if (!rnan) mad = grp_median<W>(g, keys, cnt, ntot, f32, hist);
+    }
+    if (threadIdx.x == 0) {
+        if (!rows) {
+            a.col_med[diag * a.nchan + idx] = med;
+            a.col_mad[diag * a.nchan + idx] = mad;
+        } else {
+            a.row_med[diag * a.nsub + idx] = med;
+            a.row_mad[diag * a.nsub + idx] = mad;
+        }
+    }
+}
+
 // ============================================================ combine
 
 __device__ __forceinline__ double scale_masked_d(double dv, bool valid, double med, double mad, double thr)
@@ -3623,6 +3826,12 @@ hipError_t launch_tnorm(hipStream_t st, const double *T64, const PwPlan *plan, i
     return hipGetLastError();
 }
 
+static int env_knob(const char *name, int dflt)
+{
+    const char *e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
+}
+
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
 {
     // columns (length nsub), then rows (length nchan); wave-private LDS:
@@ -3632,6 +3841,24 @@ hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
         const int len = rows ? a.nchan : a.nsub;
         const int lines = 4 * (rows ? a.nsub : a.nchan);
         if (lines == 0 || len == 0) continue;
+        // few long lines (the rows): W waves per line (IC_LS_GRP = W in {0, 4, 8},
+        // 0 = one wave per line; IC_LS_GRP_MINLEN = the shortest line it takes)
+        if (lines < 8192 && len >= env_knob("IC_LS_GRP_MINLEN", 1024)) {
+            const int W = env_knob("IC_LS_GRP", 8);
+            if (W == 4 || W == 8) {
+                const int seg = (((len + W - 1) / W) + 63) & ~63;
+                const size_t gshm = 1024 + 16 * (size_t)W + (size_t)W * seg * 8;
+                if (gshm <= 160 * 1024) {
+                    if (W == 4)
+                        hipLaunchKernelGGL(k_linestats_grp<4>, dim3(lines), dim3(256), gshm, st, a, rows, len);
+                    else
+                        hipLaunchKernelGGL(k_linestats_grp<8>, dim3(lines), dim3(512), gshm, st, a, rows, len);
+                    const hipError_t e = hipGetLastError();
+                    if (e != hipSuccess) return e;
+                    continue;
+                }
+            }
+        }
         const int per_wave = 1024 + ((len * 8 + 15) / 16) * 16;
         int wpb = 4;
         while (wpb > 1 && (size_t)wpb * per_wave > 64 * 1024) --wpb;

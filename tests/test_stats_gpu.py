@@ -67,3 +67,37 @@ def test_stats_match_c_oracle_larger(nbin, oracle_lib):
     sd, mn, pt, ff = oracle_lib.diagnostics(Xw, w != 0)
     ref = oracle_lib.test_values(w != 0, sd, mn, pt, ff, 5, 5)
     _check(test, diags, ref, w != 0, (sd, mn, pt, ff))
+
+
+@pytest.mark.parametrize("grp", ["0", "4", "8"])
+def test_line_medians_per_block_match(grp, monkeypatch, oracle_lib):
+    """The per-line median/MAD in its two forms: one wave per line, and a block
+    of W waves per line (k_linestats_grp, taken by default for few lines of
+    >= 1024 values; IC_LS_GRP_MINLEN=1 forces it onto every line here).
+    Both must reproduce the reference's selections: the edge cases of
+    stats_cases.npz (NaN, empty, tied lines), and long rows (nchan 3000) with
+    ties, zapped entries and outliers against the C oracle."""
+    from oracle import restated as R
+
+    from iterative_cleaner_amd import _native
+    monkeypatch.setenv("IC_LS_GRP", grp)
+    monkeypatch.setenv("IC_LS_GRP_MINLEN", "1")
+    z = np.load(os.path.join(GOLDEN, "stats_cases.npz"))
+    for i in range(int(z["n"])):
+        X, w = z["X_%d" % i], z["w_%d" % i]
+        ct, st = thresholds(z, i)
+        test, diags = _native.comprehensive_stats(X, w, ct, st, diagnostics=True)
+        _check(test, diags, z["test_%d" % i], w != 0)
+    rng = np.random.default_rng(77)
+    for nsub, nchan, nbin in ((5, 3000, 32), (3, 1999, 16)):
+        X = rng.standard_normal((nsub, nchan, nbin)).astype(np.float32)
+        X[:, ::7, :] = np.round(X[:, ::7, :])           # ties
+        X[1, rng.integers(0, nchan, 40), :] += 80       # outliers
+        w = np.ones((nsub, nchan), np.float32)
+        w[:, rng.integers(0, nchan, 200)] = 0
+        w[2, :nchan // 2] = 0                           # a half-zapped row
+        test, diags = _native.comprehensive_stats(X, w, 5, 5, diagnostics=True)
+        Xw = R.weighted_cube(X, w)
+        sd, mn, pt, ff = oracle_lib.diagnostics(Xw, w != 0)
+        ref = oracle_lib.test_values(w != 0, sd, mn, pt, ff, 5, 5)
+        _check(test, diags, ref, w != 0, (sd, mn, pt, ff))
