@@ -2912,12 +2912,16 @@ __device__ __forceinline__ double unkey64(unsigned long long k)
 }
 
 // ---- per-line median / MAD: one wave per line, radix select ------------------
+#ifndef IC_LS_EARLY
+#define IC_LS_EARLY 1   // finish a select by one scan once a single key holds the prefix
+#endif
 // Lines: columns (length nsub) of each diagnostic, or rows (length nchan);
 // diag 0 std, 1 mean, 2 ptp (f32 arithmetic), 3 fft (plain: every entry valid).
 // The valid values of the line go to wave-private LDS as order-preserving
 // 64-bit keys (key64), compacted with a ballot.  Order statistics come from a
 // most-significant-digit radix select: 8-bit digits from the highest bit where min and max differ,
 // a 256-bin LDS histogram per digit, the target bin found by a DPP prefix scan.
+// Once the chosen bin holds a single key, one compare-only scan returns it.
 // numpy.ma median arithmetic: odd -> 0+mid, even -> ((0+lo)+hi)/2 in the
 // dtype; any NaN -> NaN.
 
@@ -2987,20 +2991,35 @@ __device__ unsigned long long wave_select(const unsigned long long *keys, int n,
         int below = __shfl(incl - sl, L);
         const uint4 cl = *(const uint4 *)&hist[L * 4];
         int bin = L * 4;
+        unsigned cb = cl.x;   // keys in the chosen bin
         if (r - below >= (int)cl.x) {
             below += cl.x;
             ++bin;
+            cb = cl.y;
             if (r - below >= (int)cl.y) {
                 below += cl.y;
                 ++bin;
+                cb = cl.z;
                 if (r - below >= (int)cl.z) {
                     below += cl.z;
                     ++bin;
+                    cb = cl.w;
                 }
             }
         }
         r -= below;
         prefix |= (unsigned long long)bin << shift;
+        if (IC_LS_EARLY && cb == 1u && shift > 0) {
+            // one key left under the prefix: it is the answer, found in one
+            // compare-only scan instead of the remaining digit passes
+            const unsigned long long m = ~0ull << shift;
+            unsigned long long f = 0ull;
+            for (int j = lane; j < n; j += 64) {
+                const unsigned long long k = keys[j];
+                if ((k & m) == prefix) f = k;
+            }
+            return wave_max_u64(f);
+        }
         wave_sync();
     }
     return prefix;
@@ -3192,20 +3211,33 @@ __device__ unsigned long long grp_select(GrpRed<W> &g, const unsigned long long 
         int below = __shfl(incl - sl, L);
         const uint4 cl = *(const uint4 *)&hist[L * 4];
         int bin = L * 4;
+        unsigned cb = cl.x;   // keys in the chosen bin
         if (r - below >= (int)cl.x) {
             below += cl.x;
             ++bin;
+            cb = cl.y;
             if (r - below >= (int)cl.y) {
                 below += cl.y;
                 ++bin;
+                cb = cl.z;
                 if (r - below >= (int)cl.z) {
                     below += cl.z;
                     ++bin;
+                    cb = cl.w;
                 }
             }
         }
         r -= below;
         prefix |= (unsigned long long)bin << shift;
+        if (IC_LS_EARLY && cb == 1u && shift > 0) {   // uniform: every wave read the same bins
+            const unsigned long long m = ~0ull << shift;
+            unsigned long long f = 0ull;
+            for (int j = lane; j < n; j += 64) {
+                const unsigned long long k = keys[j];
+                if ((k & m) == prefix) f = k;
+            }
+            return g.max_u64(f);   // its barriers also order the bin reads before any re-zeroing
+        }
         __syncthreads();   // every wave has read the bins before the next zeroing
     }
     return prefix;
