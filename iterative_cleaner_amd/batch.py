@@ -18,12 +18,17 @@ list): no collective.
 """
 from __future__ import annotations
 
+import os
 import queue
+import sys
 import threading
 
 import numpy as np
 
 from . import _native
+
+# how long closing the lanes waits for a worker's current ic_run (seconds)
+JOIN_TIMEOUT_S = float(os.environ.get("IC_BATCH_JOIN_TIMEOUT", "600"))
 
 
 def pipeline(session, items, fetch=True):
@@ -151,8 +156,14 @@ def run_lanes(sessions, items, fetch=True, stop=None):
                 work.put_nowait(None)
             except queue.Full:
                 break
-        for th in threads:
-            th.join()                     # at most the run a worker is in
+        for th, sess in zip(threads, sessions):
+            th.join(timeout=JOIN_TIMEOUT_S)   # at most the run a worker is in
+            if th.is_alive():
+                # a worker stuck inside ic_run: leak its session (never destroyed
+                # under a running call) rather than hang the caller's cleanup
+                sys.stderr.write("iterative_cleaner: batch lane still inside ic_run after %.0f s; "
+                                 "leaking its session\n" % JOIN_TIMEOUT_S)
+                sess.h = None
         feeder.join(timeout=5.0)          # may wait in `items`: the caller's stop ends that
 
 

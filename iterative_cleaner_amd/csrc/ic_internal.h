@@ -92,7 +92,9 @@ struct FitStateArrays {
         *x2, *pnorm, *wa1, *xa;
     int32_t *iter, *nfev, *mode, *slow;
     double *o_fnorm, *o_acnorm, *o_f0, *o_J0, *o_sum;
-    int32_t *o_exact;
+    int32_t *o_exact;   // bit 0: the A sweep took the exact path; bit 1: J(1) == T (round 0)
+    // the first outer iteration's profile-independent qrfac (k_fit_prep): U = {valid, acnorm, aj, Jn0}
+    double *U;
 };
 
 struct LineStatsArgs {
@@ -103,7 +105,14 @@ struct LineStatsArgs {
     int ptp_f32;                    // 1: ptp lines use f32 arithmetic (numpy.ma on f32 data)
     double *col_med, *col_mad;      // [4][nchan]
     double *row_med, *row_mad;      // [4][nsub]
+    // row-median form (A/B knobs, read from the environment by linestats_knobs
+    // when a session is created, never per launch): grp_waves waves per line
+    // (0 = one wave per line, 4 or 8) for rows of >= grp_minlen values
+    int grp_waves = 8, grp_minlen = 1024;
 };
+// IC_LS_GRP / IC_LS_GRP_MINLEN -> a.grp_waves / a.grp_minlen; an unsupported
+// IC_LS_GRP is reported on stderr and the default (8) kept
+void linestats_knobs(LineStatsArgs &a);
 
 // ---- launch wrappers (ic_kernels.hip); all asynchronous on `st` ----
 // mode 0: part = sum W*ded; 1: part2 = sum W*f32(ded-base) + wpart; 2: both;
@@ -152,20 +161,27 @@ hipError_t launch_unpack_rowstats(hipStream_t st, const ShardGeom &g, int rows_p
                                   double *row_med, double *row_mad);
 // buf[i] = sum_r gathered[r][i]
 hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, int n, int32_t *buf);
+// T2 (optional): [2 nbin] receives T64[0..nbin) twice
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
-                           double *T64);
+                           double *T64, double *T2 = nullptr);
 hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
+// S.U from the template (one thread; before round 0 of every fit)
+hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double *T64, int nbin);
 // list == nullptr: all P profiles; else list[0 .. *nlist) with *nlist <= bound
 // (the host sizes grids from a count it already knows: counts only shrink).
+// nlistB (the round after round 0 only): count of round 0's unanswered B
+// requests, stored from the end of the P-entry list down (k_fit_state's ctrB)
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const int32_t *nlist, long bound,
-                           const FitStateArrays &S);
+                           const FitStateArrays &S, const int32_t *nlistB = nullptr);
 // ctr: zeroed device counter, finished blocks << 32 | survivors (its low word,
 // little-endian, is the next round's list length); host_n: host-mapped int the
 // last block writes the final count to
+// ctrB (zeroed; used in round 0 only): see launch_fit_pass's nlistB
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
-                            unsigned long long *ctr, int32_t *host_n);
+                            unsigned long long *ctr, int32_t *host_n, const int32_t *nlistB = nullptr,
+                            unsigned *ctrB = nullptr);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
                            double *amp, int32_t *info, unsigned long long *sweeps);
@@ -185,6 +201,7 @@ struct DiagArgs {
     int ldD;
     const float *raw, *base;
     const double *T64, *TT;
+    const double *T2;   // [2 nbin]: T64[0..nbin) twice (k_diag_cl's wrap-free gather), or null
     double *amp;
     int32_t *info;
     const float *w0;

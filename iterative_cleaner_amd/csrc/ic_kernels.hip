@@ -26,6 +26,8 @@
 #include <float.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -58,18 +60,20 @@ constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirr
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v)
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, true));
 }
 template <int CTRL>
 __device__ __forceinline__ int dpp(int v)
 {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true);
 }
+// (every lane reads an in-range lane for these controls, so the f64 form needs
+// no `old` operand: mov_dpp saves the two zeroing moves per level)
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v)
 {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ float lane_read(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
@@ -421,7 +425,7 @@ __global__ __launch_bounds__(256) void k_sb_tree(const double *__restrict__ part
 // T[i] = f32( f32(sum_s wf*F / sum_s wf) * 10000 )
 __global__ __launch_bounds__(256) void k_tscrunch(const float *__restrict__ F, const float *__restrict__ wf,
                                                   int nsub, int nbin, float *__restrict__ T,
-                                                  double *__restrict__ T64)
+                                                  double *__restrict__ T64, double *__restrict__ T2)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nbin) return;
@@ -455,6 +459,10 @@ __global__ __launch_bounds__(256) void k_tscrunch(const float *__restrict__ F, c
     const float tt = t * 10000.0f;
     T[i] = tt;
     T64[i] = (double)tt;
+    if (T2) {
+        T2[i] = (double)tt;
+        T2[i + nbin] = (double)tt;
+    }
 }
 
 // ============================================================ exact lmdif
@@ -920,27 +928,36 @@ struct PassIn {
 struct PassOut {
     double fnorm, acnorm, f0, J0, sum;
     bool bad;                    // fast path left its verified range
+    bool jt;                     // FUSE: J(1) == T, sum is qtf's dot
 };
 
 // Fast sweep body: straight-line over a 16-bin tile, wave-uniform predicates
 // only (lanes that did not request the sweep compute on defaults; their
 // results are discarded).  Zero-padded samples (p = 0, T = 0) are exact
 // no-ops: f = J = 0 adds nothing to either norm, and Jn*f = 0 to the dot.
-template <bool DA, bool DB>
+// FUSE (round 0: DA at x = 1 for every lane, k_fit_init): the A sweep at
+// x = 1 specialised (1 t = t; h = 2^-26, so J = RN(d / h) = d 2^26 exactly,
+// which is what mdiv gives), plus the dot of the B sweep that would follow,
+// sum_i RN(Jn_i f_i) with Jn_i = RN(J_i / aj) (+1 at i = 0) and the shared aj
+// of k_fit_prep, and jt = (J_i == T_i for every i): when that holds, and the
+// profile's own qrfac is k_fit_prep's, the dot is the B sweep's own.
+template <bool DA, bool DB, bool FUSE = false>
 struct FastBody {
     static constexpr bool kPeel = true;
     const PassIn &in;
     const double *__restrict__ T64;
     FastAcc fF, fJ;
-    double fa0, Ja0, sum;
+    double fa0, Ja0, sum, fsum;
     int lo_ok;
+    bool jt;
 
     __device__ __forceinline__ FastBody(const PassIn &i, const double *T) : in(i), T64(T)
     {
         fa_zero(fF);
         fa_zero(fJ);
-        fa0 = Ja0 = sum = 0.0;
+        fa0 = Ja0 = sum = fsum = 0.0;
         lo_ok = 1;
+        jt = true;
     }
 
     // the flag is materialised here (empty asm): otherwise the compiler sinks
@@ -959,6 +976,7 @@ struct FastBody {
     __device__ __forceinline__ void fence()
     {
         asm volatile("" : "+v"(fF.s2), "+v"(fJ.s2), "+v"(sum), "+v"(fF.minhm1), "+v"(fJ.minhm1));
+        if (FUSE) asm volatile("" : "+v"(fsum));
     }
 
     double tv[FIT_TB];   // the tile's template values (wave-uniform: SGPRs)
@@ -981,7 +999,46 @@ struct FastBody {
         double p[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) p[k] = (double)pf[k];
-        if (DA) {
+        if (DA && FUSE) {
+            // x = 1: f = RN(t - p), d = RN(RN((1 + 2^-26) t) - p) - f, J = d 2^26
+            constexpr double xh1 = 1.0 + 0x1p-26;
+            double f[4], d[4], q[4], r[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = xh1 * t[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) f[k] = t[k] - p[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = d[k] - p[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = d[k] - f[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = d[k] * 0x1p26;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                fa_add<CHK>(fF, f[k]);
+                fa_add<CHK>(fJ, q[k]);
+            }
+            if (first) {
+                fa0 = f[0];
+                Ja0 = q[0];
+            }
+            // Jn = mdiv(J, aj, yaj, ylj) (the B sweep's), dot in sample order
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = q[k] * in.ylj;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = fma(q[k], in.yaj, d[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = fma(-in.ajb, d[k], q[k]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = fma(r[k], in.yaj, d[k]);
+            if (first) d[0] = d[0] + 1.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                jt = jt && (q[k] == t[k]);
+                d[k] = d[k] * f[k];
+                fsum = fsum + d[k];
+            }
+        } else if (DA) {
             double f[4], d[4], q[4], r[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) f[k] = in.xa * t[k];
@@ -1122,19 +1179,21 @@ struct ExactBody {
     }
 };
 
-template <bool DA, bool DB>
+template <bool DA, bool DB, bool FUSE = false>
 __device__ __forceinline__ void fast_sweep(const DmaTiles &d, int ldD, const PassIn &in,
                                            const double *__restrict__ T64, double agiant, PassOut &out)
 {
-    FastBody<DA, DB> body(in, T64);
+    FastBody<DA, DB, FUSE> body(in, T64);
     sweep_dma(d, ldD, body);
     const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant * agiant) >> 32);
     out.f0 = body.fa0;
     out.J0 = body.Ja0;
-    out.sum = body.sum;
+    out.sum = FUSE ? body.fsum : body.sum;
     out.fnorm = fa_fin(body.fF);
     out.acnorm = fa_fin(body.fJ);
     out.bad = DA && in.A && !(body.lo_ok && fa_hi_ok(body.fF, hg) && fa_hi_ok(body.fJ, hg));
+    // the dot counts only where J stayed in the fast path's verified range (mdiv = RN division)
+    out.jt = FUSE && body.jt && !out.bad;
 }
 
 // ---- split lmdif: state machine (k_fit_state) <-> data sweeps (k_fit_pass) ----
@@ -1162,6 +1221,24 @@ __device__ __forceinline__ void lm_store(const LmState &L, const FitStateArrays 
     S.iter[k] = L.iter; S.nfev[k] = L.nfev;
 }
 
+// A round's input list: list[0 .. nA), then - in the round after round 0 only -
+// the B requests that round 0's first transitions could not answer (k_fit_pass
+// summed qtf's dot for the others), stored from the end of the list buffer
+// down (list[P - 1 - j], j < nB), so that A and B requests sit in separate
+// waves: a wave with both runs both sweep bodies.
+struct RoundList {
+    const int32_t *list;
+    long nA, nB, P;
+    __device__ __forceinline__ RoundList(const int32_t *l, const int32_t *nlist, const int32_t *nlistB, long P_)
+        : list(l), nA(l ? (long)*nlist : P_), nB(l && nlistB ? (long)*nlistB : 0), P(P_) {}
+    __device__ __forceinline__ long n() const { return nA + nB; }
+    __device__ __forceinline__ long at(long s) const
+    {
+        if (!list) return s;
+        return s < nA ? (long)list[s] : (long)list[P - 1 - (s - nA)];
+    }
+};
+
 // request encoding in S.mode: ST_A0 / ST_A2 -> sweep A at S.xa; ST_B -> sweep B
 // at (S.x, S.aj); ST_DONE -> nothing.  S.slow: J at x came from an exact sweep.
 __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
@@ -1173,20 +1250,63 @@ __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
     S.x[k] = 1.0; S.par[k] = 0.0; S.iter[k] = 1; S.nfev[k] = 0; S.slow[k] = 0;
 }
 
-// list == nullptr: profiles [0, P) in order (first round); else list[0..nlist).
-// One wave per block (the LDS buffers are private to the wave: no barriers).
+// The first outer iteration, at x = 1 for every profile, has a Jacobian that is
+// the template itself: h = eps |x| = 2^-26 exactly, (1 + 2^-26) t is exact for
+// an f32 t, and whenever RN(t - p) and RN(RN((1 + 2^-26) t) - p) are exact (t
+// and p within ~2^29 of each other, or p = 0) the forward difference is
+// (2^-26 t) / 2^-26 = t exactly.  Then enorm(J) (= acnorm = ajnorm), the sign,
+// Jn_0 and qtf's weights Jn_i = RN(J_i / aj) are the same for every profile
+// (lm_outer, MINPACK qrfac with n = 1), and the B sweep's dot
+// sum_i RN(Jn_i f_i) can be summed in round 0 together with the A sweep, which
+// has the same f_i: one full sweep of the fit cube less per iteration.  A
+// profile whose J differs anywhere (k_fit_pass checks J_i == T_i), or whose
+// own acnorm / aj / Jn0 differ, sends its B request as before.
+// One thread: U = {valid, acnorm, aj, Jn0} (k_fit_pass's round-0 form computes
+// Jn_i = RN(J_i / aj) itself, as the B sweep does).
+__global__ __launch_bounds__(64) void k_fit_prep(const double *__restrict__ T64, int nbin, int nsw,
+                                                 double *__restrict__ U)
+{
+    if (threadIdx.x != 0) return;
+    // MINPACK enorm over the sweep (k_fit_pass: agiant = RGIANT/nbin, padded zeros are no-ops)
+    Enorm e;
+    en_zero(e);
+    const double agiant = kRgiant / (double)nbin;
+    for (int i = 0; i < nsw; ++i) en_add(e, T64[i], agiant);
+    const double acn = en_fin(e);
+    const double J0 = T64[0];
+    double ajnorm = acn, Jn0 = J0;   // lm_outer
+    if (ajnorm != 0.0) {
+        if (J0 < 0.0) ajnorm = -ajnorm;
+        Jn0 = J0 / ajnorm;
+        Jn0 = Jn0 + 1.0;
+    }
+    // the fast B sweep's conditions on aj as well (x = 1 is in range)
+    const bool valid = acn != 0.0 && Jn0 != 0.0 && x_in_fast_range(ajnorm);
+    U[0] = valid ? 1.0 : 0.0;
+    U[1] = acn;
+    U[2] = valid ? ajnorm : 1.0;
+    U[3] = Jn0;
+}
+
+// R0: the round-0 form (list == nullptr, every request A at x = 1), which sums
+// the first B sweep's dot in the same sweep (k_fit_prep's U); a kernel of its
+// own so that the other rounds keep their register allocation (and occupancy)
+template <bool R0>
 __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, const double *__restrict__ T64,
                                                  long P, int nbin, int ldD, int nsw, int dtiled,
                                                  const int32_t *__restrict__ list,
-                                                 const int32_t *__restrict__ nlist, FitStateArrays S)
+                                                 const int32_t *__restrict__ nlist,
+                                                 const int32_t *__restrict__ nlistB, FitStateArrays S,
+                                                 const double *__restrict__ U)
 {
     __shared__ __attribute__((aligned(16))) char lbuf[2 * FIT_BUF];
     const int lane = threadIdx.x;
     const long slot = (long)blockIdx.x * 64 + lane;
-    const long nact = list ? (long)*nlist : P;   // the grid is only an upper bound
+    const RoundList rl(list, nlist, nlistB, P);
+    const long nact = rl.n();   // the grid is only an upper bound
     if ((long)blockIdx.x * 64 >= nact) return;
     const bool in_range = slot < nact;
-    const long k = in_range ? (list ? (long)list[slot] : slot) : 0;
+    const long k = in_range ? rl.at(slot) : 0;
     const int st = in_range ? S.mode[k] : ST_DONE;
     const bool reqA = (st == ST_A0) || (st == ST_A2);
     const bool reqB = (st == ST_B);
@@ -1200,7 +1320,7 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
         for (int m = 0; m < 4; ++m) {
             const long sl = (long)blockIdx.x * 64 + m * 16 + (lane >> 2);
             long kr = 0;   // empty slots read row 0 (valid: D is padded)
-            if (sl < nact) kr = list ? (long)list[sl] : sl;
+            if (sl < nact) kr = rl.at(sl);
 #if IC_FIT_ROWPROBE   // A/B probe only: every wave sweeps rows 0..63 (L2-resident data, VALU-only time)
             kr = m * 16 + (lane >> 2);
 #endif
@@ -1235,15 +1355,28 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     in.A = fastA;
     in.B = fastB;
     PassOut o;
-    o.bad = false;
+    o.bad = o.jt = false;
     o.fnorm = o.acnorm = o.f0 = o.J0 = o.sum = 0.0;
     const bool anyA = __any(fastA), anyB = __any(fastB);
-    if (anyA && anyB)
-        fast_sweep<true, true>(dt, nsw, in, T64, agiant, o);
-    else if (anyA)
-        fast_sweep<true, false>(dt, nsw, in, T64, agiant, o);
-    else if (anyB)
-        fast_sweep<false, true>(dt, nsw, in, T64, agiant, o);
+    if constexpr (R0) {
+        // every profile at x = 1: the first B sweep's dot rides along (k_fit_prep)
+        // (the dot is summed even when k_fit_prep found no shared qrfac, U[0] == 0:
+        // k_fit_state then ignores it)
+        in.ajb = U[2];
+        in.yaj = 1.0 / in.ajb;
+        in.ylj = recip_lo(in.ajb, in.yaj);
+        // uniform, but held in VGPRs: the sweep's scalars (a tile of template
+        // values) already fill the SGPR file
+        asm volatile("" : "+v"(in.ajb), "+v"(in.yaj), "+v"(in.ylj));
+        if (anyA) fast_sweep<true, false, true>(dt, nsw, in, T64, agiant, o);
+    } else {
+        if (anyA && anyB)
+            fast_sweep<true, true>(dt, nsw, in, T64, agiant, o);
+        else if (anyA)
+            fast_sweep<true, false>(dt, nsw, in, T64, agiant, o);
+        else if (anyB)
+            fast_sweep<false, true>(dt, nsw, in, T64, agiant, o);
+    }
     const bool exA = reqA && (!fastA || o.bad);
     const bool exB = reqB && !fastB;
     if (__any(exA || exB)) {
@@ -1265,7 +1398,8 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
         S.o_acnorm[k] = o.acnorm;
         S.o_f0[k] = o.f0;
         S.o_J0[k] = o.J0;
-        S.o_exact[k] = exA ? 1 : 0;
+        S.o_exact[k] = (exA ? 1 : 0) | (o.jt ? 2 : 0);
+        if (o.jt) S.o_sum[k] = o.sum;
     }
     if (reqB) S.o_sum[k] = o.sum;
 }
@@ -1279,16 +1413,23 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 #ifndef FIT_STATE_BS
 #define FIT_STATE_BS 512
 #endif
+// ctrB (round 0 only, list == nullptr): count of the unanswered B requests,
+// appended from the end of next_list down (RoundList).
 __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
                                                             const int32_t *__restrict__ nlist,
+                                                            const int32_t *__restrict__ nlistB,
                                                             double *__restrict__ amp_o, int32_t *__restrict__ info_o,
                                                             int32_t *__restrict__ next_list,
-                                                            unsigned long long *__restrict__ ctr, int32_t *host_n)
+                                                            unsigned long long *__restrict__ ctr,
+                                                            unsigned *__restrict__ ctrB, int32_t *host_n)
 {
     __shared__ int wcnt[FIT_STATE_BS / 64];
     __shared__ int woff[FIT_STATE_BS / 64];
+    __shared__ int wcntB[FIT_STATE_BS / 64];
+    __shared__ int woffB[FIT_STATE_BS / 64];
     const long slot = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long nact = list ? (long)*nlist : P;
+    const RoundList rl(list, nlist, nlistB, P);
+    const long nact = rl.n();
     // the grid is sized from an upper bound: blocks past the list return at
     // once, and only the nblk blocks with work take part in the append (a
     // same-address atomic each, ~12 ns apiece, serialised)
@@ -1298,10 +1439,10 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             __hip_atomic_store(host_n, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
-    int still = 0;
+    int still = 0, stillB = 0;
     long k = 0;
     if (slot < nact) {
-        k = list ? (long)list[slot] : slot;
+        k = rl.at(slot);
         int st = S.mode[k];
         if (st == ST_B) {
             // after a B sweep only qtf and the inner-loop start change: read the
@@ -1334,9 +1475,16 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             L.acnorm = S.o_acnorm[k];
             L.f0 = S.o_f0[k];
             L.J0 = S.o_J0[k];
-            S.slow[k] = S.o_exact[k];
+            const int oe = S.o_exact[k];
+            S.slow[k] = oe & 1;
             st = lm_outer(L);
-            if (st == ST_B) {
+            // J(1) == T and the same qrfac as k_fit_prep's: the round-0 sweep
+            // already summed qtf's dot, so the B request is answered here
+            if (st == ST_B && (oe & 2) && S.U[0] != 0.0 && L.acnorm == S.U[1] && L.aj == S.U[2] &&
+                L.Jn0 == S.U[3]) {
+                st = lm_after_b(L, S.o_sum[k]);
+                lm_store(L, S, k);
+            } else if (st == ST_B) {
                 S.fnorm[k] = L.fnorm; S.nfev[k] = L.nfev; S.acnorm[k] = L.acnorm; S.f0[k] = L.f0;
                 S.J0[k] = L.J0; S.Jn0[k] = L.Jn0; S.aj[k] = L.aj; S.r[k] = L.r; S.diag[k] = L.diag;
                 S.xnorm[k] = L.xnorm; S.delta[k] = L.delta;
@@ -1348,6 +1496,8 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             if (st == ST_DONE) {
                 amp_o[k] = L.x;
                 info_o[k] = L.info;
+            } else if (st == ST_B && ctrB) {
+                stillB = 1;   // round 0's unanswered B request: the other region
             } else {
                 still = 1;
             }
@@ -1359,7 +1509,7 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
                 L.f02 = S.o_f0[k];
                 L.J02 = S.o_J0[k];
                 st = lm_after_a2(L, S.o_fnorm[k]);
-                if (L.x == L.x2) S.slow[k] = S.o_exact[k];
+                if (L.x == L.x2) S.slow[k] = S.o_exact[k] & 1;
             }
             lm_store(L, S, k);
             S.mode[k] = st;
@@ -1375,11 +1525,27 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
     // block-aggregated append
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned long long m = __ballot(still);
-    if (lane == 0) wcnt[wave] = __popcll(m);
+    const unsigned long long mB = ctrB ? __ballot(stillB) : 0ull;
+    if (lane == 0) {
+        wcnt[wave] = __popcll(m);
+        wcntB[wave] = __popcll(mB);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += wcnt[w];
+        int tot = 0, totB = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+            tot += wcnt[w];
+            totB += wcntB[w];
+        }
+        if (ctrB) {
+            // the B region first, ordered before this block counts as finished
+            int baseB = totB ? (int)atomicAdd(ctrB, (unsigned)totB) : 0;
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+                woffB[w] = baseB;
+                baseB += wcntB[w];
+            }
+            __threadfence();
+        }
         // one atomic per block: finished blocks in the high word, survivors in the low
         const unsigned long long old = atomicAdd(ctr, (1ull << 32) | (unsigned long long)(unsigned)tot);
         int base = (int)(uint32_t)old;
@@ -1387,11 +1553,17 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             woff[w] = base;
             base += wcnt[w];
         }
-        if ((old >> 32) == (unsigned long long)nblk - 1)   // last block with work: base is the final count
+        if ((old >> 32) == (unsigned long long)nblk - 1) {   // last block with work: base is the final count
+            if (ctrB) {
+                __threadfence();
+                base += (int)__hip_atomic_load(ctrB, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            }
             __hip_atomic_store(host_n, base, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     __syncthreads();
     if (still) next_list[woff[wave] + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
+    if (stillB) next_list[P - 1 - (woffB[wave] + __popcll(mB & ((1ull << lane) - 1ull)))] = (int32_t)k;
 }
 
 // ---- tail: the last few thousand profiles, one wave each, to completion ----
@@ -2534,6 +2706,317 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             // invalid: rfft of f64(X) = +-0 -> 0, unless R was non-finite (X NaN)
             int nanx = 0;
             for (int i = t; i < N; i += TPP) nanx |= isnan(X[xaddr(i)]);
+            nanx = group_tree<WPP, 64>(nanx, OpOr(), (int *)(red + 52), wave, lane);
+            fftv = nanx ? NAN : 0.0;
+        }
+        if (t == 0) {
+            a.std_o[k] = valid ? sd : 0.0;
+            a.mean_o[k] = valid ? mean : 0.0;
+            a.ptp_o[k] = ptp;
+            a.fft_o[k] = fftv;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_diag_cl<N, MODE>: DIAG_EXACT / DIAG_CLOSED diagnostics for N >= 1024 (f32
+// data, no pulse region), chain layout.  Same arithmetic and the same bits as
+// k_diag_p2 (ic.py:206-217, :272-288, :296); what changes is where the data
+// lives:
+// - Thread t of a profile group (L = N/16 threads: one wave at N = 1024) owns
+//   pairwise chain t = (leaf t/8, accumulator t%8), the dispersed-frame samples
+//   j = 128(t/8) + t%8 + 8q, q < 16, and loads them straight from the raw row
+//   (one 64-bit address per profile, immediate offsets 32q).
+// - The template is gathered at i = (j - sh) mod N from T2 = [T, T] (2N f64),
+//   so the wrap costs nothing: one address, immediate offsets 64q.
+// - mean / var / ptp run on the residual in registers (no LDS round trip), and
+//   the var pass stores d = f64(X) - mean, which IS the FFT's input, as f64
+//   into the complex work array in the first stage's gather order, so the FFT
+//   starts without conversions or subtractions.  The work array's input image
+//   is swizzled slot(p) = p ^ (((p >> 6) & 3) << 2): the chain stores (32
+//   lanes x 8 B per half-wave) and the stage-1 gathers (16-B points) are both
+//   bank-conflict free, and all addresses are per-thread bases + immediates.
+// - Profile-uniform conditions (fit status, w0 == 0 / 1) are scalar branches.
+// DIAG_CLOSED first forms the closed-form amplitude over the dedispersed-frame
+// chains (p_i gathered from raw at (i + sh) mod N, k_diag_p2's arithmetic).
+constexpr int p2_tw_entries(int N)
+{
+    const int M = N / 2;
+    int lg = 0;
+    while ((1 << lg) < M) ++lg;
+    int n = M;
+    for (int done = 0, ns = 1; done < lg;) {
+        const int rem = lg - done, R = rem >= 3 ? 8 : (rem == 2 ? 4 : 2);
+        if (ns > 1) n += ns * (R - 1);
+        ns *= R;
+        done += R == 8 ? 3 : (R == 4 ? 2 : 1);
+    }
+    return n;
+}
+
+// A/B build knobs of the one-wave (N = 1024) form: IC_CL_TWG = twiddles read
+// through L1/L2 instead of an LDS copy, IC_CL_MINW = waves per SIMD the
+// register allocation must allow, IC_CL_GPB = waves (profile groups) per block
+#ifndef IC_CL_OPAQUE_T
+#define IC_CL_OPAQUE_T 0
+#endif
+#ifndef IC_CL_TWG
+#define IC_CL_TWG 0
+#endif
+#ifndef IC_CL_MINW
+#define IC_CL_MINW 4
+#endif
+#ifndef IC_CL_GPB
+#define IC_CL_GPB 8
+#endif
+// timing probes (wrong results; A/B builds only): 1 = no template gather,
+// 2 = no raw row loads, 3 = FFT stages 2.. skipped
+#ifndef IC_CL_PROBE
+#define IC_CL_PROBE 0
+#endif
+template <int N>
+struct CLay {
+    static constexpr int L = N / 16;     // threads per profile = chains of 16 samples
+    static constexpr int WPP = L / 64;   // waves per profile
+    static constexpr int M = N / 2;
+    static constexpr int LG = __builtin_ctz(M);
+    static constexpr int GPB = WPP > 1 ? 1 : IC_CL_GPB;   // profile groups per block
+    static constexpr bool TWG = WPP > 1 || IC_CL_TWG;   // multi-wave groups read the table through L1/L2
+    static constexpr int TW_LDS = TWG ? 0 : p2_tw_entries(N);
+    static constexpr int CBYTES = M * 16;
+    static constexpr int RED_BYTES = WPP > 1 ? 512 : 0;
+    static constexpr int GROUP_BYTES = CBYTES + RED_BYTES;
+    static_assert(N >= 1024 && L % 64 == 0, "chain layout: one chain of 16 samples per thread");
+};
+
+__device__ __forceinline__ float ufirst(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+__device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double ufirst(double v)
+{
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+
+template <int N, int MODE>
+__global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MINW) void k_diag_cl(DiagArgs a)
+{
+    using C = CLay<N>;
+    constexpr int L = C::L, WPP = C::WPP, M = C::M;
+    constexpr bool closed = MODE == DIAG_CLOSED;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const double2 *tw = C::TWG ? a.tw_p2 : (const double2 *)smem;
+    const int lane = threadIdx.x & 63;
+    const int group = WPP == 1 ? (int)(threadIdx.x >> 6) : 0;
+    const int gpb = WPP == 1 ? (int)(blockDim.x >> 6) : 1;
+    const int wave = WPP == 1 ? 0 : (int)(threadIdx.x >> 6);
+    int t = WPP == 1 ? lane : (int)threadIdx.x;
+    if (!C::TWG) {
+        for (int q = threadIdx.x; q < C::TW_LDS; q += blockDim.x) ((double2 *)smem)[q] = a.tw_p2[q];
+        __syncthreads();
+    }
+    unsigned char *gb = smem + (size_t)C::TW_LDS * 16 + (size_t)group * C::GROUP_BYTES;
+    double2 *Cb = (double2 *)gb;
+    double *red = (double *)(gb + C::CBYTES);
+    const unsigned P = (unsigned)a.nsub * (unsigned)a.nchan;
+    const unsigned stride = gridDim.x * gpb;
+    const unsigned nchan = (unsigned)a.nchan;
+    const int ca = t >> 3, cc = t & 7;
+    const int jb = 128 * ca + cc;   // first sample of the thread's chain
+    // byte offsets in the work array: d of chain sample q at wb[q & 3] + 64 (q & ~3)
+    // (point p = jb/2 + 4q, part cc & 1); stage-1 point t + L r at rb[r & 3] + 16 L r
+    int wb[4], rb[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        wb[m] = 16 * (64 * ca + ((4 * m + (cc >> 1)) ^ (4 * (ca & 3)))) + 8 * (cc & 1);
+        rb[m] = 16 * (t ^ ((((t >> 6) + (L / 64) * m) & 3) << 2));
+    }
+    float pv[16];
+    auto loadrow = [&](unsigned kk) {
+        const float *pn = a.raw + (size_t)kk * N + jb;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) pv[q] = IC_CL_PROBE == 2 ? (float)(q + kk) : pn[8 * q];
+    };
+    unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group);
+    double nx = 0.0;
+    int nst = 0, nsh = 0;
+    float nw = 0.0f, nb = 0.0f;
+    if (k < P) {
+        loadrow(k);
+        if (!closed) {
+            nx = a.amp[k];
+            nst = a.info[k];
+        }
+        nb = a.base[k];
+        nw = a.w0[k];
+        nsh = a.shift[k % nchan];
+    }
+    for (; k < P; k += stride) {
+        // multi-wave groups: keep the FFT's LDS addresses inside the loop (hoisted,
+        // they spill at N >= 2048; k_diag_p2); one wave: hoisted, 118 VGPRs
+        if (WPP > 1 || IC_CL_OPAQUE_T) asm volatile("" : "+v"(t));
+        double x = ufirst(nx);
+        int st = ufirst(nst);
+        const float w = ufirst(nw);
+        const float bk = nb;
+        const int sh = ufirst(nsh);
+        // template at the dedispersed index of every chain sample
+        double tg[16];
+        {
+            const double *tb = a.T2 + ((unsigned)(jb - sh) & (unsigned)(N - 1));
+#pragma unroll
+            for (int q = 0; q < 16; ++q) tg[q] = IC_CL_PROBE == 1 ? 1.0 + q : tb[8 * q];
+        }
+        if constexpr (closed) {
+            // a = sum(T*p)/sum(T*T) over the dedispersed-frame chains i = jb + 8q,
+            // p_i = f32(raw[(i + sh) mod N] - base)
+            const float *row = a.raw + (size_t)k * N;
+            const unsigned j0 = (unsigned)(jb + sh);
+            float pi[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) pi[q] = row[(j0 + 8u * q) & (unsigned)(N - 1)];
+            double r = a.T64[jb] * (double)(pi[0] - bk);
+#pragma unroll
+            for (int q = 1; q < 16; ++q) {
+                const double pr = a.T64[jb + 8 * q] * (double)(pi[q] - bk);
+                r = r + pr;
+            }
+            double cs[1] = {r};
+            const double dot = 0.0 + chain_total<N, double>(cs, red, wave, lane);
+            const double TT = *a.TT;
+            x = ufirst(TT != 0.0 ? dot / TT : 0.0);
+            st = isfinite(x) ? 1 : 5;
+            if (t == 0) {
+                a.amp[k] = x;
+                a.info[k] = st;
+            }
+        }
+        // residual (ic.py:279-288) of the dispersed-frame sample j, f32 store
+        // (:272), apply_weights (:296): X_j = f32(f32(x T_i - D_i) * w), D_i = f32(raw_j - base0)
+        const bool ok = st >= 1 && st <= 4;
+        const bool valid = w != 0.0f;
+        float X[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const float pj = pv[q] - bk;
+            const double e = x * tg[q] - (double)pj;
+            X[q] = (float)e;
+        }
+        if (w != 1.0f) {   // fractional weights (w * 1 = w exactly: skipped)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) X[q] = X[q] * w;
+        }
+        if (!ok) {   // a bad leastsq status zeroes the residual (ic.py:284-286)
+            asm volatile("");   // a rare branch, not 16 selects on every profile
+#pragma unroll
+            for (int q = 0; q < 16; ++q) X[q] = 0.0f * w;
+        }
+        if (k + stride < P) {
+            const unsigned kn = k + stride;
+            loadrow(kn);
+            if (!closed) {
+                nx = a.amp[kn];
+                nst = a.info[kn];
+            }
+            nb = a.base[kn];
+            nw = a.w0[kn];
+            nsh = a.shift[kn % nchan];
+        }
+        double mean = 0.0, sd = 0.0, fftv = 0.0, ptp = (double)1e20f;
+        if (valid) {
+            // mean: f32 chain, then the pairwise tree (ic.py:207)
+            float s = X[0];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) s = s + X[q];
+            float fs[1] = {s};
+            const float s32 = 0.0f + chain_total<N, float>(fs, (float *)(red + 16), wave, lane);
+            mean = (double)s32 / (double)N;
+            // the previous profile's spectrum reads are done before d overwrites the array
+            gsync<WPP>();
+            // var (ic.py:206): f64 pairwise sum of (f64(X) - mean)^2; d -> FFT input
+            double r = 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const double d = (double)X[q] - mean;
+                const double sq = d * d;
+                r = q == 0 ? sq : r + sq;
+                *(double *)(gb + wb[q & 3] + 64 * (q & ~3)) = d;
+            }
+            double rs[1] = {r};
+            const double ss = 0.0 + chain_total<N, double>(rs, red + 24, wave, lane);
+            sd = sqrt(ss / (double)N);
+            // ptp (ic.py:208), NaN-propagating
+            float mx = -INFINITY, mn = INFINITY;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                mx = OpMaxF()(mx, X[q]);
+                mn = OpMinF()(mn, X[q]);
+            }
+            mx = group_tree<WPP, 64>(mx, OpMaxF(), (float *)(red + 32), wave, lane);
+            mn = group_tree<WPP, 64>(mn, OpMinF(), (float *)(red + 36), wave, lane);
+            int nan = 0;
+            if (isnan(s32)) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) nan |= isnan(X[q]);
+                nan = group_tree<WPP, 64>(nan, OpOr(), (int *)(red + 40), wave, lane);
+            }
+            ptp = nan ? (double)NAN : (double)(float)(mx - mn);
+            // rFFT of d (ic.py:210-212): stage 1 (radix 8, no twiddles) from the
+            // swizzled input image, then k_diag_p2's stages
+            gsync<WPP>();
+            double2 v[8];
+#pragma unroll
+            for (int r8 = 0; r8 < 8; ++r8) v[r8] = *(const double2 *)(gb + rb[r8 & 3] + 16 * L * r8);
+            gsync<WPP>();
+            dft_small<8>(v);
+            {
+                const int A = 8 * t + (t & 7);   // cidx(8t + r) = A ^ r
+#pragma unroll
+                for (int r8 = 0; r8 < 8; ++r8) Cb[A ^ r8] = v[r8];
+            }
+            gsync<WPP>();
+            if (IC_CL_PROBE != 3) p2_fft<M, L, C::LG, 3, 8, M, float>(Cb, (const float *)nullptr, 0.0, tw, t);
+            // spectrum in conjugate bin pairs (k_diag_p2).  No NaN bookkeeping:
+            // a finite f32 sum s32 means every X is finite, and then every d,
+            // Z and |X_k|^2 is finite (|X_k|^2 < 1e85); a non-finite s32 (a NaN or
+            // Inf sample, or an f32 overflow: d = -Inf) makes some bin NaN in
+            // any FFT order, so numpy's max|rfft| is NaN (ic.py:210-212)
+            constexpr int H = M / 2;
+            constexpr int JF = H / L;
+            double best2 = 0.0;
+            auto post = [&](const double2 zk, const double2 zm, const double2 wv) {
+                const double er = zk.x + zm.x, ei = zk.y - zm.y;
+                const double orr = zk.y + zm.y, oi = zm.x - zk.x;
+                const double tr = __builtin_fma(orr, wv.x, -(oi * wv.y));
+                const double ti = __builtin_fma(orr, wv.y, oi * wv.x);
+                const double re = er + tr, im = ei + ti;
+                const double rm = er - tr, imm = ti - ei;
+                const double a2 = __builtin_fma(re, re, im * im);
+                const double b2 = __builtin_fma(rm, rm, imm * imm);
+                best2 = fmax(best2, fmax(a2, b2));
+            };
+#pragma unroll
+            for (int j = 0; j < JF; ++j) {
+                const int kk = t + L * j;
+                const double2 zk = Cb[cidx(t) + L * j];
+                const double2 zm = Cb[kk == 0 ? 0 : cidx(L - t) + (M - L * (j + 1))];
+                post(zk, zm, tw[kk]);
+            }
+            {
+                // the self-paired bin k = M/2 (one task): post(Z, Z, w) with the
+                // exact zeros ei = oi = 0 of a finite Z folded in, on every lane
+                const double2 z = Cb[cidx(H)], wv = tw[H];
+                const double er = z.x + z.x, orr = z.y + z.y;
+                const double tr = orr * wv.x, ti = orr * wv.y;
+                const double re = er + tr, rm = er - tr, q2 = ti * ti;
+                best2 = fmax(best2, fmax(__builtin_fma(re, re, q2), __builtin_fma(rm, rm, q2)));
+            }
+            best2 = group_tree<WPP, 64>(best2, OpMaxF(), red + 44, wave, lane);
+            fftv = isfinite(s32) ? 0.5 * sqrt(best2) : (double)NAN;
+        } else {
+            // invalid: rfft of f64(X) = +-0 -> 0, unless R was non-finite (X NaN)
+            int nanx = 0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) nanx |= isnan(X[q]);
             nanx = group_tree<WPP, 64>(nanx, OpOr(), (int *)(red + 52), wave, lane);
             fftv = nanx ? NAN : 0.0;
         }
@@ -3740,9 +4223,9 @@ hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, in
 }
 
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
-                           double *T64)
+                           double *T64, double *T2)
 {
-    hipLaunchKernelGGL(k_tscrunch, dim3(cdiv(nbin, 64)), dim3(64), 0, st, F, wf, nsub, nbin, T, T64);
+    hipLaunchKernelGGL(k_tscrunch, dim3(cdiv(nbin, 64)), dim3(64), 0, st, F, wf, nsub, nbin, T, T64, T2);
     return hipGetLastError();
 }
 
@@ -3752,9 +4235,16 @@ hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P)
     return hipGetLastError();
 }
 
+hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double *T64, int nbin)
+{
+    const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
+    hipLaunchKernelGGL(k_fit_prep, dim3(1), dim3(64), 0, st, T64, nbin, nsw, S.U);
+    return hipGetLastError();
+}
+
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const int32_t *nlist, long bound,
-                           const FitStateArrays &S)
+                           const FitStateArrays &S, const int32_t *nlistB)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
@@ -3762,19 +4252,23 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
     // stride ldD may be longer (padding off the power-of-two stride)
     const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
     if (ldD % 4 != 0 || ldD < nsw || (dtiled && ldD % 32 != 0)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_fit_pass, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled, list,
-                       nlist, S);
+    if (!list)
+        hipLaunchKernelGGL(k_fit_pass<true>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled,
+                           list, nlist, (const int32_t *)nullptr, S, (const double *)S.U);
+    else
+        hipLaunchKernelGGL(k_fit_pass<false>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw,
+                           dtiled, list, nlist, nlistB, S, (const double *)nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
-                            unsigned long long *ctr, int32_t *host_n)
+                            unsigned long long *ctr, int32_t *host_n, const int32_t *nlistB, unsigned *ctrB)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nlist, amp,
-                       info, next_list, ctr, host_n);
+    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nlist,
+                       nlistB, amp, info, next_list, ctr, list ? nullptr : ctrB, host_n);
     return hipGetLastError();
 }
 
@@ -3810,6 +4304,30 @@ static hipError_t launch_p2(hipStream_t st, const DiagArgs &a, size_t P)
     return hipGetLastError();
 }
 
+template <int NN>
+static hipError_t launch_cl(hipStream_t st, const DiagArgs &a, size_t P)
+{
+    using C = CLay<NN>;
+    const int gpb = C::GPB;
+    const size_t shm = (size_t)C::TW_LDS * 16 + gpb * (size_t)C::GROUP_BYTES;
+    const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
+    if (a.mode == DIAG_EXACT)
+        hipLaunchKernelGGL((k_diag_cl<NN, DIAG_EXACT>), dim3(grid), dim3(C::L * gpb), shm, st, a);
+    else
+        hipLaunchKernelGGL((k_diag_cl<NN, DIAG_CLOSED>), dim3(grid), dim3(C::L * gpb), shm, st, a);
+    return hipGetLastError();
+}
+
+// IC_DIAG_CL=0 (read once): the row-layout k_diag_p2 for every nbin (A/B knob)
+static bool diag_cl_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("IC_DIAG_CL");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
 {
     const int nbin = a.nbin;
@@ -3819,6 +4337,13 @@ hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
                               : (!a.D || a.ldD < nbin || (a.mode != DIAG_STATS && (!a.amp || !a.info)) ||
                                  (a.mode == DIAG_FIT && !a.TT)))
         return hipErrorInvalidValue;
+    // the chain-layout kernel: exact / closed modes from the raw cube, f32 data, no pulse region
+    if ((a.mode == DIAG_EXACT || a.mode == DIAG_CLOSED) && a.T2 && a.raw && a.base && !a.pr_on && !a.data_f64 &&
+        diag_cl_enabled()) {
+        if (nbin == 1024) return launch_cl<1024>(st, a, P);
+        if (nbin == 2048) return launch_cl<2048>(st, a, P);
+        if (nbin == 4096) return launch_cl<4096>(st, a, P);
+    }
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
         if (a.data_f64 && a.mode != DIAG_FIT) return launch_p2<NN, true>(st, a, P);                \
@@ -3864,6 +4389,16 @@ static int env_knob(const char *name, int dflt)
     return (e && *e) ? atoi(e) : dflt;
 }
 
+void linestats_knobs(LineStatsArgs &a)
+{
+    a.grp_waves = env_knob("IC_LS_GRP", 8);
+    a.grp_minlen = env_knob("IC_LS_GRP_MINLEN", 1024);
+    if (a.grp_waves != 0 && a.grp_waves != 4 && a.grp_waves != 8) {
+        fprintf(stderr, "iterative_cleaner: IC_LS_GRP=%d unsupported (0, 4 or 8); using 8\n", a.grp_waves);
+        a.grp_waves = 8;
+    }
+}
+
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
 {
     // columns (length nsub), then rows (length nchan); wave-private LDS:
@@ -3873,10 +4408,10 @@ hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
         const int len = rows ? a.nchan : a.nsub;
         const int lines = 4 * (rows ? a.nsub : a.nchan);
         if (lines == 0 || len == 0) continue;
-        // few long lines (the rows): W waves per line (IC_LS_GRP = W in {0, 4, 8},
-        // 0 = one wave per line; IC_LS_GRP_MINLEN = the shortest line it takes)
-        if (lines < 8192 && len >= env_knob("IC_LS_GRP_MINLEN", 1024)) {
-            const int W = env_knob("IC_LS_GRP", 8);
+        // few long lines (the rows): W waves per line (a.grp_waves = W in {0, 4, 8},
+        // 0 = one wave per line; a.grp_minlen = the shortest line it takes)
+        if (lines < 8192 && len >= a.grp_minlen) {
+            const int W = a.grp_waves;
             if (W == 4 || W == 8) {
                 const int seg = (((len + W - 1) / W) + 63) & ~63;
                 const size_t gshm = 1024 + 16 * (size_t)W + (size_t)W * seg * 8;

@@ -10,8 +10,10 @@
 #include <stdarg.h>
 #include <stdlib.h>
 #include <stdio.h>
+#include <sched.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -104,7 +106,8 @@ struct Session {
     uint8_t *valid = nullptr;
     int32_t *shift = nullptr, *win = nullptr, *wflag = nullptr, *info = nullptr, *counters = nullptr;
     double *part = nullptr, *part2 = nullptr, *wpart = nullptr, *T64 = nullptr, *amp = nullptr, *std_ = nullptr,
-           *mean = nullptr, *fft = nullptr, *test = nullptr, *lstat = nullptr, *TT = nullptr;
+           *mean = nullptr, *fft = nullptr, *test = nullptr, *lstat = nullptr, *TT = nullptr,
+           *T2 = nullptr;   // [2 nbin]: the template twice (k_diag_cl)
     double2 *tw = nullptr, *tw_p2 = nullptr;
     PwPlan *plan = nullptr;
     FitStateArrays fs{};
@@ -118,6 +121,7 @@ struct Session {
     void *fs_block = nullptr;   // one allocation backing fs
     int fit_rounds = 0;
     int plan_ub = 0;            // max(leaves, ops) of the pairwise plan (k_tnorm scratch)
+    LineStatsArgs ls_knobs;     // row-median form, from the environment at creation
     long tail_threshold = kTailProfiles;
     ic_run_stats stats{};
     std::vector<int32_t> bad_fits;   // per iteration of the last run: fit statuses outside 1-4
@@ -201,15 +205,44 @@ static hipError_t take_event(Session *s, hipEvent_t *e)
     return hipSuccess;
 }
 
-// wait for the stream by polling an event (the blocking wait's wake-up cost
-// ~0.1 ms per iteration boundary on the MI355X hosts)
+// Wait for an event by polling it (the blocking wait's wake-up cost ~0.1 ms
+// per iteration boundary on the MI355X hosts): a busy poll for the first
+// 200 us (the common case: the GPU is a few kernels behind), then polls with
+// sched_yield between them, so a long wait does not hold a host core; after
+// IC_SYNC_TIMEOUT seconds (default 600) it gives up with hipErrorLaunchTimeOut,
+// so a kernel that never finishes fails the run instead of hanging its caller.
+static double sync_timeout_s()
+{
+    static const double t = [] {
+        const char *e = getenv("IC_SYNC_TIMEOUT");
+        const double v = (e && *e) ? atof(e) : 600.0;
+        return v > 0.0 ? v : 600.0;
+    }();
+    return t;
+}
+
+static hipError_t poll_event(hipEvent_t ev)
+{
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const auto spin = std::chrono::microseconds(200);
+    const auto limit = std::chrono::duration<double>(sync_timeout_s());
+    hipError_t e;
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+        const auto dt = clk::now() - t0;
+        if (dt > spin) {
+            if (dt > limit) return hipErrorLaunchTimeOut;
+            sched_yield();
+        }
+    }
+    return e;
+}
+
 static hipError_t spin_sync(Session *s)
 {
     hipError_t e = hipEventRecord(s->sev, s->stream);
     if (e != hipSuccess) return e;
-    while ((e = hipEventQuery(s->sev)) == hipErrorNotReady) {
-    }
-    return e;
+    return poll_event(s->sev);
 }
 
 #define LAUNCH(S, KID, CALL)                                                   \
@@ -285,7 +318,7 @@ void free_all(Session *s)
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
-                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph};
+                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph, s->T2, s->fs.U};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     void *rbufs[] = {s->std_r, s->mean_r, s->fft_r, s->ptp_r, s->valid_r};
@@ -432,7 +465,7 @@ int scrunch_stage(Session *s)
         LAUNCH(s, K_SHARD_PACK, launch_unpack_fscrunch(s->stream, s->geom, s->rows_pad, s->fg_blk, nbin, s->xfg_recv,
                                                        s->F, s->wf));
     }
-    LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64));
+    LAUNCH(s, K_TSCRUNCH, launch_tscrunch(s->stream, s->F, s->wf, nsub, nbin, s->T, s->T64, s->T2));
     return 0;
 }
 
@@ -603,6 +636,8 @@ int shard_rowstats(Session *s, const LineStatsArgs &la)
     lr.fft_d = s->fft_r;
     lr.ptp_d = s->ptp_r;
     lr.ptp_f32 = la.ptp_f32;
+    lr.grp_waves = la.grp_waves;
+    lr.grp_minlen = la.grp_minlen;
     lr.col_med = lr.col_mad = nullptr;
     lr.row_med = s->xr_send;
     lr.row_mad = s->xr_send + 4 * s->rows_own;
@@ -625,11 +660,14 @@ int run_fit(Session *s)
     const long P = (long)s->P;
     const int nbin = s->p.nbin;
     CK(launch_fit_init(s->stream, s->fs, P));
+    CK(launch_fit_prep(s->stream, s->fs, s->T64, nbin));
     // per round: blocks done << 32 | survivors; then the tail's sweep counter,
     // which accumulates over the run (zeroed and read once per run by ic_run)
     CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * 2 * kMaxRounds, s->stream));
     unsigned long long *ctr = (unsigned long long *)s->rcount;
     unsigned long long *tail_sweeps = ctr + kMaxRounds;
+    unsigned *ctrB = (unsigned *)(ctr + kMaxRounds + 1);   // round 0's unanswered B requests
+    CK(hipMemsetAsync(ctrB, 0, sizeof(unsigned long long), s->stream));
     int32_t *bufs[2] = {s->lists, s->lists + P};
     const int32_t *cur = nullptr, *cin = nullptr;   // round 0: all profiles
     long bound = P;                                 // >= the active count of the next round
@@ -644,21 +682,20 @@ int run_fit(Session *s)
             break;
         }
         int32_t *next = bufs[r & 1];
+        // round 1's list has round 0's unanswered B requests at its end (RoundList)
+        const int32_t *cinB = r == 1 ? (const int32_t *)ctrB : nullptr;
         LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
-                                                s->fs));
+                                                s->fs, cinB));
         s->h_rcount[r] = -1;
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
-                                                ctr + r, s->d_h_rcount + r));
+                                                ctr + r, s->d_h_rcount + r, cinB, ctrB));
         CK(hipEventRecord(s->rev[r & 1], s->stream));
         ++rounds;
         cur = next;
         cin = (const int32_t *)(ctr + r);   // low word: the survivor count
         if (r >= 1) {
             // count after round r-1 (= input of round r) bounds the count after round r
-            hipError_t qe;
-            while ((qe = hipEventQuery(s->rev[(r - 1) & 1])) == hipErrorNotReady) {
-            }
-            CK(qe);
+            CK(poll_event(s->rev[(r - 1) & 1]));
             const long c = s->h_rcount[r - 1];
             if (c == 0) break;   // round r had nothing to do
             bound = c;
@@ -742,6 +779,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(IC_EHIP, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
     Session *s = new Session();
+    linestats_knobs(s->ls_knobs);
     s->p = p;
     s->device = device;
     s->rank = rank;
@@ -843,6 +881,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->T64, (size_t)s->ldD);
     if (hipMemset(s->T64, 0, sizeof(double) * s->ldD) != hipSuccess)
         return bail(fail(IC_EHIP, "hipMemset(T64) failed"));   // zero tail: padded samples are no-ops
+    AL(s->T2, (size_t)2 * nbin);
     AL(s->amp, P);
     AL(s->info, P);
     AL(s->std_, P);
@@ -856,7 +895,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     if (exact) AL(s->lists, 2 * P);
-    AL(s->rcount, (size_t)2 * kMaxRounds + 2);
+    AL(s->rcount, (size_t)2 * kMaxRounds + 4);   // + tail sweeps (u64) + round 0's B count (u64)
     if (sharded) {
         const char *cerr = nullptr;
         s->comm = make_comm(&cerr);
@@ -936,6 +975,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         for (auto *q : dp) { *q = (double *)b; b += dstride; }
         int32_t **ip[] = {&s->fs.iter, &s->fs.nfev, &s->fs.mode, &s->fs.slow, &s->fs.o_exact};
         for (auto *q : ip) { *q = (int32_t *)b; b += istride; }
+        // k_fit_prep's 4 scalars
+        if (dalloc(&s->fs.U, 8) != hipSuccess) return bail(fail(IC_ENOMEM, "hipMalloc(fit prep) failed"));
     }
     // twiddles exp(-2 pi i q / n) and the pairwise plan
     std::vector<double2> tw(nbin);
@@ -1177,6 +1218,7 @@ DiagArgs diag_args(Session *s, int pr_start, int pr_end)
     a.raw = s->raw;
     a.base = s->base0;
     a.T64 = s->T64;
+    a.T2 = s->T2;
     a.TT = s->TT;
     a.amp = s->amp;
     a.info = s->info;
@@ -1217,6 +1259,10 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         s->ran = false;
     }
     if (!s->uploaded) return fail(IC_ESTATE, "ic_run before ic_upload");
+    // timed launches of earlier runs: fold them into the totals so the event
+    // pool stays at one run's worth (the previous run ended synchronised)
+    if (s->events.size() > 4096)
+        if (int rc = collect_timing(s)) return rc;
     if (s->fftded && !s->delays_set) return fail(IC_ESTATE, "ic_run before ic_set_delays (dedisp_mode FFT)");
     const ic_params &p = s->p;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
@@ -1234,6 +1280,8 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     la.fft_d = s->fft;
     la.ptp_d = s->ptp;
     la.ptp_f32 = !p.data_f64;
+    la.grp_waves = s->ls_knobs.grp_waves;
+    la.grp_minlen = s->ls_knobs.grp_minlen;
     la.col_med = s->lstat;
     la.col_mad = s->lstat + 4 * nchan;
     la.row_med = s->lstat + 8 * nchan;
@@ -1582,6 +1630,7 @@ int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const floa
     la.fft_d = ff;
     la.ptp_d = pt;
     la.ptp_f32 = 1;
+    linestats_knobs(la);
     la.col_med = lstat;
     la.col_mad = lstat + 4 * nchan;
     la.row_med = lstat + 8 * nchan;
@@ -1631,6 +1680,8 @@ int ic_fit_profiles(int device, int nprof, int nbin, const float *T, const float
     std::vector<double> t64(s->ldD, 0.0);
     for (int i = 0; i < nbin; ++i) t64[i] = (double)T[i];
     CK(hipMemcpyAsync(s->T64, t64.data(), sizeof(double) * s->ldD, hipMemcpyHostToDevice, s->stream));
+    CK(hipMemcpyAsync(s->T2, t64.data(), sizeof(double) * nbin, hipMemcpyHostToDevice, s->stream));
+    CK(hipMemcpyAsync(s->T2 + nbin, t64.data(), sizeof(double) * nbin, hipMemcpyHostToDevice, s->stream));
     CK(hipMemsetAsync(s->shift, 0, sizeof(int32_t) * s->nchan, s->stream));
     CK(hipMemsetAsync(s->base0, 0, sizeof(float) * P, s->stream));
     {

@@ -303,7 +303,15 @@ def load(path: str, channels=None):
         delay = 4.148808e3 * dm * (freqs ** -2 - cfreq ** -2)
         shift = np.rint(delay / period * nbin).astype(np.int64) % nbin
         if fractional_dedispersion():
-            frac = delay / period * nbin
+            from . import phase_rotation
+            if phase_rotation.is_supported(nbin) and 64 <= nbin <= 4096:
+                frac = delay / period * nbin
+            else:
+                # the rotation kernels take power-of-two nbin in 64..4096: keep the
+                # integer shift for this archive rather than fail its load / session
+                import warnings
+                warnings.warn("IC_DEDISPERSION=fft: nbin=%d is not a power of two in 64..4096; "
+                              "%s is dedispersed by the integer shift" % (nbin, path))
     else:
         shift = np.zeros(nchan, np.int64)
     mjd0 = float(primary.get("STT_IMJD", 60000)) + (float(primary.get("STT_SMJD", 0))

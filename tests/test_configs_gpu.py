@@ -3,7 +3,8 @@ in HBM exactly as bench.py does (bench.make_cube_device /
 make_block_cube_device):
 
 * C3  1024 x 8192 x 1024 (34 GB): determinism, 8 in-process channel shards
-  bit-equal to the single session, sampled-subint oracle checks of the exact
+  bit-equal to the single session, the final template against the oracle's
+  (whole archive), sampled-subint oracle checks of the exact
   fit and the diagnostics, whole-archive oracle test values and weights;
 * C4  128 x 1024 x 512 archives through batch.clean_batch (one lane and two):
   every archive bit-equal to its own single session, oracle stage checks on one;
@@ -74,6 +75,18 @@ def c3():
     with _native.GpuSession(nsub, nchan, nbin, device=0) as s:
         s.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
         outs = [_details(s), _details(s)]
+    # the weights the final template was built from (iteration k-1's, ic.py:88-94):
+    # the same loop stopped one iteration earlier
+    k = outs[0]["n_iter"]
+    if k == 1:
+        w_prev = w0.cpu().numpy()
+    elif outs[0]["changed"][-1] == 0:
+        w_prev = outs[0]["weights"]
+    else:
+        with _native.GpuSession(nsub, nchan, nbin, max_iter=k - 1, device=0) as s:
+            s.upload_device(cube.data_ptr(), w0.data_ptr(), shift.data_ptr())
+            w_prev = s.run()["weights"]
+    outs[0]["w_prev"] = w_prev
     host = (cube.cpu().numpy(), w0.cpu().numpy(), shift.cpu().numpy().astype(np.int64))
     del cube, w0, shift
     torch.cuda.empty_cache()
@@ -95,6 +108,14 @@ def test_c3_eight_channel_shards(c3):
     assert out["loops"] == one["loops"] and np.array_equal(out["changed"], one["changed"])
     for key in ("weights", "test", "amp", "info", "std", "mean", "ptp", "fft", "T"):
         assert bits_equal(out[key], one[key]), key
+
+
+def test_c3_template(c3, oracle_lib):
+    """The final template against the oracle's, whole archive: 32 channel
+    super-blocks, the deepest canonical channel tree of the configs
+    (tests/test_fullsize_gpu.py does the same for C2)."""
+    (raw, w0, shift), (one, _) = c3
+    assert bits_equal(oracle_lib.template(raw, one["w_prev"], shift), one["T"])
 
 
 def test_c3_sampled_subints_and_test_values(c3, oracle_lib):

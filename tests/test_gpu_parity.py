@@ -80,6 +80,35 @@ def test_loop_matches_reference(path, fit_mode):
 
 
 @pytest.mark.parametrize("path", clean_fixtures(), ids=lambda p: os.path.basename(p)[6:-4])
+def test_every_iteration_matches_reference(path):
+    """Iterations 1 .. n_iter-1 of the reference's loop, stage by stage: a
+    session stopped at max_iter = k holds iteration k's template (ic.py:94),
+    leastsq amplitudes and status (:278), diagnostics (:206-217), test values
+    (:225) and weights (:125), which must equal the fixture's *_k records
+    (test_loop_matches_reference checks the last iteration)."""
+    z, meta, raw, w0, shift, args = load_clean_case(path)
+    nit = int(z["n_iter"])
+    for k in range(1, nit):
+        a = dict(args, max_iter=k)
+        with _session(raw.shape, a, data_f64=meta.get("data_f64", False), delay=case_delay(z, meta)) as s:
+            s.upload(raw, w0, shift)
+            out = s.run()
+            T = s.template()
+            amp, info = s.fit()
+            sd, mn, pt, ff = s.diagnostics()
+        assert out["n_iter"] == k
+        assert bits_equal(T, z["T_%d" % k]), "template, iteration %d" % k
+        assert bits_equal(amp.ravel(), z["amp_%d" % k]), "leastsq amplitudes, iteration %d" % k
+        assert bits_equal(info.ravel(), z["info_%d" % k]), "leastsq status, iteration %d" % k
+        assert bits_equal(sd, z["diag_std_%d" % k]), "std, iteration %d" % k
+        assert bits_equal(mn, z["diag_mean_%d" % k]), "mean, iteration %d" % k
+        assert bits_equal(pt, z["diag_ptp_%d" % k]), "ptp, iteration %d" % k
+        assert _close_fft(ff, z["diag_fft_%d" % k]), "fftmax, iteration %d" % k
+        assert _close_test(out["test"], z["test_%d" % k]), "test, iteration %d" % k
+        assert bits_equal(out["weights"], z["weights_%d" % k]), "weights, iteration %d" % k
+
+
+@pytest.mark.parametrize("path", clean_fixtures(), ids=lambda p: os.path.basename(p)[6:-4])
 def test_clean_stdout_matches_reference(path, tmp_path, monkeypatch, capsys):
     """clean() prints exactly what the reference printed (ic.py:82-145)."""
     from iterative_cleaner_amd import archive as ica

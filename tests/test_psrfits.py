@@ -83,3 +83,21 @@ def test_npz_archives_stay_npz(tmp_path):
     ar.unload(p)
     assert not psrfits.is_psrfits(p)
     assert os.path.getsize(p) > 0 and ica.Archive_load(p).get_data().shape == (2, 1, 4, 8)
+
+
+@pytest.mark.parametrize("nbin", [100, 32])
+def test_fft_dedispersion_falls_back_for_unsupported_nbin(tmp_path, monkeypatch, nbin):
+    """IC_DEDISPERSION=fft with a profile length the rotation kernels do not take
+    (not a power of two in 64..4096): the archive still loads, with the integer
+    shift and a warning, instead of failing the load or the GPU session."""
+    ar = synth.make_archive(2, 8, nbin, seed=4)
+    ar._dm, ar._period = 30.0, 0.05
+    ar._chan_freqs = 1400.0 + np.arange(8) * 10.0 - 35.0
+    p = str(tmp_path / "u.fits")
+    psrfits.save(ar, p, stand_in_meta=False)
+    monkeypatch.setenv("IC_DEDISPERSION", "fft")
+    with pytest.warns(UserWarning, match="integer shift"):
+        br = psrfits.load(p)
+    delay = 4.148808e3 * 30.0 * (ar._chan_freqs ** -2 - 1400.0 ** -2)
+    assert np.array_equal(br.get_dm_shift(), np.rint(delay / 0.05 * nbin).astype(np.int64) % nbin)
+    assert br.get_dm_delay() is None
