@@ -279,6 +279,38 @@ def fast_mode_summary(_native, cube, w0, shift, shape, device, steps, torch, del
                     "mode, not the reference's leastsq arithmetic"}
 
 
+EXCHANGE_KINDS = ("allgather", "alltoallv", "allreduce")
+
+
+def per_rank_report(ktimes, exch, rank, world, dev):
+    """One clean's compute and exchange time on every rank (channel shards),
+    gathered to every rank as a tensor: [{rank, world_size_seen (the process
+    group's), compute_ms (the shard kernels), exchange_ms / calls / MB per
+    collective type}], so that a multi-GPU line shows where each rank's time
+    went."""
+    import torch
+    import torch.distributed as dist
+    ws = dist.get_world_size() if dist.is_initialized() else 1
+    compute = sum(v["ms"] for k, v in ktimes.items() if k.startswith("k_"))
+    row = [float(rank), float(ws), compute]
+    for kind in EXCHANGE_KINDS:
+        e = exch.get(kind, {"ms": 0.0, "calls": 0, "bytes": 0})
+        row += [e["ms"], float(e["calls"]), e["bytes"] / 1e6]
+    t = torch.tensor(row, dtype=torch.float64, device=dev if dist.get_backend() != "gloo" else "cpu")
+    rows = [t] if world == 1 else [torch.empty_like(t) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(rows, t)
+    out = []
+    for r in rows:
+        v = r.cpu().tolist()
+        rec = {"rank": int(v[0]), "world_size_seen": int(v[1]), "compute_ms": round(v[2], 3), "exchange": {}}
+        for i, kind in enumerate(EXCHANGE_KINDS):
+            ms, calls, mb = v[3 + 3 * i: 6 + 3 * i]
+            rec["exchange"][kind] = {"ms": round(ms, 3), "calls": int(calls), "MB": round(mb, 3)}
+        out.append(rec)
+    return out
+
+
 def batch_main(a, workload, rank, world, local, dev):
     """C4: every rank cleans `--batch` archives per step from page-locked host
     memory through the batch pipeline (iterative_cleaner_amd/batch.py); three
@@ -458,10 +490,16 @@ def main():
     # roofline prices.
     ktimes_all = {}
     dom = None
+    rank_report = None
     if not a.untimed_kernels:
         sess.set_timing(True)
+        if sharded:
+            comm.timing = True
         sess.run(fetch=False)
         ktimes_all = sess.kernel_times()
+        if sharded:
+            comm.timing = False
+            rank_report = per_rank_report(ktimes_all, comm.exchange_report(), rank, world, dev)
         kk = {k: v for k, v in ktimes_all.items() if k.startswith("k_") and v["launches"]}
         dom = max(kk, key=lambda k: kk[k]["ms"])
         sess.set_timing(True, only=dom)
@@ -614,6 +652,8 @@ def main():
             rec["fast_mode"] = fast
         if "exchange" in ktimes and ktimes["exchange"]["launches"]:
             rec["config"]["exchange_ms_per_step"] = round(ktimes["exchange"]["ms"] / a.steps, 3)
+        if rank_report is not None:
+            rec["config"]["per_rank"] = rank_report
         if world == 1 and not a.no_cpu_baseline:
             try:
                 rec["cpu_baseline"] = cpu_baseline(nchan, nbin, seed, rfi, a.cpu_budget)

@@ -165,26 +165,25 @@ hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, in
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
                            double *T64, double *T2 = nullptr);
 hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
-// S.U from the template (one thread; before round 0 of every fit)
+// S.U from the template (one block; before round 0 of every fit)
 hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double *T64, int nbin);
-// list == nullptr: all P profiles; else list[0 .. *nlist) with *nlist <= bound
-// (the host sizes grids from a count it already knows: counts only shrink).
-// nlistB (the round after round 0 only): count of round 0's unanswered B
-// requests, stored from the end of the P-entry list down (k_fit_state's ctrB)
+// list == nullptr: all P profiles (round 0); else the list written by the
+// previous round's k_fit_state, partitioned by request: nctr -> its packed
+// counts ([47:24] B requests at the list's end, [23:0] A requests at its
+// front), their sum <= bound (the host sizes grids from a count it already
+// knows: counts only shrink).
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           int dtiled, const int32_t *list, const int32_t *nlist, long bound,
-                           const FitStateArrays &S, const int32_t *nlistB = nullptr);
-// ctr: zeroed device counter, finished blocks << 32 | survivors (its low word,
-// little-endian, is the next round's list length); host_n: host-mapped int the
-// last block writes the final count to
-// ctrB (zeroed; used in round 0 only): see launch_fit_pass's nlistB
+                           int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
+                           const FitStateArrays &S);
+// ctr: zeroed device word, packed [63:48] finished blocks, [47:24] B survivors,
+// [23:0] A survivors (the next round's nctr); host_n: host-mapped int the
+// last block writes the survivor total to
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
-                            const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
-                            unsigned long long *ctr, int32_t *host_n, const int32_t *nlistB = nullptr,
-                            unsigned *ctrB = nullptr);
+                            const unsigned long long *nctr, long bound, double *amp, int32_t *info,
+                            int32_t *next_list, unsigned long long *ctr, int32_t *host_n);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           int dtiled, const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
-                           double *amp, int32_t *info, unsigned long long *sweeps);
+                           int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
+                           const FitStateArrays &S, double *amp, int32_t *info, unsigned long long *sweeps);
 // Diagnostics kernels (k_diag_p2<N> for power-of-two nbin 64..4096, k_diag
 // otherwise).  mode: DIAG_EXACT = residual from the exact fit's amp/info and
 // the fit cube D (row stride ldD); DIAG_CLOSED = fit_mode 1, the closed-form

@@ -1221,16 +1221,33 @@ __device__ __forceinline__ void lm_store(const LmState &L, const FitStateArrays 
     S.iter[k] = L.iter; S.nfev[k] = L.nfev;
 }
 
-// A round's input list: list[0 .. nA), then - in the round after round 0 only -
-// the B requests that round 0's first transitions could not answer (k_fit_pass
-// summed qtf's dot for the others), stored from the end of the list buffer
-// down (list[P - 1 - j], j < nB), so that A and B requests sit in separate
-// waves: a wave with both runs both sweep bodies.
+// A round's input list.  k_fit_state writes the survivors of a round into the
+// P-entry list buffer partitioned by request: A requests from the front
+// (list[0 .. nA)), B requests from the end down (list[P - 1 - j], j < nB), so
+// that the next round's waves hold one kind each (a wave with both runs both
+// sweep bodies; round 0's unanswered B requests and the profiles one stage
+// behind after them would otherwise spread over most waves).  Both counts and
+// the finished-block count share one 64-bit word (one atomic per block):
+// [63:48] blocks done, [47:24] nB, [23:0] nA (P < 2^24, checked by the host).
+__host__ __device__ constexpr unsigned long long rl_pack(unsigned long long blocks, unsigned long long nB,
+                                                         unsigned long long nA)
+{
+    return (blocks << 48) | (nB << 24) | nA;
+}
 struct RoundList {
     const int32_t *list;
     long nA, nB, P;
-    __device__ __forceinline__ RoundList(const int32_t *l, const int32_t *nlist, const int32_t *nlistB, long P_)
-        : list(l), nA(l ? (long)*nlist : P_), nB(l && nlistB ? (long)*nlistB : 0), P(P_) {}
+    __device__ __forceinline__ RoundList(const int32_t *l, const unsigned long long *ctr, long P_) : list(l), P(P_)
+    {
+        if (!l) {
+            nA = P_;
+            nB = 0;
+        } else {
+            const unsigned long long v = *ctr;
+            nA = (long)(v & 0xffffffull);
+            nB = (long)((v >> 24) & 0xffffffull);
+        }
+    }
     __device__ __forceinline__ long n() const { return nA + nB; }
     __device__ __forceinline__ long at(long s) const
     {
@@ -1261,33 +1278,6 @@ __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
 // has the same f_i: one full sweep of the fit cube less per iteration.  A
 // profile whose J differs anywhere (k_fit_pass checks J_i == T_i), or whose
 // own acnorm / aj / Jn0 differ, sends its B request as before.
-// One thread: U = {valid, acnorm, aj, Jn0} (k_fit_pass's round-0 form computes
-// Jn_i = RN(J_i / aj) itself, as the B sweep does).
-__global__ __launch_bounds__(64) void k_fit_prep(const double *__restrict__ T64, int nbin, int nsw,
-                                                 double *__restrict__ U)
-{
-    if (threadIdx.x != 0) return;
-    // MINPACK enorm over the sweep (k_fit_pass: agiant = RGIANT/nbin, padded zeros are no-ops)
-    Enorm e;
-    en_zero(e);
-    const double agiant = kRgiant / (double)nbin;
-    for (int i = 0; i < nsw; ++i) en_add(e, T64[i], agiant);
-    const double acn = en_fin(e);
-    const double J0 = T64[0];
-    double ajnorm = acn, Jn0 = J0;   // lm_outer
-    if (ajnorm != 0.0) {
-        if (J0 < 0.0) ajnorm = -ajnorm;
-        Jn0 = J0 / ajnorm;
-        Jn0 = Jn0 + 1.0;
-    }
-    // the fast B sweep's conditions on aj as well (x = 1 is in range)
-    const bool valid = acn != 0.0 && Jn0 != 0.0 && x_in_fast_range(ajnorm);
-    U[0] = valid ? 1.0 : 0.0;
-    U[1] = acn;
-    U[2] = valid ? ajnorm : 1.0;
-    U[3] = Jn0;
-}
-
 // R0: the round-0 form (list == nullptr, every request A at x = 1), which sums
 // the first B sweep's dot in the same sweep (k_fit_prep's U); a kernel of its
 // own so that the other rounds keep their register allocation (and occupancy)
@@ -1295,14 +1285,13 @@ template <bool R0>
 __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, const double *__restrict__ T64,
                                                  long P, int nbin, int ldD, int nsw, int dtiled,
                                                  const int32_t *__restrict__ list,
-                                                 const int32_t *__restrict__ nlist,
-                                                 const int32_t *__restrict__ nlistB, FitStateArrays S,
+                                                 const unsigned long long *__restrict__ nctr, FitStateArrays S,
                                                  const double *__restrict__ U)
 {
     __shared__ __attribute__((aligned(16))) char lbuf[2 * FIT_BUF];
     const int lane = threadIdx.x;
     const long slot = (long)blockIdx.x * 64 + lane;
-    const RoundList rl(list, nlist, nlistB, P);
+    const RoundList rl(list, nctr, P);
     const long nact = rl.n();   // the grid is only an upper bound
     if ((long)blockIdx.x * 64 >= nact) return;
     const bool in_range = slot < nact;
@@ -1413,22 +1402,18 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 #ifndef FIT_STATE_BS
 #define FIT_STATE_BS 512
 #endif
-// ctrB (round 0 only, list == nullptr): count of the unanswered B requests,
-// appended from the end of next_list down (RoundList).
 __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
-                                                            const int32_t *__restrict__ nlist,
-                                                            const int32_t *__restrict__ nlistB,
+                                                            const unsigned long long *__restrict__ nctr,
                                                             double *__restrict__ amp_o, int32_t *__restrict__ info_o,
                                                             int32_t *__restrict__ next_list,
-                                                            unsigned long long *__restrict__ ctr,
-                                                            unsigned *__restrict__ ctrB, int32_t *host_n)
+                                                            unsigned long long *__restrict__ ctr, int32_t *host_n)
 {
     __shared__ int wcnt[FIT_STATE_BS / 64];
     __shared__ int woff[FIT_STATE_BS / 64];
     __shared__ int wcntB[FIT_STATE_BS / 64];
     __shared__ int woffB[FIT_STATE_BS / 64];
     const long slot = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const RoundList rl(list, nlist, nlistB, P);
+    const RoundList rl(list, nctr, P);
     const long nact = rl.n();
     // the grid is sized from an upper bound: blocks past the list return at
     // once, and only the nblk blocks with work take part in the append (a
@@ -1461,7 +1446,7 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
                 amp_o[k] = L.x;
                 info_o[k] = L.info;
             } else {
-                still = 1;
+                still = st == ST_B ? 2 : 1;   // B requests go to the list's end
             }
         } else if (st == ST_A0) {
             // the first transition: the state is k_fit_init's (x = 1, par = 0,
@@ -1496,10 +1481,8 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             if (st == ST_DONE) {
                 amp_o[k] = L.x;
                 info_o[k] = L.info;
-            } else if (st == ST_B && ctrB) {
-                stillB = 1;   // round 0's unanswered B request: the other region
             } else {
-                still = 1;
+                still = st == ST_B ? 2 : 1;   // B requests go to the list's end
             }
         } else if (st != ST_DONE) {
             LmState L;
@@ -1518,14 +1501,15 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
                 amp_o[k] = L.x;
                 info_o[k] = L.info;
             } else {
-                still = 1;
+                still = st == ST_B ? 2 : 1;   // B requests go to the list's end
             }
         }
     }
-    // block-aggregated append
+    // block-aggregated append, partitioned by request (RoundList)
+    stillB = still == 2;
+    still = still == 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long m = __ballot(still);
-    const unsigned long long mB = ctrB ? __ballot(stillB) : 0ull;
+    const unsigned long long m = __ballot(still), mB = __ballot(stillB);
     if (lane == 0) {
         wcnt[wave] = __popcll(m);
         wcntB[wave] = __popcll(mB);
@@ -1537,29 +1521,17 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             tot += wcnt[w];
             totB += wcntB[w];
         }
-        if (ctrB) {
-            // the B region first, ordered before this block counts as finished
-            int baseB = totB ? (int)atomicAdd(ctrB, (unsigned)totB) : 0;
-            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-                woffB[w] = baseB;
-                baseB += wcntB[w];
-            }
-            __threadfence();
-        }
-        // one atomic per block: finished blocks in the high word, survivors in the low
-        const unsigned long long old = atomicAdd(ctr, (1ull << 32) | (unsigned long long)(unsigned)tot);
-        int base = (int)(uint32_t)old;
+        // one atomic per block: blocks done, B count, A count
+        const unsigned long long old = atomicAdd(ctr, rl_pack(1, (unsigned)totB, (unsigned)tot));
+        int base = (int)(old & 0xffffffull), baseB = (int)((old >> 24) & 0xffffffull);
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
             woff[w] = base;
             base += wcnt[w];
+            woffB[w] = baseB;
+            baseB += wcntB[w];
         }
-        if ((old >> 32) == (unsigned long long)nblk - 1) {   // last block with work: base is the final count
-            if (ctrB) {
-                __threadfence();
-                base += (int)__hip_atomic_load(ctrB, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __hip_atomic_store(host_n, base, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if ((old >> 48) == (unsigned long long)nblk - 1)   // last block with work: the final counts
+            __hip_atomic_store(host_n, base + baseB, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
     if (still) next_list[woff[wave] + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
@@ -1621,6 +1593,52 @@ __device__ __forceinline__ void seq_sums(const double *a, const double *b, int n
         s = s + a[q];
         if (TWO) t = t + b[q];
     }
+}
+
+// One block: U = {valid, acnorm, aj, Jn0} (k_fit_pass's round-0 form computes
+// Jn_i = RN(J_i / aj) itself, as the B sweep does).  MINPACK's enorm is a
+// sequential sum: every thread squares its samples into LDS and checks the
+// range, then one thread adds the squares in order (register blocks, the
+// next block's reads ahead of the adds) - sqrt(sum_seq t^2) is MINPACK's enorm
+// while every component is 0 or inside (RDWARF, agiant) (fa_add's argument);
+// MINPACK's branchy enorm otherwise.
+__global__ __launch_bounds__(256) void k_fit_prep(const double *__restrict__ T64, int nbin, int nsw,
+                                                  double *__restrict__ U)
+{
+    extern __shared__ double sq[];   // [nsw]
+    const double agiant = kRgiant / (double)nbin;
+    int ok = 1;
+    for (int i = threadIdx.x; i < nsw; i += blockDim.x) {
+        const double a = fabs(T64[i]);
+        ok &= (a == 0.0 || (a > kRdwarf && a < agiant)) ? 1 : 0;
+        sq[i] = a * a;
+    }
+    const bool in_range = __syncthreads_and(ok) != 0;
+    if (threadIdx.x != 0) return;
+    double acn;
+    if (in_range) {
+        double s2 = 0.0, unused = 0.0;
+        seq_sums<16, false>(sq, nullptr, nsw, s2, unused);
+        acn = s2 != 0.0 ? sqrt(s2) : 0.0;   // MINPACK: sqrt(s2 (1 + 0)) with no small / large components
+    } else {
+        Enorm e;
+        en_zero(e);
+        for (int i = 0; i < nsw; ++i) en_add(e, T64[i], agiant);
+        acn = en_fin(e);
+    }
+    const double J0 = T64[0];
+    double ajnorm = acn, Jn0 = J0;   // lm_outer
+    if (ajnorm != 0.0) {
+        if (J0 < 0.0) ajnorm = -ajnorm;
+        Jn0 = J0 / ajnorm;
+        Jn0 = Jn0 + 1.0;
+    }
+    // the fast B sweep's conditions on aj as well (x = 1 is in range)
+    const bool valid = acn != 0.0 && Jn0 != 0.0 && x_in_fast_range(ajnorm);
+    U[0] = valid ? 1.0 : 0.0;
+    U[1] = acn;
+    U[2] = valid ? ajnorm : 1.0;
+    U[3] = Jn0;
 }
 
 // one fit-cube row in either layout (d_ofs)
@@ -1733,7 +1751,8 @@ __device__ __forceinline__ double tail_sweep_b(const RowRef &p, const double *__
 __global__ __launch_bounds__(64 * TAIL_WAVES, IC_TAIL_MINW) void k_fit_tail(const float *__restrict__ D,
                                                               const double *__restrict__ T64, long P, int nbin,
                                                               int ldD, int dtiled, const int32_t *__restrict__ list,
-                                                              const int32_t *__restrict__ nlist, FitStateArrays S,
+                                                              const unsigned long long *__restrict__ nctr,
+                                                              FitStateArrays S,
                                                               double *__restrict__ amp_o,
                                                               int32_t *__restrict__ info_o,
                                                               unsigned long long *__restrict__ sweeps)
@@ -1741,11 +1760,12 @@ __global__ __launch_bounds__(64 * TAIL_WAVES, IC_TAIL_MINW) void k_fit_tail(cons
     __shared__ double sbuf[TAIL_WAVES][4][TAIL_CH];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double(*buf)[TAIL_CH] = sbuf[wave];
-    const long nact = list ? (long)*nlist : P;
+    const RoundList rl(list, nctr, P);
+    const long nact = rl.n();
     const double agiant = kRgiant / (double)nbin;
     unsigned long long nsw = 0;
     for (long slot = (long)blockIdx.x * TAIL_WAVES + wave; slot < nact; slot += (long)gridDim.x * TAIL_WAVES) {
-        const long k = list ? (long)list[slot] : slot;
+        const long k = rl.at(slot);
         int st = S.mode[k];
         if (st == ST_DONE) continue;
         LmState L;
@@ -4238,13 +4258,13 @@ hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P)
 hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double *T64, int nbin)
 {
     const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
-    hipLaunchKernelGGL(k_fit_prep, dim3(1), dim3(64), 0, st, T64, nbin, nsw, S.U);
+    hipLaunchKernelGGL(k_fit_prep, dim3(1), dim3(256), sizeof(double) * nsw, st, T64, nbin, nsw, S.U);
     return hipGetLastError();
 }
 
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           int dtiled, const int32_t *list, const int32_t *nlist, long bound,
-                           const FitStateArrays &S, const int32_t *nlistB)
+                           int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
+                           const FitStateArrays &S)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
@@ -4254,32 +4274,32 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
     if (ldD % 4 != 0 || ldD < nsw || (dtiled && ldD % 32 != 0)) return hipErrorInvalidValue;
     if (!list)
         hipLaunchKernelGGL(k_fit_pass<true>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled,
-                           list, nlist, (const int32_t *)nullptr, S, (const double *)S.U);
+                           list, nctr, S, (const double *)S.U);
     else
         hipLaunchKernelGGL(k_fit_pass<false>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw,
-                           dtiled, list, nlist, nlistB, S, (const double *)nullptr);
+                           dtiled, list, nctr, S, (const double *)nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
-                            const int32_t *nlist, long bound, double *amp, int32_t *info, int32_t *next_list,
-                            unsigned long long *ctr, int32_t *host_n, const int32_t *nlistB, unsigned *ctrB)
+                            const unsigned long long *nctr, long bound, double *amp, int32_t *info,
+                            int32_t *next_list, unsigned long long *ctr, int32_t *host_n)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nlist,
-                       nlistB, amp, info, next_list, ctr, list ? nullptr : ctrB, host_n);
+    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nctr, amp,
+                       info, next_list, ctr, host_n);
     return hipGetLastError();
 }
 
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                           int dtiled, const int32_t *list, const int32_t *nlist, long bound, const FitStateArrays &S,
-                           double *amp, int32_t *info, unsigned long long *sweeps)
+                           int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
+                           const FitStateArrays &S, double *amp, int32_t *info, unsigned long long *sweeps)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min<long>(cdiv(n, TAIL_WAVES), 65536);
-    hipLaunchKernelGGL(k_fit_tail, dim3(grid), dim3(64 * TAIL_WAVES), 0, st, D, T64, P, nbin, ldD, dtiled, list, nlist,
+    hipLaunchKernelGGL(k_fit_tail, dim3(grid), dim3(64 * TAIL_WAVES), 0, st, D, T64, P, nbin, ldD, dtiled, list, nctr,
                        S, amp, info, sweeps);
     return hipGetLastError();
 }

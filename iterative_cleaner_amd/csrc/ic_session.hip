@@ -666,10 +666,9 @@ int run_fit(Session *s)
     CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * 2 * kMaxRounds, s->stream));
     unsigned long long *ctr = (unsigned long long *)s->rcount;
     unsigned long long *tail_sweeps = ctr + kMaxRounds;
-    unsigned *ctrB = (unsigned *)(ctr + kMaxRounds + 1);   // round 0's unanswered B requests
-    CK(hipMemsetAsync(ctrB, 0, sizeof(unsigned long long), s->stream));
     int32_t *bufs[2] = {s->lists, s->lists + P};
-    const int32_t *cur = nullptr, *cin = nullptr;   // round 0: all profiles
+    const int32_t *cur = nullptr;                    // round 0: all profiles
+    const unsigned long long *cin = nullptr;         // the round's packed list counts (RoundList)
     long bound = P;                                 // >= the active count of the next round
     int rounds = 0;
     bool tail = false;
@@ -682,17 +681,15 @@ int run_fit(Session *s)
             break;
         }
         int32_t *next = bufs[r & 1];
-        // round 1's list has round 0's unanswered B requests at its end (RoundList)
-        const int32_t *cinB = r == 1 ? (const int32_t *)ctrB : nullptr;
         LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
-                                                s->fs, cinB));
+                                                s->fs));
         s->h_rcount[r] = -1;
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
-                                                ctr + r, s->d_h_rcount + r, cinB, ctrB));
+                                                ctr + r, s->d_h_rcount + r));
         CK(hipEventRecord(s->rev[r & 1], s->stream));
         ++rounds;
         cur = next;
-        cin = (const int32_t *)(ctr + r);   // low word: the survivor count
+        cin = ctr + r;   // packed A / B counts of the next round's list
         if (r >= 1) {
             // count after round r-1 (= input of round r) bounds the count after round r
             CK(poll_event(s->rev[(r - 1) & 1]));
@@ -780,6 +777,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
     Session *s = new Session();
     linestats_knobs(s->ls_knobs);
+    if (const char *e = getenv("IC_FIT_TAIL"))   // A/B knob: the tail hand-over threshold (ic_set_fit_tail)
+        if (*e) s->tail_threshold = atol(e);
     s->p = p;
     s->device = device;
     s->rank = rank;
@@ -834,6 +833,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     const size_t P = s->P, N = s->N;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
     const bool exact = p.fit_mode == IC_FIT_EXACT;
+    // the fit rounds' list counts are 24-bit fields of one packed word (RoundList)
+    if (exact && P >= (1u << 24))
+        return bail(fail(IC_EINVAL, "the exact fit takes < 2^24 profiles per session or shard (%zu)", P));
     AL(s->slot_raw[0], N);
     s->raw = s->slot_raw[0];
     // the closed-form fit reads the raw cube (no fit cube, no lmdif state), unless
@@ -895,7 +897,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     if (exact) AL(s->lists, 2 * P);
-    AL(s->rcount, (size_t)2 * kMaxRounds + 4);   // + tail sweeps (u64) + round 0's B count (u64)
+    AL(s->rcount, (size_t)2 * kMaxRounds + 2);   // + the tail's sweep counter (u64)
     if (sharded) {
         const char *cerr = nullptr;
         s->comm = make_comm(&cerr);

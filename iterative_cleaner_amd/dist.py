@@ -109,6 +109,10 @@ class TorchComm:
         self.fail_at = fail_at
         self.calls = 0
         self.aborted = False
+        # per-collective timing (bench.py's per-rank report): HIP events around
+        # each collective on the session stream while `timing` is set
+        self.timing = False
+        self._events = []
 
     def _count(self):
         self.calls += 1
@@ -160,10 +164,36 @@ class TorchComm:
     def _staged(self):
         return self.backend == "gloo" and self.device.type == "cuda"
 
+    def _timed(self, kind, nbytes, fn):
+        """Run fn() (inside the stream context); with timing on, bracket it by
+        events on the current (session) stream."""
+        if not (self.timing and self.device.type == "cuda"):
+            return fn()
+        cuda = self.torch.cuda
+        a, b = cuda.Event(enable_timing=True), cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        self._events.append((kind, int(nbytes), a, b))
+
+    def exchange_report(self):
+        """{collective: {"ms", "calls", "bytes"}} of the timed collectives since
+        the last report (synchronises on their events)."""
+        out = {}
+        for kind, nbytes, a, b in self._events:
+            b.synchronize()
+            r = out.setdefault(kind, {"ms": 0.0, "calls": 0, "bytes": 0})
+            r["ms"] += a.elapsed_time(b)
+            r["calls"] += 1
+            r["bytes"] += nbytes
+        self._events = []
+        return out
+
     def allgather(self, send, recv, stream=None):
         dist = self.dist
         self._count()
-        with self._stream_ctx(stream):
+
+        def run():
             if self._staged():
                 self.torch.cuda.current_stream(self.device).synchronize()
                 s_c, r_c = send.cpu(), recv.new_empty(recv.shape, device="cpu")
@@ -173,11 +203,14 @@ class TorchComm:
                 dist.all_gather(list(recv.chunk(self.world)), send, group=self.group)
             else:
                 dist.all_gather_into_tensor(recv, send, group=self.group)
+        with self._stream_ctx(stream):
+            self._timed("allgather", recv.numel() * recv.element_size(), run)
 
     def alltoallv(self, send, send_sizes, recv, recv_sizes, stream=None):
         dist = self.dist
         self._count()
-        with self._stream_ctx(stream):
+
+        def run():
             if self._staged():
                 self.torch.cuda.current_stream(self.device).synchronize()
                 s_c, r_c = send.cpu(), recv.new_empty(recv.shape, device="cpu")
@@ -185,11 +218,14 @@ class TorchComm:
                 recv.copy_(r_c)
             else:
                 dist.all_to_all_single(recv, send, list(recv_sizes), list(send_sizes), group=self.group)
+        with self._stream_ctx(stream):
+            self._timed("alltoallv", sum(send_sizes) * send.element_size(), run)
 
     def allreduce_sum(self, t, stream=None):
         dist = self.dist
         self._count()
-        with self._stream_ctx(stream):
+
+        def run():
             if self._staged():
                 self.torch.cuda.current_stream(self.device).synchronize()
                 c = t.cpu()
@@ -197,6 +233,8 @@ class TorchComm:
                 t.copy_(c)
             else:
                 dist.all_reduce(t, group=self.group)
+        with self._stream_ctx(stream):
+            self._timed("allreduce", t.numel() * t.element_size(), run)
 
     # ------------------------------------------------------------ C callbacks
     def ops(self):

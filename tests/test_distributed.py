@@ -152,3 +152,48 @@ def test_cpp_shard_layout_matches_python(nsub, nchan):
         assert _native.shard_layout(nsub, nchan, world) == want
     with pytest.raises(_native.NativeError):
         _native.shard_layout(nsub, nchan, 3)
+
+
+def _report_worker(rank, world, port, q):
+    import sys
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        ktimes = {"k_fit_pass": {"ms": 10.0 + rank, "launches": 30}, "k_diag": {"ms": 5.0, "launches": 3},
+                  "exchange": {"ms": 99.0, "launches": 7}}
+        exch = {"alltoallv": {"ms": 0.5 * (rank + 1), "calls": 6, "bytes": 8_000_000},
+                "allgather": {"ms": 0.25, "calls": 6, "bytes": 4_000_000}}
+        q.put((rank, bench.per_rank_report(ktimes, exch, rank, world, "cpu")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_per_rank_report_two_ranks():
+    """bench.py's multi-GPU line carries every rank's compute time, exchange
+    time per collective type and the world size its process group saw."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_report_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]                      # the same gathered table on every rank
+    table = res[0]
+    assert [r["rank"] for r in table] == [0, 1]
+    for r in table:
+        assert r["world_size_seen"] == 2
+        assert r["compute_ms"] == 15.0 + r["rank"]           # kernels only, not the exchange bucket
+        assert r["exchange"]["alltoallv"] == {"ms": 0.5 * (r["rank"] + 1), "calls": 6, "MB": 8.0}
+        assert r["exchange"]["allgather"]["calls"] == 6
+        assert r["exchange"]["allreduce"] == {"ms": 0.0, "calls": 0, "MB": 0.0}
