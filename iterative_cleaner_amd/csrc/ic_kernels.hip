@@ -4130,7 +4130,7 @@ hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, cons
     dim3 grid(cdiv(nbin, bs), nsb, nsub);
     if (mode == 3 && (!D || ldD < nbin || (dtiled && ldD % 32 != 0))) return hipErrorInvalidValue;
 #define IC_CP(M)                                                                                                  \
-    hipLaunchKernelGGL(k_chan_partials<M>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin, \
+    IC_GGL(k_chan_partials<M>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin, \
                        nsb, part, part2, wpart, D, ldD, dtiled)
     if (mode == 0)
         IC_CP(0);
@@ -4152,7 +4152,7 @@ hipError_t launch_window(hipStream_t st, const double *part, long ss, long sl, c
     if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
     const size_t shm = window_lds_bytes(nbin);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_window, dim3(nsub), dim3(kWindowThreads), shm, st, part, ss, sl, plan, nbin, width, win, flags);
+    IC_GGL(k_window, dim3(nsub), dim3(kWindowThreads), shm, st, part, ss, sl, plan, nbin, width, win, flags);
     return hipGetLastError();
 }
 
@@ -4161,13 +4161,13 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
 {
     const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 16), 16384);
-    hipLaunchKernelGGL(k_base, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
+    IC_GGL(k_base, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
     return hipGetLastError();
 }
 
 hipError_t launch_pscrunch(hipStream_t st, float *raw, const float *pol1, size_t n)
 {
-    hipLaunchKernelGGL(k_pscrunch, dim3(std::min<unsigned>(cdiv(n / 4 + 1, 256), 8192)), dim3(256), 0, st, raw, pol1, n);
+    IC_GGL(k_pscrunch, dim3(std::min<unsigned>(cdiv(n / 4 + 1, 256), 8192)), dim3(256), 0, st, raw, pol1, n);
     return hipGetLastError();
 }
 
@@ -4176,7 +4176,7 @@ hipError_t launch_fscrunch(hipStream_t st, const double *part, long ss, long sl,
 {
     if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
-    hipLaunchKernelGGL(k_fscrunch, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, ss, sl, wpart, wss, wsl, plan,
+    IC_GGL(k_fscrunch, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, ss, sl, wpart, wss, wsl, plan,
                        nbin, F, wf);
     return hipGetLastError();
 }
@@ -4187,14 +4187,14 @@ hipError_t launch_sb_tree(hipStream_t st, const double *part, const double *wpar
     if (plan.n < 1 || plan.n > kMaxSbLeaves) return hipErrorInvalidValue;
     if (ostr < nbin + (wpart ? 1 : 0)) return hipErrorInvalidValue;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
-    hipLaunchKernelGGL(k_sb_tree, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, wpart, plan, nbin, ostr, out);
+    IC_GGL(k_sb_tree, dim3(cdiv(nbin, bs), nsub), dim3(bs), 0, st, part, wpart, plan, nbin, ostr, out);
     return hipGetLastError();
 }
 
 hipError_t launch_unpack_windows(hipStream_t st, const ShardGeom &g, int blk, const int32_t *recv, int32_t *win,
                                  int32_t *flags)
 {
-    hipLaunchKernelGGL(k_unpack_windows, dim3(cdiv(g.nsub, 256)), dim3(256), 0, st, g, blk, recv, win, flags);
+    IC_GGL(k_unpack_windows, dim3(cdiv(g.nsub, 256)), dim3(256), 0, st, g, blk, recv, win, flags);
     return hipGetLastError();
 }
 
@@ -4202,7 +4202,7 @@ hipError_t launch_unpack_fscrunch(hipStream_t st, const ShardGeom &g, int rows_p
                                   const float *recv, float *F, float *wf)
 {
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
-    hipLaunchKernelGGL(k_unpack_fscrunch, dim3(cdiv(nbin, bs), g.nsub), dim3(bs), 0, st, g, rows_pad, blk, nbin,
+    IC_GGL(k_unpack_fscrunch, dim3(cdiv(nbin, bs), g.nsub), dim3(bs), 0, st, g, rows_pad, blk, nbin,
                        recv, F, wf);
     return hipGetLastError();
 }
@@ -4213,7 +4213,7 @@ hipError_t launch_pack_rows(hipStream_t st, const ShardGeom &g, int nchan_loc, c
 {
     const size_t P = (size_t)g.nsub * nchan_loc;
     if (P == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pack_rows, dim3(std::min<unsigned>(cdiv(P, 256), 4096)), dim3(256), 0, st, g, nchan_loc,
+    IC_GGL(k_pack_rows, dim3(std::min<unsigned>(cdiv(P, 256), 4096)), dim3(256), 0, st, g, nchan_loc,
                        std_d, mean_d, fft_d, ptp_d, valid, send);
     return hipGetLastError();
 }
@@ -4223,7 +4223,7 @@ hipError_t launch_assemble_rows(hipStream_t st, const ShardGeom &g, const unsign
 {
     const size_t n = (size_t)(g.row0[g.rank + 1] - g.row0[g.rank]) * g.nchan_g;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_assemble_rows, dim3(std::min<unsigned>(cdiv(n, 256), 4096)), dim3(256), 0, st, g, recv,
+    IC_GGL(k_assemble_rows, dim3(std::min<unsigned>(cdiv(n, 256), 4096)), dim3(256), 0, st, g, recv,
                        std_r, mean_r, fft_r, ptp_r, valid_r);
     return hipGetLastError();
 }
@@ -4231,34 +4231,34 @@ hipError_t launch_assemble_rows(hipStream_t st, const ShardGeom &g, const unsign
 hipError_t launch_unpack_rowstats(hipStream_t st, const ShardGeom &g, int rows_pad, const double *recv,
                                   double *row_med, double *row_mad)
 {
-    hipLaunchKernelGGL(k_unpack_rowstats, dim3(cdiv(4 * (size_t)g.nsub, 256)), dim3(256), 0, st, g, rows_pad, recv,
+    IC_GGL(k_unpack_rowstats, dim3(cdiv(4 * (size_t)g.nsub, 256)), dim3(256), 0, st, g, rows_pad, recv,
                        row_med, row_mad);
     return hipGetLastError();
 }
 
 hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, int n, int32_t *buf)
 {
-    hipLaunchKernelGGL(k_sum_i32, dim3(cdiv(n, 64)), dim3(64), 0, st, gathered, world, n, buf);
+    IC_GGL(k_sum_i32, dim3(cdiv(n, 64)), dim3(64), 0, st, gathered, world, n, buf);
     return hipGetLastError();
 }
 
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
                            double *T64, double *T2)
 {
-    hipLaunchKernelGGL(k_tscrunch, dim3(cdiv(nbin, 64)), dim3(64), 0, st, F, wf, nsub, nbin, T, T64, T2);
+    IC_GGL(k_tscrunch, dim3(cdiv(nbin, 64)), dim3(64), 0, st, F, wf, nsub, nbin, T, T64, T2);
     return hipGetLastError();
 }
 
 hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P)
 {
-    hipLaunchKernelGGL(k_fit_init, dim3(cdiv(P, 256)), dim3(256), 0, st, S, P);
+    IC_GGL(k_fit_init, dim3(cdiv(P, 256)), dim3(256), 0, st, S, P);
     return hipGetLastError();
 }
 
 hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double *T64, int nbin)
 {
     const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
-    hipLaunchKernelGGL(k_fit_prep, dim3(1), dim3(256), sizeof(double) * nsw, st, T64, nbin, nsw, S.U);
+    IC_GGL(k_fit_prep, dim3(1), dim3(256), sizeof(double) * nsw, st, T64, nbin, nsw, S.U);
     return hipGetLastError();
 }
 
@@ -4273,10 +4273,10 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
     const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
     if (ldD % 4 != 0 || ldD < nsw || (dtiled && ldD % 32 != 0)) return hipErrorInvalidValue;
     if (!list)
-        hipLaunchKernelGGL(k_fit_pass<true>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled,
+        IC_GGL(k_fit_pass<true>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled,
                            list, nctr, S, (const double *)S.U);
     else
-        hipLaunchKernelGGL(k_fit_pass<false>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw,
+        IC_GGL(k_fit_pass<false>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw,
                            dtiled, list, nctr, S, (const double *)nullptr);
     return hipGetLastError();
 }
@@ -4287,7 +4287,7 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nctr, amp,
+    IC_GGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nctr, amp,
                        info, next_list, ctr, host_n);
     return hipGetLastError();
 }
@@ -4299,7 +4299,7 @@ hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, lo
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min<long>(cdiv(n, TAIL_WAVES), 65536);
-    hipLaunchKernelGGL(k_fit_tail, dim3(grid), dim3(64 * TAIL_WAVES), 0, st, D, T64, P, nbin, ldD, dtiled, list, nctr,
+    IC_GGL(k_fit_tail, dim3(grid), dim3(64 * TAIL_WAVES), 0, st, D, T64, P, nbin, ldD, dtiled, list, nctr,
                        S, amp, info, sweeps);
     return hipGetLastError();
 }
@@ -4314,13 +4314,13 @@ static hipError_t launch_p2(hipStream_t st, const DiagArgs &a, size_t P)
     const size_t shm = fixed + gpb * (size_t)C::GROUP_BYTES;
     const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
     if (a.mode == DIAG_EXACT)
-        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_EXACT, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
+        IC_GGL((k_diag_p2<NN, DIAG_EXACT, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     else if (a.mode == DIAG_CLOSED)
-        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_CLOSED, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
+        IC_GGL((k_diag_p2<NN, DIAG_CLOSED, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     else if (a.mode == DIAG_FIT)   // f32 rows either way (launch_diag passes D64 = false)
-        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_FIT, false>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
+        IC_GGL((k_diag_p2<NN, DIAG_FIT, false>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     else   // comprehensive_stats of given rows (f64 data: the fractional-dedispersion loop)
-        hipLaunchKernelGGL((k_diag_p2<NN, DIAG_STATS, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
+        IC_GGL((k_diag_p2<NN, DIAG_STATS, D64>), dim3(grid), dim3(C::TPP * gpb), shm, st, a);
     return hipGetLastError();
 }
 
@@ -4332,9 +4332,9 @@ static hipError_t launch_cl(hipStream_t st, const DiagArgs &a, size_t P)
     const size_t shm = (size_t)C::TW_LDS * 16 + gpb * (size_t)C::GROUP_BYTES;
     const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
     if (a.mode == DIAG_EXACT)
-        hipLaunchKernelGGL((k_diag_cl<NN, DIAG_EXACT>), dim3(grid), dim3(C::L * gpb), shm, st, a);
+        IC_GGL((k_diag_cl<NN, DIAG_EXACT>), dim3(grid), dim3(C::L * gpb), shm, st, a);
     else
-        hipLaunchKernelGGL((k_diag_cl<NN, DIAG_CLOSED>), dim3(grid), dim3(C::L * gpb), shm, st, a);
+        IC_GGL((k_diag_cl<NN, DIAG_CLOSED>), dim3(grid), dim3(C::L * gpb), shm, st, a);
     return hipGetLastError();
 }
 
@@ -4381,7 +4381,7 @@ hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
     const size_t shm = fixed + wpb * lay.per_wave;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<size_t>((P + wpb - 1) / wpb, 8192);
-    hipLaunchKernelGGL(k_diag, dim3(grid), dim3(64 * wpb), shm, st, a);
+    IC_GGL(k_diag, dim3(grid), dim3(64 * wpb), shm, st, a);
     return hipGetLastError();
 }
 
@@ -4399,7 +4399,7 @@ size_t diag_lds_bytes(int nbin)
 hipError_t launch_tnorm(hipStream_t st, const double *T64, const PwPlan *plan, int nleaf_ub, double *TT)
 {
     const size_t shm = (size_t)(nleaf_ub * 9 + nleaf_ub + 8) * 8;
-    hipLaunchKernelGGL(k_tnorm, dim3(1), dim3(64), shm, st, T64, plan, TT);
+    IC_GGL(k_tnorm, dim3(1), dim3(64), shm, st, T64, plan, TT);
     return hipGetLastError();
 }
 
@@ -4437,9 +4437,9 @@ hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
                 const size_t gshm = 1024 + 16 * (size_t)W + (size_t)W * seg * 8;
                 if (gshm <= 160 * 1024) {
                     if (W == 4)
-                        hipLaunchKernelGGL(k_linestats_grp<4>, dim3(lines), dim3(256), gshm, st, a, rows, len);
+                        IC_GGL(k_linestats_grp<4>, dim3(lines), dim3(256), gshm, st, a, rows, len);
                     else
-                        hipLaunchKernelGGL(k_linestats_grp<8>, dim3(lines), dim3(512), gshm, st, a, rows, len);
+                        IC_GGL(k_linestats_grp<8>, dim3(lines), dim3(512), gshm, st, a, rows, len);
                     const hipError_t e = hipGetLastError();
                     if (e != hipSuccess) return e;
                     continue;
@@ -4451,7 +4451,7 @@ hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)
         while (wpb > 1 && (size_t)wpb * per_wave > 64 * 1024) --wpb;
         const size_t shm = (size_t)wpb * per_wave;
         if (shm > 160 * 1024) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_linestats, dim3(cdiv(lines, wpb)), dim3(64 * wpb), shm, st, a, rows, len, wpb,
+        IC_GGL(k_linestats, dim3(cdiv(lines, wpb)), dim3(64 * wpb), shm, st, a, rows, len, wpb,
                            per_wave);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -4469,7 +4469,7 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
 {
     const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 256), 1024);
-    hipLaunchKernelGGL(k_combine, dim3(grid), dim3(256), 0, st, nsub, nchan, valid, info, w0, std_d,
+    IC_GGL(k_combine, dim3(grid), dim3(256), 0, st, nsub, nchan, valid, info, w0, std_d,
                        mean_d, ptp_d, ptp_f32, fft_d, col_med, col_mad, row_med, row_mad, chanthresh, subintthresh,
                        test, W, hist, iter, counters);
     return hipGetLastError();
@@ -4483,7 +4483,7 @@ hipError_t launch_residual(hipStream_t st, const float *D, const float *raw, con
     const size_t P = (size_t)nsub * nchan;
     if (!D && (!raw || !base)) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 4), 16384);
-    hipLaunchKernelGGL(k_residual, dim3(grid), dim3(256), 0, st, D, raw, base, T64, amp, info, shift, P, nchan, nbin,
+    IC_GGL(k_residual, dim3(grid), dim3(256), 0, st, D, raw, base, T64, amp, info, shift, P, nchan, nbin,
                        ldD, dtiled, pr_on, pr_factor, pr_start, pr_end, R);
     return hipGetLastError();
 }
@@ -4507,7 +4507,7 @@ hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
     const unsigned grid = (unsigned)std::min<size_t>(P, 16384);
 #define IC_ROT(NN)                                                                                 \
     case NN:                                                                                       \
-        hipLaunchKernelGGL(k_rotate<NN>, dim3(grid), dim3(RotCfg<NN>::TB), 0, st, a);              \
+        IC_GGL(k_rotate<NN>, dim3(grid), dim3(RotCfg<NN>::TB), 0, st, a);              \
         break;
     switch (a.nbin) {
         IC_ROT(64) IC_ROT(128) IC_ROT(256) IC_ROT(512) IC_ROT(1024) IC_ROT(2048) IC_ROT(4096)

@@ -23,6 +23,10 @@
 
 using namespace icgpu;
 
+namespace icgpu {
+thread_local PendingTiming g_timing;
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -245,6 +249,12 @@ static hipError_t spin_sync(Session *s)
     return poll_event(s->sev);
 }
 
+#ifndef IC_TIMING_MARKERS
+#define IC_TIMING_MARKERS 0   // A/B knob: 1 = hipEventRecord markers around every timed launch
+#endif
+// Timed launches go through the dispatch packet (g_timing, ic_internal.h):
+// no marker packets around them.  A wrapper that launched nothing drops its
+// events; one that launched several kernels ends the interval with a marker.
 #define LAUNCH(S, KID, CALL)                                                   \
     do {                                                                       \
         Timed t_{KID, nullptr, nullptr};                                       \
@@ -252,12 +262,18 @@ static hipError_t spin_sync(Session *s)
         if (tm_) {                                                             \
             CK(take_event((S), &t_.a));                                        \
             CK(take_event((S), &t_.b));                                        \
-            CK(hipEventRecord(t_.a, (S)->stream));                             \
+            if (IC_TIMING_MARKERS) CK(hipEventRecord(t_.a, (S)->stream));      \
+            else g_timing = PendingTiming{t_.a, t_.b, 0, 0};                   \
         }                                                                      \
-        CK(CALL);                                                              \
-        if (tm_) {                                                             \
-            CK(hipEventRecord(t_.b, (S)->stream));                             \
+        const hipError_t lc_ = (CALL);                                         \
+        const PendingTiming pt_ = g_timing;                                    \
+        g_timing = PendingTiming{};                                            \
+        CK(lc_);                                                               \
+        if (tm_ && (pt_.used || IC_TIMING_MARKERS)) {                          \
+            if (pt_.extra || IC_TIMING_MARKERS) CK(hipEventRecord(t_.b, (S)->stream)); \
             (S)->events.push_back(t_);                                         \
+        } else if (tm_) {                                                      \
+            (S)->enext -= 2;   /* nothing launched: the pair goes back */      \
         }                                                                      \
     } while (0)
 
@@ -527,7 +543,7 @@ RotateArgs residual_rotate_args(Session *s, int pr_start, int pr_end)
 int prepare(Session *s)
 {
     const int nsub = s->p.nsub, nchan = s->nchan, nbin = s->p.nbin;
-    hipLaunchKernelGGL(k_valid, dim3((unsigned)((s->P + 255) / 256)), dim3(256), 0, s->stream, s->w0,
+    IC_GGL(k_valid, dim3((unsigned)((s->P + 255) / 256)), dim3(256), 0, s->stream, s->w0,
                        s->valid, s->W, s->hist, s->P);
     CK(hipGetLastError());
     if (s->comm) {
@@ -1605,7 +1621,7 @@ int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const floa
     if (!tw2.empty()) CK(hipMemcpyAsync(btw2.p, tw2.data(), 16 * tw2.size(), hipMemcpyHostToDevice, st));
     CK(hipMemcpyAsync(bplan.p, &plan, sizeof plan, hipMemcpyHostToDevice, st));
     CK(hipMemsetAsync(cnt, 0, 4 * 8, st));
-    hipLaunchKernelGGL(k_valid, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, w0, valid, W, hist, P);
+    IC_GGL(k_valid, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, w0, valid, W, hist, P);
     CK(hipGetLastError());
     DiagArgs a{};
     a.mode = DIAG_STATS;
