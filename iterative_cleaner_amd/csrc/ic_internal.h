@@ -12,8 +12,9 @@ namespace icgpu {
 // it calls dispatches through hipExtLaunchKernelGGL, whose packet records
 // both timestamps, so a timed kernel costs no extra marker packets (C2, the
 // bench's timed region with k_fit_pass timed: 27.74 ms per clean with a
-// hipEventRecord pair around each launch, 27.62 with the packet's own).  Further kernels of the same wrapper are counted in `extra`;
-// the session then ends the interval with a marker after the wrapper.
+// hipEventRecord pair around each launch, 27.62 with the packet's own).
+// Further kernels of the same wrapper are counted in `extra`; the session
+// then ends the interval with a marker after the wrapper.
 struct PendingTiming {
     hipEvent_t a = nullptr, b = nullptr;
     int used = 0, extra = 0;
@@ -205,7 +206,8 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
 // last block writes the survivor total to
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const unsigned long long *nctr, long bound, double *amp, int32_t *info,
-                            int32_t *next_list, unsigned long long *ctr, int32_t *host_n);
+                            int32_t *next_list, unsigned long long *ctr, int32_t *host_n,
+                            uint8_t *late = nullptr);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
                            const FitStateArrays &S, double *amp, int32_t *info, unsigned long long *sweeps);
@@ -239,8 +241,17 @@ struct DiagArgs {
     double *std_o, *mean_o, *fft_o, *ptp_o;
     int data_f64;      // psrchive get_data returns f64: X = f64(R) * f64(w), f64 mean and ptp
     int dtiled;        // D is the tiled fit cube (dt_ofs); DIAG_STATS inputs are row-major
+    // only the profiles of a list (the fork of the exact fit's diagnostics):
+    // list + packed count as the fit rounds' (RoundList); nullptr = all
+    const int32_t *list = nullptr;
+    const unsigned long long *nctr = nullptr;
+    const uint8_t *skip = nullptr;   // != nullptr: profiles with skip[k] != 0 are left out
 };
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a);
+// the diagnostics kernel launch_diag picks for `a` takes a profile list
+bool diag_list_supported(const DiagArgs &a);
+// late != nullptr (launch_fit_state): late[k] = 1 for every survivor of the
+// round (the fork round; the flags were zeroed before it)
 // dynamic LDS the generic k_diag needs for one wave (0 for the power-of-two kernels)
 size_t diag_lds_bytes(int nbin);
 // *TT = numpy pairwise sum of T64[i]^2 over nbin (plan), nleaf_ub >= plan leaves/ops

@@ -1406,7 +1406,8 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
                                                             const unsigned long long *__restrict__ nctr,
                                                             double *__restrict__ amp_o, int32_t *__restrict__ info_o,
                                                             int32_t *__restrict__ next_list,
-                                                            unsigned long long *__restrict__ ctr, int32_t *host_n)
+                                                            unsigned long long *__restrict__ ctr, int32_t *host_n,
+                                                            uint8_t *__restrict__ late)
 {
     __shared__ int wcnt[FIT_STATE_BS / 64];
     __shared__ int woff[FIT_STATE_BS / 64];
@@ -1505,6 +1506,7 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             }
         }
     }
+    if (late && still) late[k] = 1;   // the fork round: still fitting after it
     // block-aggregated append, partitioned by request (RoundList)
     stillB = still == 2;
     still = still == 1;
@@ -2840,6 +2842,16 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
     const unsigned P = (unsigned)a.nsub * (unsigned)a.nchan;
     const unsigned stride = gridDim.x * gpb;
     const unsigned nchan = (unsigned)a.nchan;
+    // profiles: all P, or the slots of a list, minus those with skip[k] != 0
+    // (the two passes of the fit's forked diagnostics)
+    const RoundList rl(a.list, a.nctr, (long)P);
+    const unsigned nslot = (unsigned)rl.n();
+    const uint8_t *skip = a.skip;
+    auto next_slot = [&](unsigned sl) {   // the first slot >= sl this group measures (uniform)
+        if (skip)
+            while (sl < nslot && skip[rl.at(sl)]) sl += stride;
+        return sl;
+    };
     const int ca = t >> 3, cc = t & 7;
     const int jb = 128 * ca + cc;   // first sample of the thread's chain
     // byte offsets in the work array: d of chain sample q at wb[q & 3] + 64 (q & ~3)
@@ -2856,11 +2868,12 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
 #pragma unroll
         for (int q = 0; q < 16; ++q) pv[q] = IC_CL_PROBE == 2 ? (float)(q + kk) : pn[8 * q];
     };
-    unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group);
+    unsigned slot = next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
+    unsigned k = slot < nslot ? (unsigned)rl.at(slot) : 0u;
     double nx = 0.0;
     int nst = 0, nsh = 0;
     float nw = 0.0f, nb = 0.0f;
-    if (k < P) {
+    if (slot < nslot) {
         loadrow(k);
         if (!closed) {
             nx = a.amp[k];
@@ -2870,7 +2883,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
         nw = a.w0[k];
         nsh = a.shift[k % nchan];
     }
-    for (; k < P; k += stride) {
+    for (unsigned snext; slot < nslot; slot = snext) {
         // multi-wave groups: keep the FFT's LDS addresses inside the loop (hoisted,
         // they spill at N >= 2048; k_diag_p2); one wave: hoisted, 118 VGPRs
         if (WPP > 1 || IC_CL_OPAQUE_T) asm volatile("" : "+v"(t));
@@ -2930,8 +2943,11 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
 #pragma unroll
             for (int q = 0; q < 16; ++q) X[q] = 0.0f * w;
         }
-        if (k + stride < P) {
-            const unsigned kn = k + stride;
+        const unsigned kc = k;   // this profile (the prefetch below moves k on)
+        snext = next_slot(slot + stride);
+        if (snext < nslot) {
+            const unsigned kn = (unsigned)rl.at(snext);
+            k = kn;
             loadrow(kn);
             if (!closed) {
                 nx = a.amp[kn];
@@ -3041,10 +3057,10 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
             fftv = nanx ? NAN : 0.0;
         }
         if (t == 0) {
-            a.std_o[k] = valid ? sd : 0.0;
-            a.mean_o[k] = valid ? mean : 0.0;
-            a.ptp_o[k] = ptp;
-            a.fft_o[k] = fftv;
+            a.std_o[kc] = valid ? sd : 0.0;
+            a.mean_o[kc] = valid ? mean : 0.0;
+            a.ptp_o[kc] = ptp;
+            a.fft_o[kc] = fftv;
         }
     }
 }
@@ -4283,12 +4299,12 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
 
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const unsigned long long *nctr, long bound, double *amp, int32_t *info,
-                            int32_t *next_list, unsigned long long *ctr, int32_t *host_n)
+                            int32_t *next_list, unsigned long long *ctr, int32_t *host_n, uint8_t *late)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
     IC_GGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nctr, amp,
-                       info, next_list, ctr, host_n);
+                       info, next_list, ctr, host_n, late);
     return hipGetLastError();
 }
 
@@ -4348,6 +4364,14 @@ static bool diag_cl_enabled()
     return on;
 }
 
+static bool uses_cl(const DiagArgs &a)
+{
+    return (a.mode == DIAG_EXACT || a.mode == DIAG_CLOSED) && a.T2 && a.raw && a.base && !a.pr_on && !a.data_f64 &&
+           (a.nbin == 1024 || a.nbin == 2048 || a.nbin == 4096) && diag_cl_enabled();
+}
+
+bool diag_list_supported(const DiagArgs &a) { return uses_cl(a); }
+
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
 {
     const int nbin = a.nbin;
@@ -4358,12 +4382,12 @@ hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
                                  (a.mode == DIAG_FIT && !a.TT)))
         return hipErrorInvalidValue;
     // the chain-layout kernel: exact / closed modes from the raw cube, f32 data, no pulse region
-    if ((a.mode == DIAG_EXACT || a.mode == DIAG_CLOSED) && a.T2 && a.raw && a.base && !a.pr_on && !a.data_f64 &&
-        diag_cl_enabled()) {
+    if (uses_cl(a)) {
         if (nbin == 1024) return launch_cl<1024>(st, a, P);
         if (nbin == 2048) return launch_cl<2048>(st, a, P);
         if (nbin == 4096) return launch_cl<4096>(st, a, P);
     }
+    if (a.list || a.skip) return hipErrorInvalidValue;   // lists / skips: k_diag_cl only (diag_list_supported)
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
         if (a.data_f64 && a.mode != DIAG_FIT) return launch_p2<NN, true>(st, a, P);                \

@@ -127,6 +127,19 @@ struct Session {
     int plan_ub = 0;            // max(leaves, ops) of the pairwise plan (k_tnorm scratch)
     LineStatsArgs ls_knobs;     // row-median form, from the environment at creation
     long tail_threshold = kTailProfiles;
+    // diagnostics forked onto a second stream (exact fit): the state kernel
+    // of round diag_fork (0 = off) flags the profiles still fitting; from
+    // round diag_fork + fork_delay on the others are measured on dstream while
+    // the fit's latency-bound late rounds and tail run, the flagged ones on
+    // the main stream once the fit is done.  C2, one MI355X, same box (ms per
+    // clean): no fork 28.70-28.77, fork 3 / delay 1 27.99-28.06, 3 / 0
+    // 28.53-28.61, 3 / 2 28.41-28.46, 4 / 0 28.01-28.19, 4 / 1 28.45-28.52
+    int diag_fork = 3;
+    hipStream_t dstream = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    uint8_t *late = nullptr;       // [P] 1: still fitting after round diag_fork (pass A skips them)
+    int fork_round = -1;           // this iteration's fork round (-1: none)
+    int fork_delay = 1;            // rounds between the flags and pass A (A/B knob IC_FORK_DELAY)
     ic_run_stats stats{};
     std::vector<int32_t> bad_fits;   // per iteration of the last run: fit statuses outside 1-4
     // fractional dedispersion (dedisp_mode IC_DEDISP_FFT): the dedispersed raw
@@ -255,14 +268,15 @@ static hipError_t spin_sync(Session *s)
 // Timed launches go through the dispatch packet (g_timing, ic_internal.h):
 // no marker packets around them.  A wrapper that launched nothing drops its
 // events; one that launched several kernels ends the interval with a marker.
-#define LAUNCH(S, KID, CALL)                                                   \
+#define LAUNCH(S, KID, CALL) LAUNCH_ON(S, KID, (S)->stream, CALL)
+#define LAUNCH_ON(S, KID, ST, CALL)                                            \
     do {                                                                       \
         Timed t_{KID, nullptr, nullptr};                                       \
         const bool tm_ = (S)->timing && ((S)->timing_only < 0 || (S)->timing_only == (KID)); \
         if (tm_) {                                                             \
             CK(take_event((S), &t_.a));                                        \
             CK(take_event((S), &t_.b));                                        \
-            if (IC_TIMING_MARKERS) CK(hipEventRecord(t_.a, (S)->stream));      \
+            if (IC_TIMING_MARKERS) CK(hipEventRecord(t_.a, (ST)));             \
             else g_timing = PendingTiming{t_.a, t_.b, 0, 0};                   \
         }                                                                      \
         const hipError_t lc_ = (CALL);                                         \
@@ -270,7 +284,7 @@ static hipError_t spin_sync(Session *s)
         g_timing = PendingTiming{};                                            \
         CK(lc_);                                                               \
         if (tm_ && (pt_.used || IC_TIMING_MARKERS)) {                          \
-            if (pt_.extra || IC_TIMING_MARKERS) CK(hipEventRecord(t_.b, (S)->stream)); \
+            if (pt_.extra || IC_TIMING_MARKERS) CK(hipEventRecord(t_.b, (ST))); \
             (S)->events.push_back(t_);                                         \
         } else if (tm_) {                                                      \
             (S)->enext -= 2;   /* nothing launched: the pair goes back */      \
@@ -330,7 +344,10 @@ void free_all(Session *s)
         if (s->slot_ev[q]) (void)hipEventDestroy(s->slot_ev[q]);
     }
     if (s->copy_stream) (void)hipStreamDestroy(s->copy_stream);
-    void *bufs[] = {s->D,     s->W,   s->base, s->base0, s->F,   s->wf,
+    if (s->dstream) (void)hipStreamDestroy(s->dstream);
+    if (s->fork_ev) (void)hipEventDestroy(s->fork_ev);
+    if (s->join_ev) (void)hipEventDestroy(s->join_ev);
+    void *bufs[] = {s->late, s->D,     s->W,   s->base, s->base0, s->F,   s->wf,
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
@@ -671,8 +688,14 @@ int shard_rowstats(Session *s, const LineStatsArgs &la)
 // the counts one round behind: the stream always has the next round queued.
 // Once the bound drops to tail_threshold (default kTailProfiles; 0 = never),
 // k_fit_tail finishes the rest in one launch (one wave per profile).
-int run_fit(Session *s)
+// fork != nullptr: after round s->diag_fork the diagnostics of the profiles
+// already fitted run on s->dstream (fork_diag); the survivors of that round
+// are kept in the third list buffer for the main stream's second pass.
+int fork_diag(Session *s, const DiagArgs &da, int r);
+
+int run_fit(Session *s, const DiagArgs *fork)
 {
+    s->fork_round = -1;
     const long P = (long)s->P;
     const int nbin = s->p.nbin;
     CK(launch_fit_init(s->stream, s->fs, P));
@@ -682,27 +705,41 @@ int run_fit(Session *s)
     CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * 2 * kMaxRounds, s->stream));
     unsigned long long *ctr = (unsigned long long *)s->rcount;
     unsigned long long *tail_sweeps = ctr + kMaxRounds;
-    int32_t *bufs[2] = {s->lists, s->lists + P};
+    int32_t *bufs[3] = {s->lists, s->lists + P, s->lists + 2 * P};
+    if (fork) CK(hipMemsetAsync(s->late, 0, (size_t)P, s->stream));   // the fork round's state kernel sets them
     const int32_t *cur = nullptr;                    // round 0: all profiles
     const unsigned long long *cin = nullptr;         // the round's packed list counts (RoundList)
     long bound = P;                                 // >= the active count of the next round
     int rounds = 0;
     bool tail = false;
+    int flagged = -1;   // the fork round, once its survivors are flagged and pass A not yet queued
     for (int r = 0;; ++r) {
         if (r >= kMaxRounds) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", r);
         if (bound <= s->tail_threshold) {
+            if (flagged >= 0) {
+                if (int rc = fork_diag(s, *fork, flagged)) return rc;
+                flagged = -1;
+            }
             LAUNCH(s, K_FIT_TAIL, launch_fit_tail(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
                                                   s->fs, s->amp, s->info, tail_sweeps));
             tail = true;
             break;
         }
-        int32_t *next = bufs[r & 1];
+        const bool fork_here = fork && r == s->diag_fork;
+        int32_t *next = fork_here ? bufs[2] : bufs[r & 1];
         LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
                                                 s->fs));
         s->h_rcount[r] = -1;
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
-                                                ctr + r, s->d_h_rcount + r));
+                                                ctr + r, s->d_h_rcount + r, fork_here ? s->late : nullptr));
         CK(hipEventRecord(s->rev[r & 1], s->stream));
+        if (fork_here) flagged = r;
+        // pass A is queued fork_delay rounds after the flags: the first late
+        // rounds are the largest and run alone
+        if (flagged >= 0 && r >= flagged + s->fork_delay) {
+            if (int rc = fork_diag(s, *fork, flagged)) return rc;
+            flagged = -1;
+        }
         ++rounds;
         cur = next;
         cin = ctr + r;   // packed A / B counts of the next round's list
@@ -714,6 +751,8 @@ int run_fit(Session *s)
             bound = c;
         }
     }
+    if (flagged >= 0)
+        if (int rc = fork_diag(s, *fork, flagged)) return rc;
     // no stream synchronisation: the counts below were all read by the loop
     // (after the event of their round), so the diagnostics queue right behind
     // the last fit kernel
@@ -727,6 +766,25 @@ int run_fit(Session *s)
     s->fit_rounds = effective;
     s->stats.fit_rounds += effective;
     s->stats.fit_profile_sweeps += swept;
+    return 0;
+}
+
+// The fork (run_fit, round r): the profiles that round r's state kernel did
+// not flag in s->late have their final amp / info, so their diagnostics
+// (pass A: k_diag_cl skipping the flagged ones) run on dstream, ordered after
+// round r only, while the main stream goes on with the late rounds and the
+// tail (latency-bound: a few thousand waves).  The flagged profiles, round r's
+// survivor list in the third list buffer, get pass B on the main stream after
+// the fit (run_impl), which then joins dstream.
+int fork_diag(Session *s, const DiagArgs &da, int r)
+{
+    CK(hipEventRecord(s->fork_ev, s->stream));
+    CK(hipStreamWaitEvent(s->dstream, s->fork_ev, 0));
+    DiagArgs a = da;
+    a.skip = s->late;
+    LAUNCH_ON(s, K_DIAG, s->dstream, launch_diag(s->dstream, a));
+    CK(hipEventRecord(s->join_ev, s->dstream));
+    s->fork_round = r;
     return 0;
 }
 
@@ -795,6 +853,10 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     linestats_knobs(s->ls_knobs);
     if (const char *e = getenv("IC_FIT_TAIL"))   // A/B knob: the tail hand-over threshold (ic_set_fit_tail)
         if (*e) s->tail_threshold = atol(e);
+    if (const char *e = getenv("IC_DIAG_FORK"))   // A/B knob: fork round of the diagnostics (0 = no fork)
+        if (*e) s->diag_fork = atoi(e) > 0 ? atoi(e) : 0;
+    if (const char *e = getenv("IC_FORK_DELAY"))
+        if (*e && atoi(e) >= 0) s->fork_delay = atoi(e);
     s->p = p;
     s->device = device;
     s->rank = rank;
@@ -846,6 +908,13 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (hipSetDevice(device) != hipSuccess) return bail(fail(IC_EHIP, "hipSetDevice(%d) failed", device));
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(IC_EHIP, "hipStreamCreate failed"));
+    if (p.fit_mode == IC_FIT_EXACT && p.dedisp_mode == IC_DEDISP_SHIFT && s->diag_fork > 0) {
+        // (a higher priority for the fit's stream measured no different)
+        if (hipStreamCreateWithFlags(&s->dstream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s->join_ev, hipEventDisableTiming) != hipSuccess)
+            return bail(fail(IC_EHIP, "diagnostics stream / events failed"));
+    }
     const size_t P = s->P, N = s->N;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
     const bool exact = p.fit_mode == IC_FIT_EXACT;
@@ -912,8 +981,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw, (size_t)nbin);
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
-    if (exact) AL(s->lists, 2 * P);
+    if (exact) AL(s->lists, 3 * P);   // two ping-pong round lists + the fork round's survivors
     AL(s->rcount, (size_t)2 * kMaxRounds + 2);   // + the tail's sweep counter (u64)
+    if (exact && !s->fftded && s->diag_fork > 0) AL(s->late, P);
     if (sharded) {
         const char *cerr = nullptr;
         s->comm = make_comm(&cerr);
@@ -1315,7 +1385,8 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         if (int rc = iteration_template(s, n_iter)) return rc;
         DiagArgs da = diag_args(s, pr_start, pr_end);
         if (p.fit_mode == IC_FIT_EXACT) {
-            if (int rc = run_fit(s)) return rc;
+            const bool fork = s->dstream && s->late && diag_list_supported(da);
+            if (int rc = run_fit(s, fork ? &da : nullptr)) return rc;
         } else {
             LAUNCH(s, K_TNORM, launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
         }
@@ -1333,7 +1404,16 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             da.ldD = nbin;
             da.dtiled = 0;
         }
-        LAUNCH(s, K_DIAG, launch_diag(s->stream, da));
+        if (s->fork_round >= 0) {
+            // pass B: the profiles still fitting at the fork, then join pass A
+            DiagArgs b = da;
+            b.list = s->lists + 2 * s->P;
+            b.nctr = (const unsigned long long *)s->rcount + s->fork_round;
+            LAUNCH(s, K_DIAG, launch_diag(s->stream, b));
+            CK(hipStreamWaitEvent(s->stream, s->join_ev, 0));
+        } else {
+            LAUNCH(s, K_DIAG, launch_diag(s->stream, da));
+        }
         // channel medians are local to a shard; row medians need whole rows
         LAUNCH(s, K_LINESTATS, launch_linestats(s->stream, la, s->comm ? 1 : 3));
         if (s->comm)
@@ -1711,7 +1791,7 @@ int ic_fit_profiles(int device, int nprof, int nbin, const float *T, const float
     CK(hipMemcpyAsync(s->raw, profiles, row * nprof, hipMemcpyHostToDevice, s->stream));
     if (fit_mode == IC_FIT_EXACT) {
         CK(hipMemcpy2DAsync(s->D, sizeof(float) * s->ldD, s->raw, row, row, P, hipMemcpyDeviceToDevice, s->stream));
-        if (int r = run_fit(s)) return r;
+        if (int r = run_fit(s, nullptr)) return r;
     } else {
         CK(launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
         DiagArgs da = diag_args(s, 0, 0);
