@@ -147,7 +147,15 @@ void linestats_knobs(LineStatsArgs &a);
 hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, const float *W, const int32_t *shift,
                                 const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
                                 double *part, double *part2, double *wpart, float *D = nullptr, int ldD = 0,
-                                int dtiled = 0);
+                                int dtiled = 0, uint8_t *exA = nullptr, uint8_t *exF = nullptr);
+// exA / exF (optional): per column [s][sb][i] 1 = its part / part2 sum is
+// exact in any order with weights 0 / 1 (k_chan_partials' ExTrack), the
+// condition for launch_chan_delta.  Iteration >= 2 (Wn = this iteration's weights, Wo = the
+// previous one's): part, part2 (carried levels) and wpart moved from Wo to Wn
+// through the changed channels only; inexact columns summed again in full.
+hipError_t launch_chan_delta(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
+                             const float *Wn, const float *Wo, int nsub, int nchan, int nbin, double *part,
+                             double *part2, double *wpart, const uint8_t *exA, const uint8_t *exF);
 // flags != nullptr: flags[s] = window of subint s moved (win updated in place)
 // element (s, leaf, i) of `part` is part[s*ss + leaf*sl + i]; the leaves are
 // combined with `plan` (single device: the nsb super-blocks; sharded: the

@@ -141,12 +141,42 @@ __device__ __forceinline__ void st_fitcube(float *p, float v)
     else *p = v;
 }
 
+// Exactness of a super-block column (the incremental template stage,
+// k_chan_delta), for archives whose weights are 0 or 1: the column's terms
+// are its values v_c (f64 from f32) over EVERY channel c of the super-block,
+// whatever its current weight.  With biased f32 exponents emin / emax of the
+// nonzero ones (subnormals as 1), every v_c is an integer multiple of
+// 2^(emin - 150) and 256 |v_c| < 2^(emax - 118); if emax - emin <= 21 every
+// partial sum of any subset of them, in any order and with any signs, is an
+// f64 integer multiple of 2^(emin - 150) below 2^(53 + emin - 150): exact.
+// The canonical sequential sum then equals the exact sum, and so does an old
+// sum plus the terms that entered minus those that left.  ExTrack keeps the
+// largest and smallest nonzero magnitude as bit patterns (4 VALU ops per
+// value; an Inf / NaN value is a larger pattern than any finite one and fails
+// the test).  Fractional weights: k_chan_delta ignores the flags.
+struct ExTrack {
+    unsigned mx = 0u, mn = 0xffffffffu;   // max |v| bits, min (|v| bits - 1): zero -> 0xffffffff
+    __device__ __forceinline__ void add(float v)
+    {
+        const unsigned a = __float_as_uint(v) & 0x7fffffffu;
+        mx = max(mx, a);
+        mn = min(mn, a - 1u);
+    }
+    __device__ __forceinline__ uint8_t exact() const
+    {
+        if (mx >= 0x7f800000u) return 0;   // Inf / NaN
+        if (mn == 0xffffffffu) return 1;   // all zero
+        const int emax = max((int)(mx >> 23), 1), emin = max((int)((mn + 1u) >> 23), 1);
+        return emax - emin <= 21 ? 1 : 0;
+    }
+};
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k_chan_partials(
     const float *__restrict__ raw, const float *__restrict__ W, const int32_t *__restrict__ shift,
     const float *__restrict__ base, const int32_t *__restrict__ flags, int nsub, int nchan, int nbin, int nsb,
     double *__restrict__ part, double *__restrict__ part2, double *__restrict__ wpart, float *__restrict__ D,
-    int ldD, int dtiled)
+    int ldD, int dtiled, uint8_t *__restrict__ exA, uint8_t *__restrict__ exF)
 {
     constexpr bool A = MODE == 0 || MODE == 2, F = MODE != 0, WD = MODE == 3;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -155,6 +185,9 @@ __global__ __launch_bounds__(256) void k_chan_partials(
     if (flags && flags[s] == 0) return;
     const int c0 = sb * kSuperBlock;
     const int c1 = min(c0 + kSuperBlock, nchan);
+    // column exactness (ExTrack) of this pass's sums (A: exA, F: exF)
+    const bool tA = A && exA, tF = F && exF;
+    ExTrack xa, xf;
     if (i < nbin) {
         double acc = 0.0, acc2 = 0.0;
         const size_t krow = (size_t)s * nchan;
@@ -180,6 +213,8 @@ __global__ __launch_bounds__(256) void k_chan_partials(
                 if (A) acc = acc + w * (double)xv[q];
                 if (F) acc2 = acc2 + w * (double)d;
                 if (WD) st_fitcube(D + d_ofs(krow + c + q, i, ldD, dtiled), d);
+                if (tA) xa.add(xv[q]);
+                if (tF) xf.add(d);
             }
         }
         for (; c < c1; ++c) {
@@ -192,13 +227,180 @@ __global__ __launch_bounds__(256) void k_chan_partials(
             if (A) acc = acc + w * (double)x;
             if (F) acc2 = acc2 + w * (double)d;
             if (WD) st_fitcube(D + d_ofs(k, i, ldD, dtiled), d);
+            if (tA) xa.add(x);
+            if (tF) xf.add(d);
         }
-        if (A) part[((size_t)s * nsb + sb) * nbin + i] = acc;
-        if (F) part2[((size_t)s * nsb + sb) * nbin + i] = acc2;
+        const size_t col = ((size_t)s * nsb + sb) * nbin + i;
+        if (A) part[col] = acc;
+        if (F) part2[col] = acc2;
+        if (tA) exA[col] = xa.exact();
+        if (tF) exF[col] = xf.exact();
     }
     if (F && blockIdx.x == 0 && threadIdx.x == 0) {
         double a = 0.0;
         for (int c = c0; c < c1; ++c) a = a + (double)W[(size_t)s * nchan + c];
+        wpart[(size_t)s * nsb + sb] = a;
+    }
+}
+
+// Incremental template stage (iteration >= 2, integer dedispersion): the
+// window totals `part` and the fscrunch partials `part2` of every super-block
+// column move from the previous weights Wo to the current Wn by the terms of
+// the channels whose weight changed: old + (sum of Wn v - Wo v over them),
+// exact for columns whose flag (ExTrack, set by the last full pass) holds;
+// the other columns, and every column of a super-block with a weight other
+// than 0 or 1, are summed again in canonical order over all channels.  part2
+// uses the carried levels: subints whose window moves are summed again
+// afterwards (k_chan_partials mode 1, flagged).  wpart is summed again (256
+// weights).  One block per (bin range, super-block, subint); a block whose
+// super-block has no changed channel does nothing.
+__global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ raw, const int32_t *__restrict__ shift,
+                                                    const float *__restrict__ base, const float *__restrict__ Wn,
+                                                    const float *__restrict__ Wo, int nchan, int nbin, int nsb,
+                                                    double *__restrict__ part, double *__restrict__ part2,
+                                                    double *__restrict__ wpart, const uint8_t *__restrict__ exA,
+                                                    const uint8_t *__restrict__ exF)
+{
+    __shared__ int chg[kSuperBlock];
+    __shared__ int fix[256];                 // columns summed again: bin | 1 << 16 (part) | 1 << 17 (part2)
+    __shared__ double tA[kSuperBlock], tF[kSuperBlock];
+    __shared__ int wcnt[4], wfrac[4], wfix[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int sb = blockIdx.y, s = blockIdx.z;
+    const int c0 = sb * kSuperBlock, c1 = min(c0 + kSuperBlock, nchan);
+    const size_t krow = (size_t)s * nchan;
+    // the changed channels of the super-block, in ascending order
+    int n, frac;
+    {
+        const int c = c0 + (int)threadIdx.x;
+        const float wn = c < c1 ? Wn[krow + c] : 0.0f, wo = c < c1 ? Wo[krow + c] : 0.0f;
+        const bool ch = __float_as_uint(wn) != __float_as_uint(wo);
+        const bool fr = !(wn == 0.0f || wn == 1.0f) || !(wo == 0.0f || wo == 1.0f);
+        const unsigned long long m = __ballot(ch);
+        if (lane == 0) {
+            wcnt[wave] = __popcll(m);
+            wfrac[wave] = __any(fr) ? 1 : 0;
+        }
+        __syncthreads();
+        int off = 0;
+        for (int w = 0; w < wave; ++w) off += wcnt[w];
+        if (ch) chg[off + __popcll(m & ((1ull << lane) - 1ull))] = c;
+        n = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        frac = wfrac[0] | wfrac[1] | wfrac[2] | wfrac[3];
+        __syncthreads();
+    }
+    if (n == 0) return;
+    constexpr int B = 16;
+    if (frac) {
+        // a weight other than 0 / 1: every column in canonical order (k_chan_partials' sums)
+        if (i < nbin) {
+            double acc = 0.0, acc2 = 0.0;
+            int c = c0;
+            for (; c + B <= c1; c += B) {
+                float xv[B], wv[B], bv[B];
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    int j = i + shift[c + q];
+                    if (j >= nbin) j -= nbin;
+                    xv[q] = raw[(krow + c + q) * nbin + j];
+                    wv[q] = Wn[krow + c + q];
+                    bv[q] = base[krow + c + q];
+                }
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    const double w = (double)wv[q];
+                    const float d = xv[q] - bv[q];
+                    acc = acc + w * (double)xv[q];
+                    acc2 = acc2 + w * (double)d;
+                }
+            }
+            for (; c < c1; ++c) {
+                int j = i + shift[c];
+                if (j >= nbin) j -= nbin;
+                const float x = raw[(krow + c) * nbin + j];
+                const double w = (double)Wn[krow + c];
+                const float d = x - base[krow + c];
+                acc = acc + w * (double)x;
+                acc2 = acc2 + w * (double)d;
+            }
+            const size_t col = ((size_t)s * nsb + sb) * nbin + i;
+            part[col] = acc;
+            part2[col] = acc2;
+        }
+    } else {
+        int need = 0;
+        if (i < nbin) {
+            const size_t col = ((size_t)s * nsb + sb) * nbin + i;
+            const bool okA = exA[col], okF = exF[col];
+            if (okA || okF) {
+                double dA = 0.0, dF = 0.0;
+                for (int q0 = 0; q0 < n; q0 += B) {
+                    float xv[B], bv[B], wnv[B], wov[B];
+#pragma unroll
+                    for (int q = 0; q < B; ++q) {
+                        const int c = chg[min(q0 + q, n - 1)];
+                        int j = i + shift[c];
+                        if (j >= nbin) j -= nbin;
+                        xv[q] = raw[(krow + c) * nbin + j];
+                        bv[q] = base[krow + c];
+                        wnv[q] = Wn[krow + c];
+                        wov[q] = Wo[krow + c];
+                    }
+#pragma unroll
+                    for (int q = 0; q < B; ++q) {
+                        if (q0 + q < n) {
+                            const float d = xv[q] - bv[q];
+                            const double wn = (double)wnv[q], wo = (double)wov[q];
+                            dA = dA + (wn * (double)xv[q] - wo * (double)xv[q]);
+                            dF = dF + (wn * (double)d - wo * (double)d);
+                        }
+                    }
+                }
+                if (okA) part[col] = part[col] + dA;
+                if (okF) part2[col] = part2[col] + dF;
+            }
+            need = (okA ? 0 : 1 << 16) | (okF ? 0 : 1 << 17);
+        }
+        // inexact columns: the whole block sums each again, one channel per
+        // thread, then one thread adds the 256 terms in canonical order
+        const unsigned long long m = __ballot(need != 0);
+        if (lane == 0) wfix[wave] = __popcll(m);
+        __syncthreads();
+        int off = 0;
+        for (int w = 0; w < wave; ++w) off += wfix[w];
+        if (need) fix[off + __popcll(m & ((1ull << lane) - 1ull))] = need | i;
+        const int nfix = wfix[0] + wfix[1] + wfix[2] + wfix[3];
+        __syncthreads();
+        for (int f = 0; f < nfix; ++f) {
+            const int e = fix[f], ib = e & 0xffff;
+            const int c = c0 + (int)threadIdx.x;
+            if (c < c1) {
+                int j = ib + shift[c];
+                if (j >= nbin) j -= nbin;
+                const float x = raw[(krow + c) * nbin + j];
+                const double w = (double)Wn[krow + c];
+                const float d = x - base[krow + c];
+                tA[threadIdx.x] = w * (double)x;
+                tF[threadIdx.x] = w * (double)d;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double acc = 0.0, acc2 = 0.0;
+                for (int q = 0; q < c1 - c0; ++q) {
+                    acc = acc + tA[q];
+                    acc2 = acc2 + tF[q];
+                }
+                const size_t col = ((size_t)s * nsb + sb) * nbin + ib;
+                if (e & (1 << 16)) part[col] = acc;
+                if (e & (1 << 17)) part2[col] = acc2;
+            }
+            __syncthreads();
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        double a = 0.0;
+        for (int c = c0; c < c1; ++c) a = a + (double)Wn[krow + c];
         wpart[(size_t)s * nsb + sb] = a;
     }
 }
@@ -4139,7 +4341,8 @@ static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) 
 
 hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, const float *W, const int32_t *shift,
                                 const float *base, const int32_t *flags, int nsub, int nchan, int nbin,
-                                double *part, double *part2, double *wpart, float *D, int ldD, int dtiled)
+                                double *part, double *part2, double *wpart, float *D, int ldD, int dtiled,
+                                uint8_t *exA, uint8_t *exF)
 {
     const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
     const int bs = nbin >= 256 ? 256 : ((nbin + 63) / 64) * 64;
@@ -4147,7 +4350,7 @@ hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, cons
     if (mode == 3 && (!D || ldD < nbin || (dtiled && ldD % 32 != 0))) return hipErrorInvalidValue;
 #define IC_CP(M)                                                                                                  \
     IC_GGL(k_chan_partials<M>, grid, dim3(bs), 0, st, raw, W, shift, base, flags, nsub, nchan, nbin, \
-                       nsb, part, part2, wpart, D, ldD, dtiled)
+                       nsb, part, part2, wpart, D, ldD, dtiled, exA, exF)
     if (mode == 0)
         IC_CP(0);
     else if (mode == 1)
@@ -4161,6 +4364,18 @@ hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, cons
 }
 
 size_t window_lds_bytes(int nbin) { return (size_t)nbin * 8 + kWindowThreads * (8 + 4); }
+
+hipError_t launch_chan_delta(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
+                             const float *Wn, const float *Wo, int nsub, int nchan, int nbin, double *part,
+                             double *part2, double *wpart, const uint8_t *exA, const uint8_t *exF)
+{
+    const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
+    if (!exA || !exF) return hipErrorInvalidValue;
+    // 256 threads: one per channel of the super-block (the change list), then one per bin
+    IC_GGL(k_chan_delta, dim3(cdiv(nbin, 256), nsb, nsub), dim3(256), 0, st, raw, shift, base, Wn, Wo, nchan, nbin,
+           nsb, part, part2, wpart, exA, exF);
+    return hipGetLastError();
+}
 
 hipError_t launch_window(hipStream_t st, const double *part, long ss, long sl, const SbPlan &plan, int nsub,
                          int nbin, int width, int32_t *win, int32_t *flags)

@@ -135,6 +135,12 @@ struct Session {
     // clean): no fork 28.70-28.77, fork 3 / delay 1 27.99-28.06, 3 / 0
     // 28.53-28.61, 3 / 2 28.41-28.46, 4 / 0 28.01-28.19, 4 / 1 28.45-28.52
     int diag_fork = 3;
+    // incremental template stage (integer dedispersion, iteration >= 2):
+    // column exactness flags [nsub][nsb][nbin] of part (exA, set once per run
+    // by prepare) and part2 (exF, set by every full fscrunch pass);
+    // k_chan_delta then moves the sums through the changed channels only
+    bool incr = true;
+    uint8_t *exA = nullptr, *exF = nullptr;
     hipStream_t dstream = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     uint8_t *late = nullptr;       // [P] 1: still fitting after round diag_fork (pass A skips them)
@@ -347,7 +353,7 @@ void free_all(Session *s)
     if (s->dstream) (void)hipStreamDestroy(s->dstream);
     if (s->fork_ev) (void)hipEventDestroy(s->fork_ev);
     if (s->join_ev) (void)hipEventDestroy(s->join_ev);
-    void *bufs[] = {s->late, s->D,     s->W,   s->base, s->base0, s->F,   s->wf,
+    void *bufs[] = {s->late, s->exA, s->exF, s->D,     s->W,   s->base, s->base0, s->F,   s->wf,
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
@@ -591,7 +597,7 @@ int prepare(Session *s)
     }
     LAUNCH(s, K_CHAN_PARTIALS,
            launch_chan_partials(s->stream, 0, s->raw, s->w0, s->shift, nullptr, nullptr, nsub, nchan, nbin, s->part,
-                                nullptr, nullptr));
+                                nullptr, nullptr, nullptr, 0, 0, s->exA, nullptr));
     if (int rc = window_stage(s, nullptr)) return rc;
     LAUNCH(s, K_BASE,
            launch_base(s->stream, s->raw, s->shift, s->win, nullptr, nsub, nchan, nbin, s->width, s->base0));
@@ -635,17 +641,25 @@ int iteration_template(Session *s, int iter)
     if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s; also writes D (exact fit)
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, s->D ? 3 : 1, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan,
-                                    nbin, nullptr, s->part2, s->wpart, s->D, s->ldD, s->dtiled));
+                                    nbin, nullptr, s->part2, s->wpart, s->D, s->ldD, s->dtiled, nullptr, s->exF));
     } else {
-        LAUNCH(s, K_CHAN_PARTIALS,
-               launch_chan_partials(s->stream, 2, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
-                                    s->part, s->part2, s->wpart));
+        if (s->incr) {
+            // the sums of the previous iteration moved through the changed channels
+            const float *Wo = s->hist + (size_t)(iter - 2) * s->P;
+            LAUNCH(s, K_CHAN_PARTIALS,
+                   launch_chan_delta(s->stream, s->raw, s->shift, s->base, s->W, Wo, nsub, nchan, nbin, s->part,
+                                     s->part2, s->wpart, s->exA, s->exF));
+        } else {
+            LAUNCH(s, K_CHAN_PARTIALS,
+                   launch_chan_partials(s->stream, 2, s->raw, s->W, s->shift, s->base, nullptr, nsub, nchan, nbin,
+                                        s->part, s->part2, s->wpart));
+        }
         if (int rc = window_stage(s, s->wflag)) return rc;
         LAUNCH(s, K_BASE,
                launch_base(s->stream, s->raw, s->shift, s->win, s->wflag, nsub, nchan, nbin, s->width, s->base));
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, 1, s->raw, s->W, s->shift, s->base, s->wflag, nsub, nchan, nbin,
-                                    nullptr, s->part2, s->wpart));
+                                    nullptr, s->part2, s->wpart, nullptr, 0, 0, nullptr, s->exF));
     }
     return scrunch_stage(s);
 }
@@ -853,6 +867,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     linestats_knobs(s->ls_knobs);
     if (const char *e = getenv("IC_FIT_TAIL"))   // A/B knob: the tail hand-over threshold (ic_set_fit_tail)
         if (*e) s->tail_threshold = atol(e);
+    if (const char *e = getenv("IC_TEMPLATE_INCR"))   // A/B knob: 0 = full template passes every iteration
+        if (*e) s->incr = atoi(e) != 0;
     if (const char *e = getenv("IC_DIAG_FORK"))   // A/B knob: fork round of the diagnostics (0 = no fork)
         if (*e) s->diag_fork = atoi(e) > 0 ? atoi(e) : 0;
     if (const char *e = getenv("IC_FORK_DELAY"))
@@ -960,6 +976,12 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->win, (size_t)nsub);
     AL(s->wflag, (size_t)nsub + 1);   // + window-moves counter
     AL(s->part, (size_t)nsub * s->nsb * nbin);
+    if (s->incr && !s->fftded) {
+        AL(s->exA, (size_t)nsub * s->nsb * nbin);
+        AL(s->exF, (size_t)nsub * s->nsb * nbin);
+    } else {
+        s->incr = false;
+    }
     AL(s->part2, (size_t)nsub * s->nsb * nbin);
     AL(s->wpart, (size_t)nsub * s->nsb);
     AL(s->F, (size_t)nsub * nbin);
