@@ -2514,7 +2514,11 @@ __device__ __forceinline__ T chain_total(const T (&cs)[P2<N>::CPL], T *red, int 
 // stw: this stage's twiddles w^(r k), w = exp(-2 pi i/(R NS)), as [k][r-1]
 // (host-built in long double; no recurrences).  FIRST: the input is the real
 // signal X (f32, padded addresses) minus mu, read as complex pairs.
-template <int R, int NS, bool FIRST, int M, int TPP, typename XT>
+// DER: only each butterfly's base twiddle w = stw[k][0] is read; w^2 .. w^(R-1)
+// come from repeated complex products (a few ulp off the table's correctly
+// rounded values: the FFT diagnostic is compared within 1e-9, and this trades
+// R - 2 LDS reads for 4 (R - 2) VALU ops per butterfly)
+template <int R, int NS, bool FIRST, int M, int TPP, typename XT, bool DER = false>
 __device__ __forceinline__ void p2_stage(double2 *C, const XT *X, double mu, const double2 *stw, int t)
 {
     constexpr int NB = M / R;
@@ -2553,8 +2557,18 @@ __device__ __forceinline__ void p2_stage(double2 *C, const XT *X, double mu, con
             const int k = b & (NS - 1);
             if (NS > 1) {
                 const double2 *tk = stw + k * (R - 1);
+                if constexpr (DER) {
+                    const double2 w1 = tk[0];
+                    double2 wr = w1;
 #pragma unroll
-                for (int r = 1; r < R; ++r) v[u][r] = cmul_f(v[u][r], tk[r - 1]);
+                    for (int r = 1; r < R; ++r) {
+                        if (r > 1) wr = cmul_f(wr, w1);
+                        v[u][r] = cmul_f(v[u][r], wr);
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 1; r < R; ++r) v[u][r] = cmul_f(v[u][r], tk[r - 1]);
+                }
             }
             dft_small<R>(v[u]);
             const int idx = (b - k) * R + k;
@@ -2582,15 +2596,15 @@ __device__ __forceinline__ void p2_stage(double2 *C, const XT *X, double mu, con
 
 // the whole N/2-point FFT as a compile-time chain of stages (radix 8 while >= 3
 // levels remain, then 4 or 2); OFF = offset of the next stage table in tw
-template <int M, int TPP, int LG, int DONE, int NS, int OFF, typename XT>
+template <int M, int TPP, int LG, int DONE, int NS, int OFF, typename XT, bool DER = false>
 __device__ __forceinline__ void p2_fft(double2 *C, const XT *X, double mu, const double2 *tw, int t)
 {
     if constexpr (DONE < LG) {
         constexpr int REM = LG - DONE;
         constexpr int R = REM >= 3 ? 8 : (REM == 2 ? 4 : 2);
         constexpr int LR = R == 8 ? 3 : (R == 4 ? 2 : 1);
-        p2_stage<R, NS, DONE == 0, M, TPP, XT>(C, X, mu, tw + OFF, t);
-        p2_fft<M, TPP, LG, DONE + LR, NS * R, (NS > 1 ? OFF + NS * (R - 1) : OFF), XT>(C, X, mu, tw, t);
+        p2_stage<R, NS, DONE == 0, M, TPP, XT, DER>(C, X, mu, tw + OFF, t);
+        p2_fft<M, TPP, LG, DONE + LR, NS * R, (NS > 1 ? OFF + NS * (R - 1) : OFF), XT, DER>(C, X, mu, tw, t);
     }
 }
 
@@ -2998,6 +3012,15 @@ constexpr int p2_tw_entries(int N)
 #ifndef IC_CL_PROBE
 #define IC_CL_PROBE 0
 #endif
+// Stage and spectrum twiddles derived from one base twiddle per butterfly /
+// lane (p2_stage DER; tw[t + L j] = tw[t] exp(-2 pi i j / 16)) instead of one
+// read each: for the multi-wave groups (N >= 2048), whose table is read
+// through L1/L2 (C5 k_diag 2.81 -> 2.68 ms per launch); at N = 1024, whose
+// table is in LDS, it measured no faster (2.005 -> 2.03).  IC_CL_TWDER: -1 =
+// that rule, 0 / 1 = off / on for every N (A/B knob)
+#ifndef IC_CL_TWDER
+#define IC_CL_TWDER -1
+#endif
 template <int N>
 struct CLay {
     static constexpr int L = N / 16;     // threads per profile = chains of 16 samples
@@ -3027,6 +3050,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
     using C = CLay<N>;
     constexpr int L = C::L, WPP = C::WPP, M = C::M;
     constexpr bool closed = MODE == DIAG_CLOSED;
+    constexpr bool twder = IC_CL_TWDER < 0 ? WPP > 1 : IC_CL_TWDER != 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double2 *tw = C::TWG ? a.tw_p2 : (const double2 *)smem;
     const int lane = threadIdx.x & 63;
@@ -3212,7 +3236,8 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
                 for (int r8 = 0; r8 < 8; ++r8) Cb[A ^ r8] = v[r8];
             }
             gsync<WPP>();
-            if (IC_CL_PROBE != 3) p2_fft<M, L, C::LG, 3, 8, M, float>(Cb, (const float *)nullptr, 0.0, tw, t);
+            if (IC_CL_PROBE != 3)
+                p2_fft<M, L, C::LG, 3, 8, M, float, twder>(Cb, (const float *)nullptr, 0.0, tw, t);
             // spectrum in conjugate bin pairs (k_diag_p2).  No NaN bookkeeping:
             // a finite f32 sum s32 means every X is finite, and then every d,
             // Z and |X_k|^2 is finite (|X_k|^2 < 1e85); a non-finite s32 (a NaN or
@@ -3232,12 +3257,24 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
                 const double b2 = __builtin_fma(rm, rm, imm * imm);
                 best2 = fmax(best2, fmax(a2, b2));
             };
+            static_assert(JF == 4 && 16 * L == N, "tw[t + L j] = tw[t] exp(-2 pi i j / 16)");
+            const double2 wt = tw[t];
 #pragma unroll
             for (int j = 0; j < JF; ++j) {
                 const int kk = t + L * j;
                 const double2 zk = Cb[cidx(t) + L * j];
                 const double2 zm = Cb[kk == 0 ? 0 : cidx(L - t) + (M - L * (j + 1))];
-                post(zk, zm, tw[kk]);
+                if (twder) {
+                    // exp(-2 pi i j / 16), j = 0..3
+                    constexpr double c16[4] = {1.0, 0.92387953251128675613, 0.70710678118654752440,
+                                               0.38268343236508977173};
+                    constexpr double s16[4] = {0.0, 0.38268343236508977173, 0.70710678118654752440,
+                                               0.92387953251128675613};
+                    const double2 wj = make_double2(c16[j], -s16[j]);
+                    post(zk, zm, j == 0 ? wt : cmul_f(wt, wj));
+                } else {
+                    post(zk, zm, tw[kk]);
+                }
             }
             {
                 // the self-paired bin k = M/2 (one task): post(Z, Z, w) with the
