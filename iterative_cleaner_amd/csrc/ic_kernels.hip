@@ -2680,12 +2680,23 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
 #pragma unroll
         for (int u = 0; u < NPT; ++u) pv[u] = pn[t + TPP * u];
     };
-    unsigned k = __builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group);
+    // profiles: all P, or the slots of a list, minus those with skip[k] != 0
+    // (the two passes of the exact fit's forked diagnostics)
+    const RoundList rl(a.list, a.nctr, (long)P);
+    const unsigned nslot = (unsigned)rl.n();
+    const uint8_t *skip = a.skip;
+    auto next_slot = [&](unsigned sl) {   // the first slot >= sl this group measures (uniform)
+        if (skip)
+            while (sl < nslot && skip[rl.at(sl)]) sl += stride;
+        return sl;
+    };
+    unsigned slot = next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
+    unsigned k = slot < nslot ? (unsigned)rl.at(slot) : 0u;
     // per-profile scalars, loaded one profile ahead as well
     double nx = 0.0;
     int nst = 0, nsh = 0;
     float nw = 0.0f, nb = 0.0f;
-    if (k < P) {
+    if (slot < nslot) {
         if (PREFETCH) {
             loadrow(k);
         }
@@ -2697,7 +2708,8 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         nw = a.w0[k];
         nsh = (mode == DIAG_STATS || mode == DIAG_FIT) ? 0 : a.shift[k % (unsigned)nchan];
     }
-    for (; k < P; k += stride) {
+    for (unsigned snext = 0; slot < nslot; slot = snext, k = slot < nslot ? (unsigned)rl.at(slot) : 0u) {
+        snext = next_slot(slot + stride);
         // opaque to the optimiser: the LDS addresses of the FFT stages derive
         // from t, and hoisting all of them out of the loop costs ~100 VGPRs
         // (spills at N >= 2048); recomputing them is a few VALU ops each
@@ -2750,7 +2762,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             gsync<WPP>();
         }
         if constexpr (mode == DIAG_FIT) {   // the amplitude is all this mode produces
-            if (PREFETCH && k + stride < P) loadrow(k + stride);
+            if (PREFETCH && snext < nslot) loadrow((unsigned)rl.at(snext));
             continue;
         }
         const bool ok = st >= 1 && st <= 4;
@@ -2820,8 +2832,8 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
                 X[xw(u)] = weigh(R);
             }
         }
-        if (k + stride < P) {
-            const unsigned kn = k + stride;
+        if (snext < nslot) {
+            const unsigned kn = (unsigned)rl.at(snext);
             if (PREFETCH) loadrow(kn);
             if (mode == DIAG_EXACT) {
                 nx = a.amp[kn];
@@ -3012,6 +3024,14 @@ constexpr int p2_tw_entries(int N)
 #ifndef IC_CL_PROBE
 #define IC_CL_PROBE 0
 #endif
+// closed mode: the dedispersed-order samples of the row from an LDS copy of
+// the registers' dispersed-order ones (1) or a second global read (0).  The
+// second read misses L2 often enough to add 15 % to the pass's HBM traffic,
+// but the copy costs LDS bandwidth, which binds at N = 1024 (C2 fast mode
+// 2.48 -> 2.62 ms per pass with the copy; C5 3.09 -> 3.03): off (A/B knob)
+#ifndef IC_CL_PSTAGE
+#define IC_CL_PSTAGE 0
+#endif
 // Stage and spectrum twiddles derived from one base twiddle per butterfly /
 // lane (p2_stage DER; tw[t + L j] = tw[t] exp(-2 pi i j / 16)) instead of one
 // read each: for the multi-wave groups (N >= 2048), whose table is read
@@ -3128,11 +3148,30 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
         if constexpr (closed) {
             // a = sum(T*p)/sum(T*T) over the dedispersed-frame chains i = jb + 8q,
             // p_i = f32(raw[(i + sh) mod N] - base)
-            const float *row = a.raw + (size_t)k * N;
             const unsigned j0 = (unsigned)(jb + sh);
             float pi[16];
+            if (IC_CL_PSTAGE) {
+                // the row, in registers in dispersed order, through the group's work
+                // area: element j at j ^ (((j >> 7) & 7) << 3), conflict-free for the
+                // chain stores and the rotated loads
+                float *pst = (float *)gb;
+                gsync<WPP>();   // the previous profile's spectrum reads are done
 #pragma unroll
-            for (int q = 0; q < 16; ++q) pi[q] = row[(j0 + 8u * q) & (unsigned)(N - 1)];
+                for (int q = 0; q < 16; ++q) {
+                    const int j = jb + 8 * q;
+                    pst[j ^ (((j >> 7) & 7) << 3)] = pv[q];
+                }
+                gsync<WPP>();
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int j = (int)((j0 + 8u * q) & (unsigned)(N - 1));
+                    pi[q] = pst[j ^ (((j >> 7) & 7) << 3)];
+                }
+            } else {
+                const float *row = a.raw + (size_t)k * N;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) pi[q] = row[(j0 + 8u * q) & (unsigned)(N - 1)];
+            }
             double r = a.T64[jb] * (double)(pi[0] - bk);
 #pragma unroll
             for (int q = 1; q < 16; ++q) {
@@ -4622,7 +4661,12 @@ static bool uses_cl(const DiagArgs &a)
            (a.nbin == 1024 || a.nbin == 2048 || a.nbin == 4096) && diag_cl_enabled();
 }
 
-bool diag_list_supported(const DiagArgs &a) { return uses_cl(a); }
+// profile lists / skips: k_diag_cl, and k_diag_p2 in the exact mode
+bool diag_list_supported(const DiagArgs &a)
+{
+    const int n = a.nbin;
+    return uses_cl(a) || (a.mode == DIAG_EXACT && n >= 64 && n <= 4096 && (n & (n - 1)) == 0);
+}
 
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
 {
@@ -4639,7 +4683,7 @@ hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
         if (nbin == 2048) return launch_cl<2048>(st, a, P);
         if (nbin == 4096) return launch_cl<4096>(st, a, P);
     }
-    if (a.list || a.skip) return hipErrorInvalidValue;   // lists / skips: k_diag_cl only (diag_list_supported)
+    if ((a.list || a.skip) && !diag_list_supported(a)) return hipErrorInvalidValue;
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
         if (a.data_f64 && a.mode != DIAG_FIT) return launch_p2<NN, true>(st, a, P);                \

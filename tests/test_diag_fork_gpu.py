@@ -3,7 +3,8 @@ fit round the profiles already fitted are measured on a second stream while
 the late rounds and the tail run, the rest after the fit.  Every output must be
 the same bits as the unforked schedule (IC_DIAG_FORK=0), at every fork round,
 with both tail schedules, at the chain-layout profile lengths (1024, 2048,
-4096), and against the C oracle on whole subints."""
+4096) and the row-layout ones (256, 512: k_diag_p2), and against the C oracle
+on whole subints."""
 import numpy as np
 import pytest
 
@@ -29,7 +30,8 @@ def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1):
     return raw, w0, shift, out, amp, info, diag, stats
 
 
-@pytest.mark.parametrize("shape", [(16, 256, 1024), (6, 256, 2048), (4, 192, 4096)])
+@pytest.mark.parametrize("shape", [(16, 256, 1024), (6, 256, 2048), (4, 192, 4096), (24, 256, 256),
+                                   (16, 300, 512)])
 @pytest.mark.parametrize("tail", [0, 512, None])
 def test_fork_is_bit_identical(monkeypatch, shape, tail):
     ref = _run(monkeypatch, shape, 0, tail)
