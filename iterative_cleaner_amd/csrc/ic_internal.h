@@ -198,7 +198,8 @@ hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, in
 // T2 (optional): [2 nbin] receives T64[0..nbin) twice
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
                            double *T64, double *T2 = nullptr);
-hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P);
+hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P, int32_t *z32 = nullptr,
+                           int nz32 = 0, uint8_t *late = nullptr);
 // S.U from the template (one block; before round 0 of every fit)
 hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double *T64, int nbin);
 // list == nullptr: all P profiles (round 0); else the list written by the

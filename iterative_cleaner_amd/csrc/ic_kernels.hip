@@ -254,6 +254,10 @@ __global__ __launch_bounds__(256) void k_chan_partials(
 // afterwards (k_chan_partials mode 1, flagged).  wpart is summed again (256
 // weights).  One block per (bin range, super-block, subint); a block whose
 // super-block has no changed channel does nothing.
+// BPT bins per thread (bin i0 + 256 b, b < BPT): the change list and the
+// block's fixed costs serve BPT times the columns, and BPT times the loads are
+// in flight per batch of channels
+template <int BPT>
 __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ raw, const int32_t *__restrict__ shift,
                                                     const float *__restrict__ base, const float *__restrict__ Wn,
                                                     const float *__restrict__ Wo, int nchan, int nbin, int nsb,
@@ -262,25 +266,29 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                                                     const uint8_t *__restrict__ exF)
 {
     __shared__ int chg[kSuperBlock];
-    __shared__ int fix[256];                 // columns summed again: bin | 1 << 16 (part) | 1 << 17 (part2)
+    __shared__ int fix[256 * BPT];           // columns summed again: bin | 1 << 16 (part) | 1 << 17 (part2)
     __shared__ double tA[kSuperBlock], tF[kSuperBlock];
     __shared__ int wcnt[4], wfrac[4], wfix[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i0 = blockIdx.x * 256 * BPT + threadIdx.x;
     const int sb = blockIdx.y, s = blockIdx.z;
     const int c0 = sb * kSuperBlock, c1 = min(c0 + kSuperBlock, nchan);
     const size_t krow = (size_t)s * nchan;
+    const size_t col0 = ((size_t)s * nsb + sb) * nbin;
     // the changed channels of the super-block, in ascending order
-    int n, frac;
+    int n, frac, nones;
     {
         const int c = c0 + (int)threadIdx.x;
         const float wn = c < c1 ? Wn[krow + c] : 0.0f, wo = c < c1 ? Wo[krow + c] : 0.0f;
         const bool ch = __float_as_uint(wn) != __float_as_uint(wo);
         const bool fr = !(wn == 0.0f || wn == 1.0f) || !(wo == 0.0f || wo == 1.0f);
         const unsigned long long m = __ballot(ch);
+        const unsigned long long m1 = __ballot(wn == 1.0f);
+        const bool fw = __any(fr);
         if (lane == 0) {
             wcnt[wave] = __popcll(m);
-            wfrac[wave] = __any(fr) ? 1 : 0;
+            wfrac[wave] = fw ? 1 : 0;
+            wfix[wave] = __popcll(m1);
         }
         __syncthreads();
         int off = 0;
@@ -288,19 +296,23 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
         if (ch) chg[off + __popcll(m & ((1ull << lane) - 1ull))] = c;
         n = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
         frac = wfrac[0] | wfrac[1] | wfrac[2] | wfrac[3];
+        nones = wfix[0] + wfix[1] + wfix[2] + wfix[3];
         __syncthreads();
     }
     if (n == 0) return;
-    constexpr int B = 16;
+    constexpr int B = 16 / BPT;   // channels per batch: 16 loads in flight per thread
     if (frac) {
         // a weight other than 0 / 1: every column in canonical order (k_chan_partials' sums)
-        if (i < nbin) {
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+            const int i = i0 + 256 * b;
+            if (i >= nbin) continue;
             double acc = 0.0, acc2 = 0.0;
             int c = c0;
-            for (; c + B <= c1; c += B) {
-                float xv[B], wv[B], bv[B];
+            for (; c + 16 <= c1; c += 16) {
+                float xv[16], wv[16], bv[16];
 #pragma unroll
-                for (int q = 0; q < B; ++q) {
+                for (int q = 0; q < 16; ++q) {
                     int j = i + shift[c + q];
                     if (j >= nbin) j -= nbin;
                     xv[q] = raw[(krow + c + q) * nbin + j];
@@ -308,7 +320,7 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                     bv[q] = base[krow + c + q];
                 }
 #pragma unroll
-                for (int q = 0; q < B; ++q) {
+                for (int q = 0; q < 16; ++q) {
                     const double w = (double)wv[q];
                     const float d = xv[q] - bv[q];
                     acc = acc + w * (double)xv[q];
@@ -324,54 +336,75 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                 acc = acc + w * (double)x;
                 acc2 = acc2 + w * (double)d;
             }
-            const size_t col = ((size_t)s * nsb + sb) * nbin + i;
-            part[col] = acc;
-            part2[col] = acc2;
+            part[col0 + i] = acc;
+            part2[col0 + i] = acc2;
         }
     } else {
-        int need = 0;
-        if (i < nbin) {
-            const size_t col = ((size_t)s * nsb + sb) * nbin + i;
-            const bool okA = exA[col], okF = exF[col];
-            if (okA || okF) {
-                double dA = 0.0, dF = 0.0;
-                for (int q0 = 0; q0 < n; q0 += B) {
-                    float xv[B], bv[B], wnv[B], wov[B];
+        bool okA[BPT], okF[BPT];
+        double dA[BPT], dF[BPT];
 #pragma unroll
-                    for (int q = 0; q < B; ++q) {
-                        const int c = chg[min(q0 + q, n - 1)];
-                        int j = i + shift[c];
-                        if (j >= nbin) j -= nbin;
-                        xv[q] = raw[(krow + c) * nbin + j];
-                        bv[q] = base[krow + c];
-                        wnv[q] = Wn[krow + c];
-                        wov[q] = Wo[krow + c];
-                    }
+        for (int b = 0; b < BPT; ++b) {
+            const int i = i0 + 256 * b;
+            okA[b] = i < nbin && exA[col0 + i];
+            okF[b] = i < nbin && exF[col0 + i];
+            dA[b] = dF[b] = 0.0;
+        }
+        for (int q0 = 0; q0 < n; q0 += B) {
+            float xv[B][BPT], bv[B], wnv[B], wov[B];
 #pragma unroll
-                    for (int q = 0; q < B; ++q) {
-                        if (q0 + q < n) {
-                            const float d = xv[q] - bv[q];
-                            const double wn = (double)wnv[q], wo = (double)wov[q];
-                            dA = dA + (wn * (double)xv[q] - wo * (double)xv[q]);
-                            dF = dF + (wn * (double)d - wo * (double)d);
-                        }
+            for (int q = 0; q < B; ++q) {
+                const int c = chg[min(q0 + q, n - 1)];
+                bv[q] = base[krow + c];
+                wnv[q] = Wn[krow + c];
+                wov[q] = Wo[krow + c];
+                const float *row = raw + (krow + c) * nbin;
+                const int sc = shift[c];
+#pragma unroll
+                for (int b = 0; b < BPT; ++b) {
+                    const int i = min(i0 + 256 * b, nbin - 1);
+                    int j = i + sc;
+                    if (j >= nbin) j -= nbin;
+                    xv[q][b] = row[j];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < B; ++q) {
+                if (q0 + q < n) {
+                    const double wn = (double)wnv[q], wo = (double)wov[q];
+#pragma unroll
+                    for (int b = 0; b < BPT; ++b) {
+                        const float d = xv[q][b] - bv[q];
+                        dA[b] = dA[b] + (wn * (double)xv[q][b] - wo * (double)xv[q][b]);
+                        dF[b] = dF[b] + (wn * (double)d - wo * (double)d);
                     }
                 }
-                if (okA) part[col] = part[col] + dA;
-                if (okF) part2[col] = part2[col] + dF;
             }
-            need = (okA ? 0 : 1 << 16) | (okF ? 0 : 1 << 17);
+        }
+        int need[BPT];
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+            const int i = i0 + 256 * b;
+            need[b] = 0;
+            if (i < nbin) {
+                if (okA[b]) part[col0 + i] = part[col0 + i] + dA[b];
+                if (okF[b]) part2[col0 + i] = part2[col0 + i] + dF[b];
+                need[b] = (okA[b] ? 0 : 1 << 16) | (okF[b] ? 0 : 1 << 17);
+            }
         }
         // inexact columns: the whole block sums each again, one channel per
         // thread, then one thread adds the 256 terms in canonical order
-        const unsigned long long m = __ballot(need != 0);
-        if (lane == 0) wfix[wave] = __popcll(m);
-        __syncthreads();
-        int off = 0;
-        for (int w = 0; w < wave; ++w) off += wfix[w];
-        if (need) fix[off + __popcll(m & ((1ull << lane) - 1ull))] = need | i;
-        const int nfix = wfix[0] + wfix[1] + wfix[2] + wfix[3];
-        __syncthreads();
+        int nfix = 0;
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+            const unsigned long long m = __ballot(need[b] != 0);
+            if (lane == 0) wfix[wave] = __popcll(m);
+            __syncthreads();
+            int off = nfix;
+            for (int w = 0; w < wave; ++w) off += wfix[w];
+            if (need[b]) fix[off + __popcll(m & ((1ull << lane) - 1ull))] = need[b] | (i0 + 256 * b);
+            nfix += wfix[0] + wfix[1] + wfix[2] + wfix[3];
+            __syncthreads();
+        }
         for (int f = 0; f < nfix; ++f) {
             const int e = fix[f], ib = e & 0xffff;
             const int c = c0 + (int)threadIdx.x;
@@ -391,16 +424,19 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                     acc = acc + tA[q];
                     acc2 = acc2 + tF[q];
                 }
-                const size_t col = ((size_t)s * nsb + sb) * nbin + ib;
-                if (e & (1 << 16)) part[col] = acc;
-                if (e & (1 << 17)) part2[col] = acc2;
+                if (e & (1 << 16)) part[col0 + ib] = acc;
+                if (e & (1 << 17)) part2[col0 + ib] = acc2;
             }
             __syncthreads();
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        double a = 0.0;
-        for (int c = c0; c < c1; ++c) a = a + (double)Wn[krow + c];
+        // weights 0 / 1 only: the sequential sum is the count of ones, exactly
+        double a = (double)nones;
+        if (frac) {
+            a = 0.0;
+            for (int c = c0; c < c1; ++c) a = a + (double)Wn[krow + c];
+        }
         wpart[(size_t)s * nsb + sb] = a;
     }
 }
@@ -511,6 +547,10 @@ __global__ __launch_bounds__(kWindowThreads) void k_window(const double *__restr
 // 53 every partial sum, in any order, is representable and the result equals
 // the sequential one bit for bit.  Otherwise (rare: values spanning > 2^21, or
 // Inf/NaN) the profile's 16 lanes walk the window in order.
+// V4 (nbin % 4 == 0, 16-B aligned rows): the lanes read the aligned float4s
+// that cover the window (which wraps on a float4 boundary) and keep the
+// elements inside it; the exact path does not depend on the order of the adds.
+template <bool V4>
 __global__ __launch_bounds__(256) void k_base(const float *__restrict__ raw, const int32_t *__restrict__ shift,
                                               const int32_t *__restrict__ win, const int32_t *__restrict__ flags,
                                               int nsub, int nchan, int nbin, int width, float *__restrict__ base)
@@ -530,6 +570,37 @@ __global__ __launch_bounds__(256) void k_base(const float *__restrict__ raw, con
         if (act) {
             q0 = win[k / nchan] + shift[k % nchan];
             if (q0 >= nbin) q0 -= nbin;
+            if constexpr (V4) {
+                const float4 *row4 = (const float4 *)row;
+                const int nq = nbin >> 2, a = q0 >> 2, off = q0 & 3;
+                const int nf = (off + width + 3) >> 2;   // float4s covering the window
+                constexpr int B4 = 4;
+                for (int m0 = gl; m0 < nf; m0 += GL * B4) {
+                    float4 xv[B4];
+#pragma unroll
+                    for (int u = 0; u < B4; ++u) {
+                        const int m = m0 + GL * u;
+                        int qi = a + m;
+                        if (qi >= nq) qi -= nq;
+                        xv[u] = m < nf ? row4[qi] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    }
+#pragma unroll
+                    for (int u = 0; u < B4; ++u) {
+                        const int e0 = 4 * (m0 + GL * u) - off;   // window offset of the first element
+                        const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const float x = (e0 + c >= 0 && e0 + c < width) ? xs[c] : 0.0f;
+                            acc = acc + (double)x;
+                            const int be = max((int)((__float_as_uint(x) >> 23) & 0xffu), 1);
+                            if (x != 0.0f) {
+                                emax = max(emax, be);
+                                emin = min(emin, be);
+                            }
+                        }
+                    }
+                }
+            } else
             for (int j0 = gl; j0 < width; j0 += GL * BATCH) {
                 float xv[BATCH];
 #pragma unroll
@@ -1460,10 +1531,14 @@ struct RoundList {
 
 // request encoding in S.mode: ST_A0 / ST_A2 -> sweep A at S.xa; ST_B -> sweep B
 // at (S.x, S.aj); ST_DONE -> nothing.  S.slow: J at x came from an exact sweep.
-__global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P)
+// also zeroes the round counters (nz32 words) and the late flags (P bytes, optional)
+__global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P, int32_t *__restrict__ z32, int nz32,
+                                                  uint8_t *__restrict__ late)
 {
     const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nz32) z32[k] = 0;
     if (k >= P) return;
+    if (late) late[k] = 0;
     S.mode[k] = ST_A0;
     S.xa[k] = 1.0;
     S.x[k] = 1.0; S.par[k] = 0.0; S.iter[k] = 1; S.nfev[k] = 0; S.slow[k] = 0;
@@ -4448,8 +4523,17 @@ hipError_t launch_chan_delta(hipStream_t st, const float *raw, const int32_t *sh
     const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
     if (!exA || !exF) return hipErrorInvalidValue;
     // 256 threads: one per channel of the super-block (the change list), then one per bin
-    IC_GGL(k_chan_delta, dim3(cdiv(nbin, 256), nsb, nsub), dim3(256), 0, st, raw, shift, base, Wn, Wo, nchan, nbin,
-           nsb, part, part2, wpart, exA, exF);
+#ifndef IC_CD_BPT
+#define IC_CD_BPT 0   // bins per thread of k_chan_delta; 0: by nbin
+#endif
+    const int bpt = IC_CD_BPT > 0 ? IC_CD_BPT : (nbin >= 1024 ? 4 : (nbin >= 512 ? 2 : 1));
+#define IC_CD(BP)                                                                                                 \
+    IC_GGL(k_chan_delta<BP>, dim3(cdiv(nbin, 256 * BP), nsb, nsub), dim3(256), 0, st, raw, shift, base, Wn, Wo, \
+           nchan, nbin, nsb, part, part2, wpart, exA, exF)
+    if (bpt == 4) IC_CD(4);
+    else if (bpt == 2) IC_CD(2);
+    else IC_CD(1);
+#undef IC_CD
     return hipGetLastError();
 }
 
@@ -4468,7 +4552,13 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
 {
     const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 16), 16384);
-    IC_GGL(k_base, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
+#ifndef IC_BASE_V4
+#define IC_BASE_V4 1
+#endif
+    if (IC_BASE_V4 && nbin % 4 == 0 && ((uintptr_t)raw & 15) == 0 && width <= nbin)
+        IC_GGL(k_base<true>, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
+    else
+        IC_GGL(k_base<false>, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
     return hipGetLastError();
 }
 
@@ -4556,9 +4646,9 @@ hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int 
     return hipGetLastError();
 }
 
-hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P)
+hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P, int32_t *z32, int nz32, uint8_t *late)
 {
-    IC_GGL(k_fit_init, dim3(cdiv(P, 256)), dim3(256), 0, st, S, P);
+    IC_GGL(k_fit_init, dim3(cdiv(max(P, (long)nz32), 256)), dim3(256), 0, st, S, P, z32, nz32, late);
     return hipGetLastError();
 }
 

@@ -712,15 +712,14 @@ int run_fit(Session *s, const DiagArgs *fork)
     s->fork_round = -1;
     const long P = (long)s->P;
     const int nbin = s->p.nbin;
-    CK(launch_fit_init(s->stream, s->fs, P));
+    // zeroes too: per round, blocks done << 32 | survivors (the tail's sweep
+    // counter after them accumulates over the run: zeroed and read once per
+    // run by ic_run), and the late flags the fork round's state kernel sets
+    CK(launch_fit_init(s->stream, s->fs, P, s->rcount, 2 * kMaxRounds, fork ? s->late : nullptr));
     CK(launch_fit_prep(s->stream, s->fs, s->T64, nbin));
-    // per round: blocks done << 32 | survivors; then the tail's sweep counter,
-    // which accumulates over the run (zeroed and read once per run by ic_run)
-    CK(hipMemsetAsync(s->rcount, 0, sizeof(int32_t) * 2 * kMaxRounds, s->stream));
     unsigned long long *ctr = (unsigned long long *)s->rcount;
     unsigned long long *tail_sweeps = ctr + kMaxRounds;
     int32_t *bufs[3] = {s->lists, s->lists + P, s->lists + 2 * P};
-    if (fork) CK(hipMemsetAsync(s->late, 0, (size_t)P, s->stream));   // the fork round's state kernel sets them
     const int32_t *cur = nullptr;                    // round 0: all profiles
     const unsigned long long *cin = nullptr;         // the round's packed list counts (RoundList)
     long bound = P;                                 // >= the active count of the next round

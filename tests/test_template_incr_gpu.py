@@ -56,7 +56,8 @@ def _same(a, b):
         assert bits_equal(x, y)
 
 
-@pytest.mark.parametrize("shape", [(12, 600, 256), (10, 512, 1024), (6, 300, 100)])
+@pytest.mark.parametrize("shape", [(12, 600, 256), (10, 512, 1024), (6, 300, 100), (8, 520, 512), (6, 300, 1000),
+                                   (4, 260, 2048)])
 @pytest.mark.parametrize("rough", [False, True])
 def test_incremental_template_is_bit_identical(monkeypatch, shape, rough):
     raw, w0, shift = _cube(shape, 11, rough)
