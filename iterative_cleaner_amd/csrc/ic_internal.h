@@ -32,6 +32,7 @@ extern thread_local PendingTiming g_timing;
         }                                                                                                   \
     } while (0)
 
+constexpr int kDynChunk = 8;         // profile slots per take from a shared diagnostics counter
 constexpr int kSuperBlock = 256;    // canonical channel super-block (archive.py SUPER_BLOCK)
 constexpr int kMaxLeaves = 256;     // pairwise-sum leaves (nbin <= 32768)
 constexpr int kFitTile = 32;        // bins per k_fit_pass LDS tile (fit cube row padding)
@@ -199,7 +200,7 @@ hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, in
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
                            double *T64, double *T2 = nullptr);
 hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P, int32_t *z32 = nullptr,
-                           int nz32 = 0, uint8_t *late = nullptr);
+                           int nz32 = 0, uint8_t *late = nullptr, unsigned *dq = nullptr);
 // S.U from the template (one block; before round 0 of every fit)
 hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double *T64, int nbin);
 // list == nullptr: all P profiles (round 0); else the list written by the
@@ -255,10 +256,17 @@ struct DiagArgs {
     const int32_t *list = nullptr;
     const unsigned long long *nctr = nullptr;
     const uint8_t *skip = nullptr;   // != nullptr: profiles with skip[k] != 0 are left out
+    // != nullptr: the waves take chunks of profile slots from this counter
+    // instead of a fixed stride (diag_dyn_supported), so that two launches
+    // share the profiles (the fork's pass A and the steal after the fit)
+    unsigned *dq = nullptr;
+    int grid = 0;   // > 0: at most this many blocks
 };
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a);
 // the diagnostics kernel launch_diag picks for `a` takes a profile list
 bool diag_list_supported(const DiagArgs &a);
+// ... and takes its slots from a shared counter (DiagArgs::dq)
+bool diag_dyn_supported(const DiagArgs &a);
 // late != nullptr (launch_fit_state): late[k] = 1 for every survivor of the
 // round (the fork round; the flags were zeroed before it)
 // dynamic LDS the generic k_diag needs for one wave (0 for the power-of-two kernels)

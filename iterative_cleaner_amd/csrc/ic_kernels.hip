@@ -1533,10 +1533,11 @@ struct RoundList {
 // at (S.x, S.aj); ST_DONE -> nothing.  S.slow: J at x came from an exact sweep.
 // also zeroes the round counters (nz32 words) and the late flags (P bytes, optional)
 __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P, int32_t *__restrict__ z32, int nz32,
-                                                  uint8_t *__restrict__ late)
+                                                  uint8_t *__restrict__ late, unsigned *__restrict__ dq)
 {
     const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < nz32) z32[k] = 0;
+    if (k == 0 && dq) *dq = 0;
     if (k >= P) return;
     if (late) late[k] = 0;
     S.mode[k] = ST_A0;
@@ -3173,6 +3174,23 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
             while (sl < nslot && skip[rl.at(sl)]) sl += stride;
         return sl;
     };
+    // shared counter (one wave per group): chunks of kDynChunk slots
+    unsigned cpos = 0, cend = 0;
+    auto dyn_slot = [&]() {   // the next slot this wave measures (uniform), nslot at the end
+        for (;;) {
+            if (cpos >= cend) {
+                unsigned v = 0;
+                if (lane == 0) v = atomicAdd(a.dq, (unsigned)kDynChunk);
+                v = __builtin_amdgcn_readfirstlane(v);
+                if (v >= nslot) return nslot;
+                cpos = v;
+                cend = min(v + (unsigned)kDynChunk, nslot);
+            }
+            const unsigned sl = cpos++;
+            if (!skip || !skip[rl.at(sl)]) return sl;
+        }
+    };
+    const bool dyn = WPP == 1 && a.dq != nullptr;
     const int ca = t >> 3, cc = t & 7;
     const int jb = 128 * ca + cc;   // first sample of the thread's chain
     // byte offsets in the work array: d of chain sample q at wb[q & 3] + 64 (q & ~3)
@@ -3189,7 +3207,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
 #pragma unroll
         for (int q = 0; q < 16; ++q) pv[q] = IC_CL_PROBE == 2 ? (float)(q + kk) : pn[8 * q];
     };
-    unsigned slot = next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
+    unsigned slot = dyn ? dyn_slot() : next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
     unsigned k = slot < nslot ? (unsigned)rl.at(slot) : 0u;
     double nx = 0.0;
     int nst = 0, nsh = 0;
@@ -3284,7 +3302,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
             for (int q = 0; q < 16; ++q) X[q] = 0.0f * w;
         }
         const unsigned kc = k;   // this profile (the prefetch below moves k on)
-        snext = next_slot(slot + stride);
+        snext = dyn ? dyn_slot() : next_slot(slot + stride);
         if (snext < nslot) {
             const unsigned kn = (unsigned)rl.at(snext);
             k = kn;
@@ -4646,9 +4664,10 @@ hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int 
     return hipGetLastError();
 }
 
-hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P, int32_t *z32, int nz32, uint8_t *late)
+hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P, int32_t *z32, int nz32, uint8_t *late,
+                           unsigned *dq)
 {
-    IC_GGL(k_fit_init, dim3(cdiv(max(P, (long)nz32), 256)), dim3(256), 0, st, S, P, z32, nz32, late);
+    IC_GGL(k_fit_init, dim3(cdiv(max(P, (long)nz32), 256)), dim3(256), 0, st, S, P, z32, nz32, late, dq);
     return hipGetLastError();
 }
 
@@ -4727,7 +4746,8 @@ static hipError_t launch_cl(hipStream_t st, const DiagArgs &a, size_t P)
     using C = CLay<NN>;
     const int gpb = C::GPB;
     const size_t shm = (size_t)C::TW_LDS * 16 + gpb * (size_t)C::GROUP_BYTES;
-    const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
+    unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
+    if (a.grid > 0) grid = std::min(grid, (unsigned)a.grid);
     if (a.mode == DIAG_EXACT)
         IC_GGL((k_diag_cl<NN, DIAG_EXACT>), dim3(grid), dim3(C::L * gpb), shm, st, a);
     else
@@ -4758,6 +4778,9 @@ bool diag_list_supported(const DiagArgs &a)
     return uses_cl(a) || (a.mode == DIAG_EXACT && n >= 64 && n <= 4096 && (n & (n - 1)) == 0);
 }
 
+// a shared slot counter: k_diag_cl with one wave per profile
+bool diag_dyn_supported(const DiagArgs &a) { return uses_cl(a) && CLay<1024>::WPP == 1 && a.nbin == 1024; }
+
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
 {
     const int nbin = a.nbin;
@@ -4774,6 +4797,7 @@ hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
         if (nbin == 4096) return launch_cl<4096>(st, a, P);
     }
     if ((a.list || a.skip) && !diag_list_supported(a)) return hipErrorInvalidValue;
+    if (a.dq && !diag_dyn_supported(a)) return hipErrorInvalidValue;
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
         if (a.data_f64 && a.mode != DIAG_FIT) return launch_p2<NN, true>(st, a, P);                \

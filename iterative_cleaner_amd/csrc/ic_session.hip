@@ -146,6 +146,11 @@ struct Session {
     uint8_t *late = nullptr;       // [P] 1: still fitting after round diag_fork (pass A skips them)
     int fork_round = -1;           // this iteration's fork round (-1: none)
     int fork_delay = 1;            // rounds between the flags and pass A (A/B knob IC_FORK_DELAY)
+    // > 0 (A/B knob IC_FORK_GRID, nbin 1024): pass A runs as at most fork_grid
+    // blocks taking chunks of profiles from a shared counter (dq, after the
+    // round counters), and after the fit a full-grid launch takes the rest
+    int fork_grid = 0;
+    bool fork_dyn = false;         // this iteration's pass A uses the counter
     ic_run_stats stats{};
     std::vector<int32_t> bad_fits;   // per iteration of the last run: fit statuses outside 1-4
     // fractional dedispersion (dedisp_mode IC_DEDISP_FFT): the dedispersed raw
@@ -706,6 +711,7 @@ int shard_rowstats(Session *s, const LineStatsArgs &la)
 // already fitted run on s->dstream (fork_diag); the survivors of that round
 // are kept in the third list buffer for the main stream's second pass.
 int fork_diag(Session *s, const DiagArgs &da, int r);
+unsigned *diag_counter(Session *s) { return (unsigned *)(s->rcount + 2 * kMaxRounds + 2); }
 
 int run_fit(Session *s, const DiagArgs *fork)
 {
@@ -715,7 +721,8 @@ int run_fit(Session *s, const DiagArgs *fork)
     // zeroes too: per round, blocks done << 32 | survivors (the tail's sweep
     // counter after them accumulates over the run: zeroed and read once per
     // run by ic_run), and the late flags the fork round's state kernel sets
-    CK(launch_fit_init(s->stream, s->fs, P, s->rcount, 2 * kMaxRounds, fork ? s->late : nullptr));
+    CK(launch_fit_init(s->stream, s->fs, P, s->rcount, 2 * kMaxRounds, fork ? s->late : nullptr, diag_counter(s)));
+    s->fork_dyn = false;
     CK(launch_fit_prep(s->stream, s->fs, s->T64, nbin));
     unsigned long long *ctr = (unsigned long long *)s->rcount;
     unsigned long long *tail_sweeps = ctr + kMaxRounds;
@@ -795,6 +802,11 @@ int fork_diag(Session *s, const DiagArgs &da, int r)
     CK(hipStreamWaitEvent(s->dstream, s->fork_ev, 0));
     DiagArgs a = da;
     a.skip = s->late;
+    if (s->fork_grid > 0 && diag_dyn_supported(a)) {
+        a.dq = diag_counter(s);
+        a.grid = s->fork_grid;
+        s->fork_dyn = true;
+    }
     LAUNCH_ON(s, K_DIAG, s->dstream, launch_diag(s->dstream, a));
     CK(hipEventRecord(s->join_ev, s->dstream));
     s->fork_round = r;
@@ -872,6 +884,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         if (*e) s->diag_fork = atoi(e) > 0 ? atoi(e) : 0;
     if (const char *e = getenv("IC_FORK_DELAY"))
         if (*e && atoi(e) >= 0) s->fork_delay = atoi(e);
+    if (const char *e = getenv("IC_FORK_GRID"))
+        if (*e && atoi(e) >= 0) s->fork_grid = atoi(e);
     s->p = p;
     s->device = device;
     s->rank = rank;
@@ -1003,7 +1017,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     if (exact) AL(s->lists, 3 * P);   // two ping-pong round lists + the fork round's survivors
-    AL(s->rcount, (size_t)2 * kMaxRounds + 2);   // + the tail's sweep counter (u64)
+    AL(s->rcount, (size_t)2 * kMaxRounds + 4);   // + the tail's sweep counter (u64), the diagnostics counter
     if (exact && !s->fftded && s->diag_fork > 0) AL(s->late, P);
     if (sharded) {
         const char *cerr = nullptr;
@@ -1431,6 +1445,12 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             b.list = s->lists + 2 * s->P;
             b.nctr = (const unsigned long long *)s->rcount + s->fork_round;
             LAUNCH(s, K_DIAG, launch_diag(s->stream, b));
+            if (s->fork_dyn) {   // the profiles pass A has not taken yet
+                DiagArgs c = da;
+                c.skip = s->late;
+                c.dq = diag_counter(s);
+                LAUNCH(s, K_DIAG, launch_diag(s->stream, c));
+            }
             CK(hipStreamWaitEvent(s->stream, s->join_ev, 0));
         } else {
             LAUNCH(s, K_DIAG, launch_diag(s->stream, da));
