@@ -142,31 +142,65 @@ def s8d_bytes(name, nsub, nchan, nbin, launches, iterations, steps):
     return per_iter[name] * iterations * steps
 
 
-def algorithmic_bytes(name, nsub, nchan, nbin, launches, stats, steps):
-    """Bytes a kernel's launches actually sweep, summed over the timed region
+def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True):
+    """Bytes a kernel's launches actually move, summed over the timed region
     (kernel table) - the implementation's own traffic model, not
-    §8(d)'s.  k_fit_pass: every profile-sweep reads its 4*nbin-byte profile once
-    (sweep counts come from ic_get_run_stats)."""
+    §8(d)'s.  `run`: one clean's counts, {"n_iter", "changed" (per iteration),
+    "fit_profile_sweeps", "fit_tail_sweeps", "window_moves"} (ic_run /
+    ic_get_run_stats); every clean of the timed region is the same work.
+      k_fit_pass       every profile-sweep reads its 4*nbin-byte profile once;
+      k_fit_state      ~2 x 204 B of lmdif state per profile of a round (the
+                       rounds' inputs are the sweeps of k_fit_pass);
+      k_chan_partials  (every template-stage launch, k_chan_delta included)
+                       prepare's window pass reads the cube (4N); iteration 1's
+                       pass reads it and writes the fit cube (8N exact, 4N
+                       closed); from iteration 2 on k_chan_delta reads the rows
+                       of the profiles whose weight changed in the iteration
+                       before, and the flagged pass the subints whose baseline
+                       window moved; plus the super-block partials written;
+      k_base           the window samples of every profile (prepare) and of
+                       the subints whose window moved (later iterations);
+      k_diag           one full pass per iteration whatever the launches (the
+                       fork splits it in two): the raw cube + 44 B per profile."""
     P = nsub * nchan
     N = P * nbin
     nsb = (nchan + 255) // 256
-    per_launch = {
-        "k_chan_partials": 4 * N + 8 * nsub * nsb * nbin,
-        "k_base": int(4 * P * max(1, int(0.15 * nbin))),
-        "k_diag": 4 * N + 44 * P,
-        "k_linestats": 2 * 4 * 8 * P,
-        "k_combine": 4 * 8 * P + 2 * 4 * P,
-        "k_fit_state": 2 * 204 * P,
-    }
+    width = max(1, int(0.15 * nbin))
+    n_iter = run["n_iter"]
     if name == "k_fit_pass":
-        return 4 * nbin * stats["fit_profile_sweeps"] * steps
+        return 4 * nbin * run["fit_profile_sweeps"] * steps
     if name == "k_fit_tail":
-        return 4 * nbin * stats["fit_tail_sweeps"] * steps
-    if name == "k_chan_partials":   # + the fit cube written by iteration 1's pass (mode 3)
-        return per_launch[name] * launches + 4 * N * steps
+        return 4 * nbin * run["fit_tail_sweeps"] * steps
+    if name == "k_fit_state":
+        return 2 * 204 * run["fit_profile_sweeps"] * steps
+    if name == "k_chan_partials":
+        changed = sum(int(c) for c in run["changed"][:max(0, n_iter - 1)])
+        per_run = (4 * N + (8 * N if exact else 4 * N) + 4 * nbin * changed
+                   + 4 * nchan * nbin * run["window_moves"] + 16 * nsub * nsb * nbin * n_iter)
+        return per_run * steps
+    if name == "k_base":
+        return 4 * width * (P + nchan * run["window_moves"]) * steps
+    if name == "k_diag":
+        return (4 * N + 44 * P) * n_iter * steps
+    per_launch = {"k_linestats": 2 * 4 * 8 * P, "k_combine": 4 * 8 * P + 2 * 4 * P}
     if name in per_launch:
         return per_launch[name] * launches
     return None
+
+
+CACHE_RESIDENT_BYTES = 256 * 2 ** 20   # the Infinity Cache (MI355X_MICROARCH.md): a cube this small is served on-die
+
+
+def check_kernel_rates(per_kernel, cube_bytes):
+    """Per-kernel byte rates of the traffic model must stay under the HBM peak
+    for a cube that cannot sit in the Infinity Cache: a rate above it means the
+    model charges bytes the kernel does not move (round 3: k_chan_partials
+    charged a full cube per launch after the incremental stage had cut most of
+    them).  Returns the offending kernels; main() refuses to print such a line."""
+    bad = {k: v["sweep_gbs"] for k, v in per_kernel.items() if v.get("sweep_gbs") and v["sweep_gbs"] > HBM_PEAK_GBS}
+    if cube_bytes <= CACHE_RESIDENT_BYTES:
+        return {}, bad   # on-die re-reads may legitimately beat HBM
+    return bad, {}
 
 
 def pmc_traffic(workload, kernel):
@@ -282,20 +316,24 @@ def fast_mode_summary(_native, cube, w0, shift, shape, device, steps, torch, del
 EXCHANGE_KINDS = ("allgather", "alltoallv", "allreduce")
 
 
-def per_rank_report(ktimes, exch, rank, world, dev):
+def per_rank_report(ktimes, exch, rank, world, dev, wall_ms):
     """One clean's compute and exchange time on every rank (channel shards),
     gathered to every rank as a tensor: [{rank, world_size_seen (the process
-    group's), compute_ms (the shard kernels), exchange_ms / calls / MB per
-    collective type}], so that a multi-GPU line shows where each rank's time
-    went."""
+    group's), wall_ms (the clean, host clock), compute_ms (wall_ms minus the
+    exchanges), kernel_ms (the shard kernels' summed durations: above
+    compute_ms when kernels overlap, e.g. the forked diagnostics beside the
+    fit's late rounds), exchange_ms / calls / MB per collective type}], so that
+    a multi-GPU line shows where each rank's time went."""
     import torch
     import torch.distributed as dist
     ws = dist.get_world_size() if dist.is_initialized() else 1
-    compute = sum(v["ms"] for k, v in ktimes.items() if k.startswith("k_"))
-    row = [float(rank), float(ws), compute]
+    kernel = sum(v["ms"] for k, v in ktimes.items() if k.startswith("k_"))
+    exch_ms = sum(exch.get(kind, {"ms": 0.0})["ms"] for kind in EXCHANGE_KINDS)
+    row = [float(rank), float(ws), wall_ms - exch_ms, wall_ms, kernel]
     for kind in EXCHANGE_KINDS:
         e = exch.get(kind, {"ms": 0.0, "calls": 0, "bytes": 0})
         row += [e["ms"], float(e["calls"]), e["bytes"] / 1e6]
+    head = 5
     t = torch.tensor(row, dtype=torch.float64, device=dev if dist.get_backend() != "gloo" else "cpu")
     rows = [t] if world == 1 else [torch.empty_like(t) for _ in range(world)]
     if world > 1:
@@ -303,9 +341,10 @@ def per_rank_report(ktimes, exch, rank, world, dev):
     out = []
     for r in rows:
         v = r.cpu().tolist()
-        rec = {"rank": int(v[0]), "world_size_seen": int(v[1]), "compute_ms": round(v[2], 3), "exchange": {}}
+        rec = {"rank": int(v[0]), "world_size_seen": int(v[1]), "compute_ms": round(v[2], 3),
+               "wall_ms": round(v[3], 3), "kernel_ms": round(v[4], 3), "exchange": {}}
         for i, kind in enumerate(EXCHANGE_KINDS):
-            ms, calls, mb = v[3 + 3 * i: 6 + 3 * i]
+            ms, calls, mb = v[head + 3 * i: head + 3 + 3 * i]
             rec["exchange"][kind] = {"ms": round(ms, 3), "calls": int(calls), "MB": round(mb, 3)}
         out.append(rec)
     return out
@@ -495,11 +534,15 @@ def main():
         sess.set_timing(True)
         if sharded:
             comm.timing = True
+        torch.cuda.synchronize()
+        tb0 = time.perf_counter()
         sess.run(fetch=False)
+        torch.cuda.synchronize()
+        wall_ms = 1000.0 * (time.perf_counter() - tb0)
         ktimes_all = sess.kernel_times()
         if sharded:
             comm.timing = False
-            rank_report = per_rank_report(ktimes_all, comm.exchange_report(), rank, world, dev)
+            rank_report = per_rank_report(ktimes_all, comm.exchange_report(), rank, world, dev, wall_ms)
         kk = {k: v for k, v in ktimes_all.items() if k.startswith("k_") and v["launches"]}
         dom = max(kk, key=lambda k: kk[k]["ms"])
         sess.set_timing(True, only=dom)
@@ -527,6 +570,7 @@ def main():
         ktimes[dom] = ktimes_dom[dom]
     stats = sess.run_stats()
     n_iter = out["n_iter"]
+    run_counts = dict(stats, n_iter=n_iter, changed=[int(c) for c in out["changed"]])
     exact_weights = sess.run()["weights"] if fast is not None else None
     sess.close()
 
@@ -543,7 +587,8 @@ def main():
         dk = kernels[dom]
         avg_s = dk["ms"] / 1000.0 / max(1, dk["launches"])
         # implementation bytes (every sweep the kernel makes) and SURVEY §8(d) bytes
-        total_bytes = algorithmic_bytes(dom, nsub, lnchan, nbin, dk["launches"], stats, a.steps)
+        exact_mode = fit_mode == _native.FIT_EXACT
+        total_bytes = algorithmic_bytes(dom, nsub, lnchan, nbin, dk["launches"], run_counts, a.steps, exact_mode)
         sweep_launch = total_bytes / max(1, dk["launches"]) if total_bytes else None
         s8d_total = s8d_bytes(dom, nsub, lnchan, nbin, dk["launches"], n_iter, a.steps)
         s8d_launch = s8d_total / max(1, dk["launches"]) if s8d_total else None
@@ -553,7 +598,7 @@ def main():
         for kname, kv in ktimes.items():
             if kv["launches"] == 0:
                 continue
-            tb = algorithmic_bytes(kname, nsub, lnchan, nbin, kv["launches"], stats, a.steps)
+            tb = algorithmic_bytes(kname, nsub, lnchan, nbin, kv["launches"], run_counts, a.steps, exact_mode)
             pk = {"ms_per_step": round(kv["ms"] / a.steps, 3), "launches_per_step": kv["launches"] // a.steps,
                   "sweep_gbs": round(tb / (kv["ms"] / 1000.0) / 1e9, 1) if tb else None}
             sb = s8d_bytes(kname, nsub, lnchan, nbin, kv["launches"], n_iter, a.steps)
@@ -612,6 +657,12 @@ def main():
             roof["bound_note"] = ("measured HBM traffic %.2f of peak (re-sweeps included); frac/achieved use "
                                   "SURVEY §8(d) algorithmic bytes" % roof["traffic_frac"])
         roof["per_kernel"] = per_kernel
+        over, resident = check_kernel_rates(per_kernel, 4 * nsub * lnchan * nbin)
+        if over:
+            raise SystemExit("bench.py: per-kernel rates above the HBM peak (%s GB/s) on a %d-MB cube: the byte "
+                             "model is wrong: %s" % (HBM_PEAK_GBS, 4 * nsub * lnchan * nbin // 2 ** 20, over))
+        if resident:
+            roof["cache_resident_above_hbm_peak"] = resident
         roof["timing"] = ("%s: HIP events on the session stream over the timed region (only this kernel timed "
                           "there); per_kernel: one extra run with every kernel timed, scaled to the steps" % dom)
         iter_bytes = 8 * per_rank_P * nbin + 64 * per_rank_P    # SURVEY §8(d) B_iter, one GPU's share

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define IC_ABI_VERSION 5
+#define IC_ABI_VERSION 6
 
 #define IC_OK 0
 #define IC_EINVAL -1   /* bad argument / shape                         */
@@ -206,10 +206,45 @@ typedef struct {
 } ic_run_stats;
 int ic_get_run_stats(void *session, ic_run_stats *out);
 
-/* Scheduling knob of the exact fit: when at most `threshold` profiles still
- * need data sweeps, k_fit_tail finishes them in one launch (one wave per
- * profile) instead of further sweep/state rounds.  Results are identical either
- * way (both paths are bit-exact).  0 = never; default 8192. */
+/* Schedule options of a session.  They choose how the work of the loop is
+ * scheduled, never its arithmetic: every setting gives the same bits (the GPU
+ * tests hold each schedule equal to the default and to the oracle).  Set after
+ * ic_session_create; read by the following ic_run calls.  The library reads
+ * no environment variables.  ic_set_option fails with IC_EINVAL for an unknown
+ * option or a value out of range (given below), and on a session the option
+ * cannot serve.
+ *   IC_OPT_FIT_TAIL        profiles left when k_fit_tail takes over the exact
+ *                          fit (one wave per profile), >= 0, 0 = never; 8192
+ *   IC_OPT_DIAG_FORK       fit round after which the diagnostics of the fitted
+ *                          profiles run on a second stream, 0..64, 0 = no fork;
+ *                          3 (exact fit, integer dedispersion only)
+ *   IC_OPT_FORK_DELAY      rounds between that round and the forked pass, 0..8; 1
+ *   IC_OPT_TEMPLATE_INCR   1 = incremental template stage (integer
+ *                          dedispersion), 0 = full template passes; 1
+ *   IC_OPT_FIT_TILED       1 = tiled fit cube (integer dedispersion),
+ *                          0 = row-major; 1
+ *   IC_OPT_ROWSTAT_WAVES   waves per row median/MAD line: 0 (one wave), 4 or 8; 8
+ *   IC_OPT_ROWSTAT_MINLEN  shortest row that takes them, 1..16384; 1024
+ *   IC_OPT_DIAG_CHAIN      1 = chain-layout diagnostics kernel at nbin 1024,
+ *                          2048, 4096; 0 = the row-layout kernel; 1
+ *   IC_OPT_SYNC_TIMEOUT_MS longest host wait for the GPU, >= 1 ms; 600000.  A
+ *                          wait that runs out fails its call with IC_EHIP and
+ *                          marks the session failed: every later call on it
+ *                          but ic_session_destroy fails with IC_ESTATE, and
+ *                          destroy then leaks its device memory (its kernels may
+ *                          still be running) instead of freeing it. */
+#define IC_OPT_FIT_TAIL 1
+#define IC_OPT_DIAG_FORK 2
+#define IC_OPT_FORK_DELAY 3
+#define IC_OPT_TEMPLATE_INCR 4
+#define IC_OPT_FIT_TILED 5
+#define IC_OPT_ROWSTAT_WAVES 6
+#define IC_OPT_ROWSTAT_MINLEN 7
+#define IC_OPT_DIAG_CHAIN 8
+#define IC_OPT_SYNC_TIMEOUT_MS 9
+int ic_set_option(void *session, int option, int64_t value);
+int ic_get_option(void *session, int option, int64_t *value);
+/* = ic_set_option(session, IC_OPT_FIT_TAIL, threshold) */
 int ic_set_fit_tail(void *session, int64_t threshold);
 
 const char *ic_last_error(void);
@@ -231,6 +266,11 @@ int ic_fit_profiles(int device, int nprof, int nbin, const float *T, const float
 int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const float *data, const float *weights,
                            double chanthresh, double subintthresh, double *test_out, double *std_out,
                            double *mean_out, float *ptp_out, double *fftmax_out);
+/* The same with the row-median form of IC_OPT_ROWSTAT_WAVES / _MINLEN. */
+int ic_comprehensive_stats_rowstat(int device, int nsub, int nchan, int nbin, const float *data,
+                                   const float *weights, double chanthresh, double subintthresh, double *test_out,
+                                   double *std_out, double *mean_out, float *ptp_out, double *fftmax_out,
+                                   int rowstat_waves, int rowstat_minlen);
 
 /* ------------------------------------------------------------------------
  * Channel-sharded cleaning of ONE archive across `world` shards (config C3,

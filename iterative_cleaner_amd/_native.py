@@ -13,7 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # IC_LIBRARY: an alternative build of the same library (A/B measurements)
 LIB_PATH = os.environ.get("IC_LIBRARY") or os.path.join(HERE, "libicgpu.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # symbols exported by libicgpu.so, as declared in include/iterative_cleaner.h
 EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session_destroy",
@@ -24,7 +24,12 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free",
            "ic_upload_pols", "ic_comprehensive_stats", "ic_get_bad_fits",
            "ic_fit_profiles", "ic_get_diagnostics_f64", "ic_set_delays", "ic_rotate_profiles",
-           "ic_set_timing_kernel")
+           "ic_set_timing_kernel", "ic_set_option", "ic_get_option", "ic_comprehensive_stats_rowstat")
+
+# session schedule options (ic_set_option; include/iterative_cleaner.h): they
+# choose how the loop is scheduled, never its arithmetic
+OPTIONS = {"fit_tail": 1, "diag_fork": 2, "fork_delay": 3, "template_incr": 4, "fit_tiled": 5,
+           "rowstat_waves": 6, "rowstat_minlen": 7, "diag_chain": 8, "sync_timeout_ms": 9}
 
 FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)
 FIT_CLOSED = 1   # IC_FIT_CLOSED: closed-form amplitude fused with the diagnostics (fast mode)
@@ -125,6 +130,8 @@ def load_library(path: str = LIB_PATH):
     lib.ic_set_timing_kernel.argtypes = [vp, C.c_int]
     lib.ic_get_run_stats.argtypes = [vp, C.POINTER(RunStats)]
     lib.ic_set_fit_tail.argtypes = [vp, C.c_int64]
+    lib.ic_set_option.argtypes = [vp, C.c_int, C.c_int64]
+    lib.ic_get_option.argtypes = [vp, C.c_int, C.POINTER(C.c_int64)]
     lib.ic_upload_async.argtypes = [vp, vp, vp, vp]
     lib.ic_upload_pols.argtypes = [vp, vp, C.c_int, vp, vp]
     lib.ic_host_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
@@ -143,6 +150,8 @@ def load_library(path: str = LIB_PATH):
     lib.ic_rotate_profiles.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp]
     lib.ic_comprehensive_stats.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_double, C.c_double,
                                            vp, vp, vp, vp, vp]
+    lib.ic_comprehensive_stats_rowstat.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_double,
+                                                   C.c_double, vp, vp, vp, vp, vp, C.c_int, C.c_int]
     if lib.ic_abi_version() != ABI_VERSION:
         raise NativeError("libicgpu ABI %d != expected %d" % (lib.ic_abi_version(), ABI_VERSION))
     _lib = lib
@@ -178,7 +187,7 @@ class GpuSession:
 
     def __init__(self, nsub, nchan, nbin, max_iter=5, chanthresh=5.0, subintthresh=5.0,
                  pulse_region=(0, 0, 1), baseline_duty=0.15, device=0, fit_mode=FIT_EXACT, data_f64=False,
-                 delay=None):
+                 delay=None, options=None):
         self.lib = load_library()
         self.shape = (int(nsub), int(nchan), int(nbin))
         self.max_iter = int(max_iter)
@@ -193,6 +202,8 @@ class GpuSession:
         if rc != 0:
             raise NativeError("%s: %s (rc=%d)" % (self._create_name, _err(self.lib), rc))
         self.h = h
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
         if delay is not None:
             self._initial_delays(delay)
 
@@ -335,6 +346,17 @@ class GpuSession:
         """Profiles left at which k_fit_tail takes over the fit (0 = never)."""
         self._check(self.lib.ic_set_fit_tail(self.h, int(threshold)), "ic_set_fit_tail")
 
+    def set_option(self, name: str, value: int):
+        """A schedule option (OPTIONS; ic_set_option validates the value)."""
+        if name not in OPTIONS:
+            raise ValueError("unknown option %r (one of %s)" % (name, ", ".join(sorted(OPTIONS))))
+        self._check(self.lib.ic_set_option(self.h, OPTIONS[name], int(value)), "ic_set_option(%s)" % name)
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        self._check(self.lib.ic_get_option(self.h, OPTIONS[name], C.byref(v)), "ic_get_option(%s)" % name)
+        return int(v.value)
+
     def run_stats(self):
         st = RunStats()
         self._check(self.lib.ic_get_run_stats(self.h, C.byref(st)), "ic_get_run_stats")
@@ -387,10 +409,12 @@ def rotate_profiles(cube, delay, sign=1, device=0):
     return out
 
 
-def comprehensive_stats(data, weights, chanthresh=5.0, subintthresh=5.0, device=0, diagnostics=False):
+def comprehensive_stats(data, weights, chanthresh=5.0, subintthresh=5.0, device=0, diagnostics=False,
+                        rowstat_waves=8, rowstat_minlen=1024):
     """comprehensive_stats (iterative_cleaner.py:181-226) on the GPU for the
     (nsub, nchan, nbin) data and (nsub, nchan) weights the reference masks and
-    weights at :111-117; returns test [, (std, mean, ptp, fftmax)]."""
+    weights at :111-117; returns test [, (std, mean, ptp, fftmax)].
+    rowstat_*: the row-median form (IC_OPT_ROWSTAT_WAVES / _MINLEN)."""
     lib = load_library()
     data = np.ascontiguousarray(data, dtype=np.float32)
     if data.ndim != 3:
@@ -400,8 +424,9 @@ def comprehensive_stats(data, weights, chanthresh=5.0, subintthresh=5.0, device=
     test = np.empty((nsub, nchan), np.float64)
     sd, mn, ff = (np.empty((nsub, nchan), np.float64) for _ in range(3)) if diagnostics else (None,) * 3
     pt = np.empty((nsub, nchan), np.float32) if diagnostics else None
-    rc = lib.ic_comprehensive_stats(int(device), nsub, nchan, nbin, _ptr(data), _ptr(w), float(chanthresh),
-                                    float(subintthresh), _ptr(test), _ptr(sd), _ptr(mn), _ptr(pt), _ptr(ff))
+    rc = lib.ic_comprehensive_stats_rowstat(int(device), nsub, nchan, nbin, _ptr(data), _ptr(w),
+                                            float(chanthresh), float(subintthresh), _ptr(test), _ptr(sd),
+                                            _ptr(mn), _ptr(pt), _ptr(ff), int(rowstat_waves), int(rowstat_minlen))
     if rc != 0:
         raise NativeError("ic_comprehensive_stats: %s (rc=%d)" % (_err(lib), rc))
     return (test, (sd, mn, pt, ff)) if diagnostics else test

@@ -18,17 +18,22 @@ list): no collective.
 """
 from __future__ import annotations
 
-import os
 import queue
 import sys
 import threading
+import time
 
 import numpy as np
 
 from . import _native
 
-# how long closing the lanes waits for a worker's current ic_run (seconds)
-JOIN_TIMEOUT_S = float(os.environ.get("IC_BATCH_JOIN_TIMEOUT", "600"))
+# how long closing the lanes waits, in all, for the workers' current ic_run calls (seconds)
+JOIN_TIMEOUT_S = 600.0
+
+# sessions of lanes that were still inside ic_run when the lanes closed, with
+# every host array their queued copies and runs may still read: kept alive
+# (never freed, never destroyed) for the life of the process
+_LEAKED = []
 
 
 def pipeline(session, items, fetch=True):
@@ -47,7 +52,7 @@ def pipeline(session, items, fetch=True):
     yield session.run(fetch)
 
 
-def run_lanes(sessions, items, fetch=True, stop=None):
+def run_lanes(sessions, items, fetch=True, stop=None, join_timeout=None):
     """Clean every (cube, w0, shift) of `items` on `len(sessions)` sessions of one
     shape concurrently (one host thread per session, shared work queue; each
     session overlaps its next upload with its current run).  The arrays must
@@ -58,7 +63,11 @@ def run_lanes(sessions, items, fetch=True, stop=None):
     lanes stop: the `stop` event (created here if not given) is set, queued work
     is dropped, and the generator returns only after every worker thread has
     exited - a worker finishes at most the run it is in, so no thread is inside
-    ic_run when the caller closes the sessions."""
+    ic_run when the caller closes the sessions.  The workers share one deadline
+    (`join_timeout`, default JOIN_TIMEOUT_S): a lane still inside ic_run then is
+    leaked, its session marked (`_ic_leaked`, handle dropped so nothing
+    destroys it under the running call) and, with the arrays it was handed,
+    kept in _LEAKED."""
     if len(sessions) == 1:
         yield from pipeline(sessions[0], items, fetch)
         return
@@ -66,7 +75,9 @@ def run_lanes(sessions, items, fetch=True, stop=None):
     work = queue.Queue(maxsize=2 * len(sessions))
     done = queue.Queue()
 
-    def worker(sess):
+    held = [[] for _ in sessions]   # per lane: the arrays of its uploads not yet consumed by a run
+
+    def worker(lane, sess):
         pending = None   # index uploaded to this session, not yet run
         try:
             while not stop.is_set():
@@ -81,6 +92,8 @@ def run_lanes(sessions, items, fetch=True, stop=None):
                 if item is None or stop.is_set():
                     break
                 idx, arrays = item
+                held[lane].append(arrays)
+                del held[lane][:-3]             # an upload is consumed by the second run after it
                 sess.upload_async(*arrays)
                 if pending is not None:
                     done.put((pending, sess.run(fetch)))
@@ -91,7 +104,7 @@ def run_lanes(sessions, items, fetch=True, stop=None):
             stop.set()
             done.put((-1, e))
 
-    threads = [threading.Thread(target=worker, args=(sess,), daemon=True) for sess in sessions]
+    threads = [threading.Thread(target=worker, args=(q, sess), daemon=True) for q, sess in enumerate(sessions)]
     for th in threads:
         th.start()
     n = 0
@@ -156,14 +169,20 @@ def run_lanes(sessions, items, fetch=True, stop=None):
                 work.put_nowait(None)
             except queue.Full:
                 break
-        for th, sess in zip(threads, sessions):
-            th.join(timeout=JOIN_TIMEOUT_S)   # at most the run a worker is in
+        limit = JOIN_TIMEOUT_S if join_timeout is None else float(join_timeout)
+        deadline = time.monotonic() + limit   # one deadline for every lane
+        for q, (th, sess) in enumerate(zip(threads, sessions)):
+            th.join(timeout=max(0.0, deadline - time.monotonic()))   # at most the run a worker is in
             if th.is_alive():
                 # a worker stuck inside ic_run: leak its session (never destroyed
-                # under a running call) rather than hang the caller's cleanup
-                sys.stderr.write("iterative_cleaner: batch lane still inside ic_run after %.0f s; "
-                                 "leaking its session\n" % JOIN_TIMEOUT_S)
-                sess.h = None
+                # under a running call) and keep what it may still read alive,
+                # rather than hang the caller's cleanup
+                sys.stderr.write("iterative_cleaner: batch lane %d still inside ic_run after %.0f s; "
+                                 "leaking its session\n" % (q, limit))
+                _LEAKED.append((sess, getattr(sess, "h", None), list(held[q])))
+                if hasattr(sess, "h"):
+                    sess.h = None
+                sess._ic_leaked = True
         feeder.join(timeout=5.0)          # may wait in `items`: the caller's stop ends that
 
 
@@ -185,7 +204,7 @@ class _Ring:
 
 
 def clean_batch(loader, shape, device=0, ring=None, max_iter=5, chanthresh=5.0, subintthresh=5.0,
-                pulse_region=(0, 0, 1), baseline_duty=0.15, lanes=1):
+                pulse_region=(0, 0, 1), baseline_duty=0.15, lanes=1, join_timeout=None):
     """Clean the archives produced by `loader` (an iterable of (cube, w0, shift)
     host arrays of one (nsub, nchan, nbin) shape; shift is reduced mod nbin).
     A loader thread copies them into a ring of page-locked slots; the GPU
@@ -241,7 +260,7 @@ def clean_batch(loader, shape, device=0, ring=None, max_iter=5, chanthresh=5.0, 
         for _ in range(lanes):
             sessions.append(_native.GpuSession(nsub, nchan, nbin, max_iter, chanthresh, subintthresh,
                                                pulse_region, baseline_duty, device=device))
-        lanes_gen = run_lanes(sessions, staged(), stop=stop)
+        lanes_gen = run_lanes(sessions, staged(), stop=stop, join_timeout=join_timeout)
         for k, out in enumerate(lanes_gen):
             free.put(order[k])          # archive k's slot is free once its result is yielded
             yield out
@@ -256,4 +275,7 @@ def clean_batch(loader, shape, device=0, ring=None, max_iter=5, chanthresh=5.0, 
         th.join(timeout=60)
         for sess in sessions:
             sess.close()
-        rg.close()
+        if any(getattr(sess, "_ic_leaked", False) for sess in sessions):
+            _LEAKED.append(rg)          # a leaked lane's copies may still read the page-locked ring
+        else:
+            rg.close()

@@ -32,14 +32,9 @@ extern thread_local PendingTiming g_timing;
         }                                                                                                   \
     } while (0)
 
-constexpr int kDynChunk = 8;         // profile slots per take from a shared diagnostics counter
 constexpr int kSuperBlock = 256;    // canonical channel super-block (archive.py SUPER_BLOCK)
 constexpr int kMaxLeaves = 256;     // pairwise-sum leaves (nbin <= 32768)
 constexpr int kFitTile = 32;        // bins per k_fit_pass LDS tile (fit cube row padding)
-#ifndef IC_FIT_PAD_DEFAULT
-#define IC_FIT_PAD_DEFAULT 0
-#endif
-constexpr int kFitPad = IC_FIT_PAD_DEFAULT;   // extra bins per fit-cube row when ldD % 1024 == 0
 
 // Tiled fit cube (dtiled): profiles in groups of 64 (one k_fit_pass wave),
 // each group stored as ldD/32 tiles of [64 profiles][32 bins] (8 KiB), so a
@@ -132,14 +127,11 @@ struct LineStatsArgs {
     int ptp_f32;                    // 1: ptp lines use f32 arithmetic (numpy.ma on f32 data)
     double *col_med, *col_mad;      // [4][nchan]
     double *row_med, *row_mad;      // [4][nsub]
-    // row-median form (A/B knobs, read from the environment by linestats_knobs
-    // when a session is created, never per launch): grp_waves waves per line
-    // (0 = one wave per line, 4 or 8) for rows of >= grp_minlen values
+    // row-median form (session options IC_OPT_ROWSTAT_WAVES / _MINLEN, checked
+    // when set): grp_waves waves per line (0 = one wave per line, 4 or 8) for
+    // rows of >= grp_minlen values
     int grp_waves = 8, grp_minlen = 1024;
 };
-// IC_LS_GRP / IC_LS_GRP_MINLEN -> a.grp_waves / a.grp_minlen; an unsupported
-// IC_LS_GRP is reported on stderr and the default (8) kept
-void linestats_knobs(LineStatsArgs &a);
 
 // ---- launch wrappers (ic_kernels.hip); all asynchronous on `st` ----
 // mode 0: part = sum W*ded; 1: part2 = sum W*f32(ded-base) + wpart; 2: both;
@@ -200,23 +192,29 @@ hipError_t launch_sum_i32(hipStream_t st, const int32_t *gathered, int world, in
 hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int nsub, int nbin, float *T,
                            double *T64, double *T2 = nullptr);
 hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P, int32_t *z32 = nullptr,
-                           int nz32 = 0, uint8_t *late = nullptr, unsigned *dq = nullptr);
+                           int nz32 = 0, uint8_t *late = nullptr);
 // S.U from the template (one block; before round 0 of every fit)
 hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double *T64, int nbin);
+// Round counters of the exact fit (Session::rcount, int32 words): [0, 2K) the
+// packed list counts of every round (u64: [63:32] B requests at the list's
+// end, [31:0] A requests at its front), [2K, 3K) the blocks of each round's
+// k_fit_state that finished (u32), then the tail's sweep counter (u64, zeroed
+// once per run).  k_fit_init zeroes the first 3K words every iteration.
+constexpr int kMaxRounds = 1024;   // lmdif rounds per fit (maxfev = 400 bounds it far below)
+constexpr int kRoundWords = 3 * kMaxRounds;
 // list == nullptr: all P profiles (round 0); else the list written by the
 // previous round's k_fit_state, partitioned by request: nctr -> its packed
-// counts ([47:24] B requests at the list's end, [23:0] A requests at its
-// front), their sum <= bound (the host sizes grids from a count it already
-// knows: counts only shrink).
+// counts (above), their sum <= bound (the host sizes grids from a count it
+// already knows: counts only shrink).
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
                            const FitStateArrays &S);
-// ctr: zeroed device word, packed [63:48] finished blocks, [47:24] B survivors,
-// [23:0] A survivors (the next round's nctr); host_n: host-mapped int the
-// last block writes the survivor total to
+// ctr: zeroed device word, packed [63:32] B survivors, [31:0] A survivors
+// (the next round's nctr); done: zeroed word counting the finished blocks;
+// host_n: host-mapped int the last block writes the survivor total to
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const unsigned long long *nctr, long bound, double *amp, int32_t *info,
-                            int32_t *next_list, unsigned long long *ctr, int32_t *host_n,
+                            int32_t *next_list, unsigned long long *ctr, unsigned *done, int32_t *host_n,
                             uint8_t *late = nullptr);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
@@ -256,17 +254,11 @@ struct DiagArgs {
     const int32_t *list = nullptr;
     const unsigned long long *nctr = nullptr;
     const uint8_t *skip = nullptr;   // != nullptr: profiles with skip[k] != 0 are left out
-    // != nullptr: the waves take chunks of profile slots from this counter
-    // instead of a fixed stride (diag_dyn_supported), so that two launches
-    // share the profiles (the fork's pass A and the steal after the fit)
-    unsigned *dq = nullptr;
-    int grid = 0;   // > 0: at most this many blocks
+    int chain = 1;   // 0: the row-layout k_diag_p2 at nbin 1024/2048/4096 too (IC_OPT_DIAG_CHAIN)
 };
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a);
 // the diagnostics kernel launch_diag picks for `a` takes a profile list
 bool diag_list_supported(const DiagArgs &a);
-// ... and takes its slots from a shared counter (DiagArgs::dq)
-bool diag_dyn_supported(const DiagArgs &a);
 // late != nullptr (launch_fit_state): late[k] = 1 for every survivor of the
 // round (the fork round; the flags were zeroed before it)
 // dynamic LDS the generic k_diag needs for one wave (0 for the power-of-two kernels)

@@ -1499,13 +1499,13 @@ __device__ __forceinline__ void lm_store(const LmState &L, const FitStateArrays 
 // (list[0 .. nA)), B requests from the end down (list[P - 1 - j], j < nB), so
 // that the next round's waves hold one kind each (a wave with both runs both
 // sweep bodies; round 0's unanswered B requests and the profiles one stage
-// behind after them would otherwise spread over most waves).  Both counts and
-// the finished-block count share one 64-bit word (one atomic per block):
-// [63:48] blocks done, [47:24] nB, [23:0] nA (P < 2^24, checked by the host).
-__host__ __device__ constexpr unsigned long long rl_pack(unsigned long long blocks, unsigned long long nB,
-                                                         unsigned long long nA)
+// behind after them would otherwise spread over most waves).  Both counts
+// share one 64-bit word, [63:32] nB and [31:0] nA, so that one atomic per
+// block returns both list offsets; the blocks that finished are counted in a
+// word of their own (k_fit_state).
+__host__ __device__ constexpr unsigned long long rl_pack(unsigned long long nB, unsigned long long nA)
 {
-    return (blocks << 48) | (nB << 24) | nA;
+    return (nB << 32) | nA;
 }
 struct RoundList {
     const int32_t *list;
@@ -1517,8 +1517,8 @@ struct RoundList {
             nB = 0;
         } else {
             const unsigned long long v = *ctr;
-            nA = (long)(v & 0xffffffull);
-            nB = (long)((v >> 24) & 0xffffffull);
+            nA = (long)(v & 0xffffffffull);
+            nB = (long)(v >> 32);
         }
     }
     __device__ __forceinline__ long n() const { return nA + nB; }
@@ -1533,11 +1533,10 @@ struct RoundList {
 // at (S.x, S.aj); ST_DONE -> nothing.  S.slow: J at x came from an exact sweep.
 // also zeroes the round counters (nz32 words) and the late flags (P bytes, optional)
 __global__ __launch_bounds__(256) void k_fit_init(FitStateArrays S, long P, int32_t *__restrict__ z32, int nz32,
-                                                  uint8_t *__restrict__ late, unsigned *__restrict__ dq)
+                                                  uint8_t *__restrict__ late)
 {
     const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < nz32) z32[k] = 0;
-    if (k == 0 && dq) *dq = 0;
     if (k >= P) return;
     if (late) late[k] = 0;
     S.mode[k] = ST_A0;
@@ -1684,7 +1683,8 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
                                                             const unsigned long long *__restrict__ nctr,
                                                             double *__restrict__ amp_o, int32_t *__restrict__ info_o,
                                                             int32_t *__restrict__ next_list,
-                                                            unsigned long long *__restrict__ ctr, int32_t *host_n,
+                                                            unsigned long long *__restrict__ ctr,
+                                                            unsigned *__restrict__ done, int32_t *host_n,
                                                             uint8_t *__restrict__ late)
 {
     __shared__ int wcnt[FIT_STATE_BS / 64];
@@ -1801,17 +1801,24 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
             tot += wcnt[w];
             totB += wcntB[w];
         }
-        // one atomic per block: blocks done, B count, A count
-        const unsigned long long old = atomicAdd(ctr, rl_pack(1, (unsigned)totB, (unsigned)tot));
-        int base = (int)(old & 0xffffffull), baseB = (int)((old >> 24) & 0xffffffull);
+        // one atomic per block for both list offsets (B count, A count)
+        const unsigned long long old = atomicAdd(ctr, rl_pack((unsigned)totB, (unsigned)tot));
+        long base = (long)(old & 0xffffffffull), baseB = (long)(old >> 32);
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-            woff[w] = base;
+            woff[w] = (int)base;
             base += wcnt[w];
-            woffB[w] = baseB;
+            woffB[w] = (int)baseB;
             baseB += wcntB[w];
         }
-        if ((old >> 48) == (unsigned long long)nblk - 1)   // last block with work: the final counts
-            __hip_atomic_store(host_n, base + baseB, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // then the finished-block count: acq_rel orders every block's offset
+        // atomic before its count, so the last block's load of ctr below sees
+        // every block's survivors (the final counts of the round)
+        const unsigned fin = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (fin == (unsigned)nblk - 1) {
+            const unsigned long long v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(host_n, (int32_t)((v & 0xffffffffull) + (v >> 32)), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     __syncthreads();
     if (still) next_list[woff[wave] + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)k;
@@ -3174,23 +3181,6 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
             while (sl < nslot && skip[rl.at(sl)]) sl += stride;
         return sl;
     };
-    // shared counter (one wave per group): chunks of kDynChunk slots
-    unsigned cpos = 0, cend = 0;
-    auto dyn_slot = [&]() {   // the next slot this wave measures (uniform), nslot at the end
-        for (;;) {
-            if (cpos >= cend) {
-                unsigned v = 0;
-                if (lane == 0) v = atomicAdd(a.dq, (unsigned)kDynChunk);
-                v = __builtin_amdgcn_readfirstlane(v);
-                if (v >= nslot) return nslot;
-                cpos = v;
-                cend = min(v + (unsigned)kDynChunk, nslot);
-            }
-            const unsigned sl = cpos++;
-            if (!skip || !skip[rl.at(sl)]) return sl;
-        }
-    };
-    const bool dyn = WPP == 1 && a.dq != nullptr;
     const int ca = t >> 3, cc = t & 7;
     const int jb = 128 * ca + cc;   // first sample of the thread's chain
     // byte offsets in the work array: d of chain sample q at wb[q & 3] + 64 (q & ~3)
@@ -3207,7 +3197,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
 #pragma unroll
         for (int q = 0; q < 16; ++q) pv[q] = IC_CL_PROBE == 2 ? (float)(q + kk) : pn[8 * q];
     };
-    unsigned slot = dyn ? dyn_slot() : next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
+    unsigned slot = next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
     unsigned k = slot < nslot ? (unsigned)rl.at(slot) : 0u;
     double nx = 0.0;
     int nst = 0, nsh = 0;
@@ -3302,7 +3292,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
             for (int q = 0; q < 16; ++q) X[q] = 0.0f * w;
         }
         const unsigned kc = k;   // this profile (the prefetch below moves k on)
-        snext = dyn ? dyn_slot() : next_slot(slot + stride);
+        snext = next_slot(slot + stride);
         if (snext < nslot) {
             const unsigned kn = (unsigned)rl.at(snext);
             k = kn;
@@ -4664,10 +4654,9 @@ hipError_t launch_tscrunch(hipStream_t st, const float *F, const float *wf, int 
     return hipGetLastError();
 }
 
-hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P, int32_t *z32, int nz32, uint8_t *late,
-                           unsigned *dq)
+hipError_t launch_fit_init(hipStream_t st, const FitStateArrays &S, long P, int32_t *z32, int nz32, uint8_t *late)
 {
-    IC_GGL(k_fit_init, dim3(cdiv(max(P, (long)nz32), 256)), dim3(256), 0, st, S, P, z32, nz32, late, dq);
+    IC_GGL(k_fit_init, dim3(cdiv(max(P, (long)nz32), 256)), dim3(256), 0, st, S, P, z32, nz32, late);
     return hipGetLastError();
 }
 
@@ -4699,12 +4688,13 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
 
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const unsigned long long *nctr, long bound, double *amp, int32_t *info,
-                            int32_t *next_list, unsigned long long *ctr, int32_t *host_n, uint8_t *late)
+                            int32_t *next_list, unsigned long long *ctr, unsigned *done, int32_t *host_n,
+                            uint8_t *late)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
     IC_GGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nctr, amp,
-                       info, next_list, ctr, host_n, late);
+                       info, next_list, ctr, done, host_n, late);
     return hipGetLastError();
 }
 
@@ -4746,8 +4736,7 @@ static hipError_t launch_cl(hipStream_t st, const DiagArgs &a, size_t P)
     using C = CLay<NN>;
     const int gpb = C::GPB;
     const size_t shm = (size_t)C::TW_LDS * 16 + gpb * (size_t)C::GROUP_BYTES;
-    unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
-    if (a.grid > 0) grid = std::min(grid, (unsigned)a.grid);
+    const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
     if (a.mode == DIAG_EXACT)
         IC_GGL((k_diag_cl<NN, DIAG_EXACT>), dim3(grid), dim3(C::L * gpb), shm, st, a);
     else
@@ -4755,20 +4744,10 @@ static hipError_t launch_cl(hipStream_t st, const DiagArgs &a, size_t P)
     return hipGetLastError();
 }
 
-// IC_DIAG_CL=0 (read once): the row-layout k_diag_p2 for every nbin (A/B knob)
-static bool diag_cl_enabled()
-{
-    static const bool on = [] {
-        const char *e = getenv("IC_DIAG_CL");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-
 static bool uses_cl(const DiagArgs &a)
 {
     return (a.mode == DIAG_EXACT || a.mode == DIAG_CLOSED) && a.T2 && a.raw && a.base && !a.pr_on && !a.data_f64 &&
-           (a.nbin == 1024 || a.nbin == 2048 || a.nbin == 4096) && diag_cl_enabled();
+           (a.nbin == 1024 || a.nbin == 2048 || a.nbin == 4096) && a.chain;
 }
 
 // profile lists / skips: k_diag_cl, and k_diag_p2 in the exact mode
@@ -4777,9 +4756,6 @@ bool diag_list_supported(const DiagArgs &a)
     const int n = a.nbin;
     return uses_cl(a) || (a.mode == DIAG_EXACT && n >= 64 && n <= 4096 && (n & (n - 1)) == 0);
 }
-
-// a shared slot counter: k_diag_cl with one wave per profile
-bool diag_dyn_supported(const DiagArgs &a) { return uses_cl(a) && CLay<1024>::WPP == 1 && a.nbin == 1024; }
 
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
 {
@@ -4797,7 +4773,6 @@ hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
         if (nbin == 4096) return launch_cl<4096>(st, a, P);
     }
     if ((a.list || a.skip) && !diag_list_supported(a)) return hipErrorInvalidValue;
-    if (a.dq && !diag_dyn_supported(a)) return hipErrorInvalidValue;
 #define IC_P2(NN)                                                                                  \
     if (nbin == NN) {                                                                              \
         if (a.data_f64 && a.mode != DIAG_FIT) return launch_p2<NN, true>(st, a, P);                \
@@ -4835,22 +4810,6 @@ hipError_t launch_tnorm(hipStream_t st, const double *T64, const PwPlan *plan, i
     const size_t shm = (size_t)(nleaf_ub * 9 + nleaf_ub + 8) * 8;
     IC_GGL(k_tnorm, dim3(1), dim3(64), shm, st, T64, plan, TT);
     return hipGetLastError();
-}
-
-static int env_knob(const char *name, int dflt)
-{
-    const char *e = getenv(name);
-    return (e && *e) ? atoi(e) : dflt;
-}
-
-void linestats_knobs(LineStatsArgs &a)
-{
-    a.grp_waves = env_knob("IC_LS_GRP", 8);
-    a.grp_minlen = env_knob("IC_LS_GRP_MINLEN", 1024);
-    if (a.grp_waves != 0 && a.grp_waves != 4 && a.grp_waves != 8) {
-        fprintf(stderr, "iterative_cleaner: IC_LS_GRP=%d unsupported (0, 4 or 8); using 8\n", a.grp_waves);
-        a.grp_waves = 8;
-    }
 }
 
 hipError_t launch_linestats(hipStream_t st, const LineStatsArgs &a, int which)

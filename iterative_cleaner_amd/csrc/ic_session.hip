@@ -42,6 +42,12 @@ int fail(int code, const char *fmt, ...)
     return code;
 }
 
+// calls on a session whose host wait timed out (Session::failed)
+int failed_session()
+{
+    return fail(IC_ESTATE, "session failed: a host wait timed out with its kernels possibly still running; destroy it");
+}
+
 #define CK(call)                                                                                  \
     do {                                                                                          \
         hipError_t e_ = (call);                                                                   \
@@ -56,7 +62,6 @@ const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",
                                      "k_fit_tail",      "k_sb_tree",   "k_shard_pack", "exchange",
                                      "k_tnorm",         "k_rotate"};
 
-constexpr int kMaxRounds = 1024;      // lmdif rounds per fit (maxfev = 400 bounds it far below)
 constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
 
 struct Timed {
@@ -116,7 +121,7 @@ struct Session {
     PwPlan *plan = nullptr;
     FitStateArrays fs{};
     int32_t *lists = nullptr;   // two active-profile lists of P entries
-    int32_t *rcount = nullptr;  // u64 per round (blocks done << 32 | survivors) + tail sweep counter
+    int32_t *rcount = nullptr;  // round counters (ic_internal.h kRoundWords) + the tail's sweep counter
     int32_t *h_rcount = nullptr;  // host-mapped mirror, written by k_fit_state's last block
     int32_t *h_small = nullptr;   // pinned readback of the per-iteration counters and run stats
                                   // (a pageable D2H copy is staged synchronously, ~30 us each)
@@ -125,8 +130,14 @@ struct Session {
     void *fs_block = nullptr;   // one allocation backing fs
     int fit_rounds = 0;
     int plan_ub = 0;            // max(leaves, ops) of the pairwise plan (k_tnorm scratch)
-    LineStatsArgs ls_knobs;     // row-median form, from the environment at creation
-    long tail_threshold = kTailProfiles;
+    LineStatsArgs ls_knobs;     // row-median form (IC_OPT_ROWSTAT_*)
+    long tail_threshold = kTailProfiles;   // IC_OPT_FIT_TAIL
+    bool diag_chain = true;     // IC_OPT_DIAG_CHAIN: k_diag_cl at nbin 1024/2048/4096
+    double sync_timeout_s = 600.0;   // IC_OPT_SYNC_TIMEOUT_MS
+    // a host wait timed out with kernels of this session possibly still in
+    // flight: every later call but ic_session_destroy fails (IC_ESTATE), and
+    // destroy leaks the device buffers instead of freeing memory in use
+    bool failed = false;
     // diagnostics forked onto a second stream (exact fit): the state kernel
     // of round diag_fork (0 = off) flags the profiles still fitting; from
     // round diag_fork + fork_delay on the others are measured on dstream while
@@ -145,12 +156,7 @@ struct Session {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     uint8_t *late = nullptr;       // [P] 1: still fitting after round diag_fork (pass A skips them)
     int fork_round = -1;           // this iteration's fork round (-1: none)
-    int fork_delay = 1;            // rounds between the flags and pass A (A/B knob IC_FORK_DELAY)
-    // > 0 (A/B knob IC_FORK_GRID, nbin 1024): pass A runs as at most fork_grid
-    // blocks taking chunks of profiles from a shared counter (dq, after the
-    // round counters), and after the fit a full-grid launch takes the rest
-    int fork_grid = 0;
-    bool fork_dyn = false;         // this iteration's pass A uses the counter
+    int fork_delay = 1;            // rounds between the flags and pass A (IC_OPT_FORK_DELAY)
     ic_run_stats stats{};
     std::vector<int32_t> bad_fits;   // per iteration of the last run: fit statuses outside 1-4
     // fractional dedispersion (dedisp_mode IC_DEDISP_FFT): the dedispersed raw
@@ -237,31 +243,24 @@ static hipError_t take_event(Session *s, hipEvent_t *e)
 // per iteration boundary on the MI355X hosts): a busy poll for the first
 // 200 us (the common case: the GPU is a few kernels behind), then polls with
 // sched_yield between them, so a long wait does not hold a host core; after
-// IC_SYNC_TIMEOUT seconds (default 600) it gives up with hipErrorLaunchTimeOut,
-// so a kernel that never finishes fails the run instead of hanging its caller.
-static double sync_timeout_s()
-{
-    static const double t = [] {
-        const char *e = getenv("IC_SYNC_TIMEOUT");
-        const double v = (e && *e) ? atof(e) : 600.0;
-        return v > 0.0 ? v : 600.0;
-    }();
-    return t;
-}
-
-static hipError_t poll_event(hipEvent_t ev)
+// the session's sync timeout (IC_OPT_SYNC_TIMEOUT_MS, default 600 s) it gives
+// up with hipErrorLaunchTimeOut and marks the session failed, so a kernel
+// that never finishes fails the run instead of hanging its caller, and no
+// later call reuses buffers its kernels may still be using.
+static hipError_t poll_event(Session *s, hipEvent_t ev)
 {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     const auto spin = std::chrono::microseconds(200);
-    const auto limit = std::chrono::duration<double>(sync_timeout_s());
+    const auto limit = std::chrono::duration<double>(s->sync_timeout_s);
     hipError_t e;
     while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
         const auto dt = clk::now() - t0;
-        if (dt > spin) {
-            if (dt > limit) return hipErrorLaunchTimeOut;
-            sched_yield();
+        if (dt > limit) {
+            s->failed = true;
+            return hipErrorLaunchTimeOut;
         }
+        if (dt > spin) sched_yield();
     }
     return e;
 }
@@ -270,7 +269,7 @@ static hipError_t spin_sync(Session *s)
 {
     hipError_t e = hipEventRecord(s->sev, s->stream);
     if (e != hipSuccess) return e;
-    return poll_event(s->sev);
+    return poll_event(s, s->sev);
 }
 
 #ifndef IC_TIMING_MARKERS
@@ -711,7 +710,8 @@ int shard_rowstats(Session *s, const LineStatsArgs &la)
 // already fitted run on s->dstream (fork_diag); the survivors of that round
 // are kept in the third list buffer for the main stream's second pass.
 int fork_diag(Session *s, const DiagArgs &da, int r);
-unsigned *diag_counter(Session *s) { return (unsigned *)(s->rcount + 2 * kMaxRounds + 2); }
+// the tail's sweep counter, after the round counters (accumulates over a run)
+unsigned long long *tail_counter(Session *s) { return (unsigned long long *)(s->rcount + kRoundWords); }
 
 int run_fit(Session *s, const DiagArgs *fork)
 {
@@ -721,11 +721,11 @@ int run_fit(Session *s, const DiagArgs *fork)
     // zeroes too: per round, blocks done << 32 | survivors (the tail's sweep
     // counter after them accumulates over the run: zeroed and read once per
     // run by ic_run), and the late flags the fork round's state kernel sets
-    CK(launch_fit_init(s->stream, s->fs, P, s->rcount, 2 * kMaxRounds, fork ? s->late : nullptr, diag_counter(s)));
-    s->fork_dyn = false;
+    CK(launch_fit_init(s->stream, s->fs, P, s->rcount, kRoundWords, fork ? s->late : nullptr));
     CK(launch_fit_prep(s->stream, s->fs, s->T64, nbin));
     unsigned long long *ctr = (unsigned long long *)s->rcount;
-    unsigned long long *tail_sweeps = ctr + kMaxRounds;
+    unsigned *done = (unsigned *)(s->rcount + 2 * kMaxRounds);
+    unsigned long long *tail_sweeps = tail_counter(s);
     int32_t *bufs[3] = {s->lists, s->lists + P, s->lists + 2 * P};
     const int32_t *cur = nullptr;                    // round 0: all profiles
     const unsigned long long *cin = nullptr;         // the round's packed list counts (RoundList)
@@ -751,7 +751,7 @@ int run_fit(Session *s, const DiagArgs *fork)
                                                 s->fs));
         s->h_rcount[r] = -1;
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
-                                                ctr + r, s->d_h_rcount + r, fork_here ? s->late : nullptr));
+                                                ctr + r, done + r, s->d_h_rcount + r, fork_here ? s->late : nullptr));
         CK(hipEventRecord(s->rev[r & 1], s->stream));
         if (fork_here) flagged = r;
         // pass A is queued fork_delay rounds after the flags: the first late
@@ -765,7 +765,7 @@ int run_fit(Session *s, const DiagArgs *fork)
         cin = ctr + r;   // packed A / B counts of the next round's list
         if (r >= 1) {
             // count after round r-1 (= input of round r) bounds the count after round r
-            CK(poll_event(s->rev[(r - 1) & 1]));
+            CK(poll_event(s, s->rev[(r - 1) & 1]));
             const long c = s->h_rcount[r - 1];
             if (c == 0) break;   // round r had nothing to do
             bound = c;
@@ -802,11 +802,6 @@ int fork_diag(Session *s, const DiagArgs &da, int r)
     CK(hipStreamWaitEvent(s->dstream, s->fork_ev, 0));
     DiagArgs a = da;
     a.skip = s->late;
-    if (s->fork_grid > 0 && diag_dyn_supported(a)) {
-        a.dq = diag_counter(s);
-        a.grid = s->fork_grid;
-        s->fork_dyn = true;
-    }
     LAUNCH_ON(s, K_DIAG, s->dstream, launch_diag(s->dstream, a));
     CK(hipEventRecord(s->join_ev, s->dstream));
     s->fork_round = r;
@@ -875,17 +870,6 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(IC_EHIP, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
     Session *s = new Session();
-    linestats_knobs(s->ls_knobs);
-    if (const char *e = getenv("IC_FIT_TAIL"))   // A/B knob: the tail hand-over threshold (ic_set_fit_tail)
-        if (*e) s->tail_threshold = atol(e);
-    if (const char *e = getenv("IC_TEMPLATE_INCR"))   // A/B knob: 0 = full template passes every iteration
-        if (*e) s->incr = atoi(e) != 0;
-    if (const char *e = getenv("IC_DIAG_FORK"))   // A/B knob: fork round of the diagnostics (0 = no fork)
-        if (*e) s->diag_fork = atoi(e) > 0 ? atoi(e) : 0;
-    if (const char *e = getenv("IC_FORK_DELAY"))
-        if (*e && atoi(e) >= 0) s->fork_delay = atoi(e);
-    if (const char *e = getenv("IC_FORK_GRID"))
-        if (*e && atoi(e) >= 0) s->fork_grid = atoi(e);
     s->p = p;
     s->device = device;
     s->rank = rank;
@@ -910,14 +894,6 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     s->rows_own = rr[2 * rank + 1] - rr[2 * rank];
     s->rows_pad = (p.nsub + world - 1) / world;
     s->ldD = ((p.nbin + kFitTile - 1) / kFitTile) * kFitTile;
-    // row stride of the fit cube: off a multiple of 4 KiB (a fit sweep reads
-    // one 64-B piece of 64 consecutive rows at a time; at a 4-KiB stride those
-    // land on the same HBM channels).  IC_FIT_PAD: bins of padding (A/B knob).
-    {
-        const char *e = getenv("IC_FIT_PAD");
-        const int pad = e ? atoi(e) : kFitPad;
-        if (pad > 0 && pad % 4 == 0 && (s->ldD % 1024) == 0) s->ldD += pad;
-    }
     s->Ppad = ((s->P + 63) / 64) * 64;
     s->width = (int)(p.baseline_duty * (double)p.nbin);
     if (s->width < 1) s->width = 1;
@@ -937,7 +913,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (hipSetDevice(device) != hipSuccess) return bail(fail(IC_EHIP, "hipSetDevice(%d) failed", device));
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(IC_EHIP, "hipStreamCreate failed"));
-    if (p.fit_mode == IC_FIT_EXACT && p.dedisp_mode == IC_DEDISP_SHIFT && s->diag_fork > 0) {
+    // the diagnostics fork's stream exists for every session it can serve
+    // (IC_OPT_DIAG_FORK may switch it on or off before any run)
+    if (p.fit_mode == IC_FIT_EXACT && p.dedisp_mode == IC_DEDISP_SHIFT) {
         // (a higher priority for the fit's stream measured no different)
         if (hipStreamCreateWithFlags(&s->dstream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming) != hipSuccess ||
@@ -947,9 +925,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     const size_t P = s->P, N = s->N;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
     const bool exact = p.fit_mode == IC_FIT_EXACT;
-    // the fit rounds' list counts are 24-bit fields of one packed word (RoundList)
-    if (exact && P >= (1u << 24))
-        return bail(fail(IC_EINVAL, "the exact fit takes < 2^24 profiles per session or shard (%zu)", P));
+    // the fit's lists hold int32 profile indices, its round counts are 32-bit fields (RoundList)
+    if (exact && P >= (1ull << 31))
+        return bail(fail(IC_EINVAL, "the exact fit takes < 2^31 profiles per session or shard (%zu)", P));
     AL(s->slot_raw[0], N);
     s->raw = s->slot_raw[0];
     // the closed-form fit reads the raw cube (no fit cube, no lmdif state), unless
@@ -962,11 +940,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->TT, 1);
     s->fftded = p.dedisp_mode == IC_DEDISP_FFT;
     // the fit cube written by k_chan_partials mode 3 is tiled (k_rotate's, in
-    // the FFT mode, is row-major); IC_FIT_TILED=0: row-major (A/B knob)
-    {
-        const char *e = getenv("IC_FIT_TILED");
-        s->dtiled = (!s->fftded && !(e && atoi(e) == 0)) ? 1 : 0;
-    }
+    // the FFT mode, is row-major); IC_OPT_FIT_TILED = 0: row-major
+    s->dtiled = s->fftded ? 0 : 1;
     if (s->fftded) {
         AL(s->dr, N);
         AL(s->Tc, N);
@@ -989,7 +964,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->win, (size_t)nsub);
     AL(s->wflag, (size_t)nsub + 1);   // + window-moves counter
     AL(s->part, (size_t)nsub * s->nsb * nbin);
-    if (s->incr && !s->fftded) {
+    if (!s->fftded) {   // the incremental template stage's column flags (IC_OPT_TEMPLATE_INCR)
         AL(s->exA, (size_t)nsub * s->nsb * nbin);
         AL(s->exF, (size_t)nsub * s->nsb * nbin);
     } else {
@@ -1017,8 +992,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     if (exact) AL(s->lists, 3 * P);   // two ping-pong round lists + the fork round's survivors
-    AL(s->rcount, (size_t)2 * kMaxRounds + 4);   // + the tail's sweep counter (u64), the diagnostics counter
-    if (exact && !s->fftded && s->diag_fork > 0) AL(s->late, P);
+    AL(s->rcount, (size_t)kRoundWords + 2);   // + the tail's sweep counter (u64)
+    if (exact && !s->fftded) AL(s->late, P);
     if (sharded) {
         const char *cerr = nullptr;
         s->comm = make_comm(&cerr);
@@ -1169,6 +1144,13 @@ void ic_session_destroy(void *session)
 {
     Session *s = (Session *)session;
     if (!s) return;
+    if (s->failed) {
+        // kernels of this session may still be running (a wait timed out):
+        // freeing their buffers could hand memory in use to another
+        // allocation, and a synchronising free could hang; leak them
+        delete s;
+        return;
+    }
     (void)hipSetDevice(s->device);
     free_all(s);
     delete s;
@@ -1178,6 +1160,7 @@ int ic_upload(void *session, const float *cube, const float *w0, const int32_t *
 {
     Session *s = (Session *)session;
     if (!s || !cube || !w0 || !shift) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (s->fifo_n) return fail(IC_ESTATE, "ic_upload with %d asynchronous upload(s) pending", s->fifo_n);
     CK(hipSetDevice(s->device));
     for (int c = 0; c < s->nchan; ++c)
@@ -1196,6 +1179,7 @@ int ic_upload_pols(void *session, const float *data, int npol, const float *w0, 
 {
     Session *s = (Session *)session;
     if (!s || !data || !w0 || !shift) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (npol < 1) return fail(IC_EINVAL, "npol=%d", npol);
     if (s->fifo_n) return fail(IC_ESTATE, "ic_upload_pols with %d asynchronous upload(s) pending", s->fifo_n);
     CK(hipSetDevice(s->device));
@@ -1233,6 +1217,7 @@ int ic_upload_device(void *session, const float *d_cube, const float *d_w0, cons
 {
     Session *s = (Session *)session;
     if (!s || !d_cube || !d_w0 || !d_shift) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (s->fifo_n) return fail(IC_ESTATE, "ic_upload_device with %d asynchronous upload(s) pending", s->fifo_n);
     CK(hipSetDevice(s->device));
     s->ever_uploaded = true;
@@ -1249,6 +1234,7 @@ int ic_upload_async(void *session, const float *cube, const float *w0, const int
 {
     Session *s = (Session *)session;
     if (!s || !cube || !w0 || !shift) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (s->fifo_n == 2) return fail(IC_ESTATE, "two asynchronous uploads already pending (run one first)");
     for (int c = 0; c < s->nchan; ++c)
         if (shift[c] < 0 || shift[c] >= s->p.nbin) return fail(IC_EINVAL, "shift[%d]=%d out of [0,nbin)", c, shift[c]);
@@ -1290,6 +1276,7 @@ int ic_set_timing_kernel(void *session, int kernel)
 {
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null session");
+    if (s->failed) return failed_session();
     if (kernel >= K_COUNT) return fail(IC_EINVAL, "kernel id %d >= %d", kernel, (int)K_COUNT);
     s->timing_only = kernel < 0 ? -1 : kernel;
     return IC_OK;
@@ -1299,6 +1286,7 @@ int ic_set_timing(void *session, int enabled)
 {
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null session");
+    if (s->failed) return failed_session();
     s->timing = enabled != 0;
     s->events.clear();   // events of earlier runs are discarded unread
     s->enext = 0;
@@ -1313,6 +1301,7 @@ int ic_get_kernel_times(void *session, ic_kernel_time *out, int n)
 {
     Session *s = (Session *)session;
     if (!s || (!out && n > 0)) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (int rc = collect_timing(s)) return rc;
     int m = 0;
     for (int q = 0; q < K_COUNT && m < n; ++q) {
@@ -1362,6 +1351,7 @@ DiagArgs diag_args(Session *s, int pr_start, int pr_end)
     a.fft_o = s->fft;
     a.ptp_o = s->ptp;
     a.data_f64 = p.data_f64 != 0;
+    a.chain = s->diag_chain ? 1 : 0;
     return a;
 }
 
@@ -1413,14 +1403,14 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     s->bad_fits.clear();
     int x = 0, loops = -1, n_iter = 0, converged = 0;
     // k_fit_tail's sweep counter (after the per-round counters): one run's total
-    CK(hipMemsetAsync((unsigned long long *)s->rcount + kMaxRounds, 0, sizeof(unsigned long long), s->stream));
+    CK(hipMemsetAsync(tail_counter(s), 0, sizeof(unsigned long long), s->stream));
     while (x < p.max_iter) {
         x += 1;
         ++n_iter;
         if (int rc = iteration_template(s, n_iter)) return rc;
         DiagArgs da = diag_args(s, pr_start, pr_end);
         if (p.fit_mode == IC_FIT_EXACT) {
-            const bool fork = s->dstream && s->late && diag_list_supported(da);
+            const bool fork = s->diag_fork > 0 && s->dstream && s->late && diag_list_supported(da);
             if (int rc = run_fit(s, fork ? &da : nullptr)) return rc;
         } else {
             LAUNCH(s, K_TNORM, launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
@@ -1445,12 +1435,6 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             b.list = s->lists + 2 * s->P;
             b.nctr = (const unsigned long long *)s->rcount + s->fork_round;
             LAUNCH(s, K_DIAG, launch_diag(s->stream, b));
-            if (s->fork_dyn) {   // the profiles pass A has not taken yet
-                DiagArgs c = da;
-                c.skip = s->late;
-                c.dq = diag_counter(s);
-                LAUNCH(s, K_DIAG, launch_diag(s->stream, c));
-            }
             CK(hipStreamWaitEvent(s->stream, s->join_ev, 0));
         } else {
             LAUNCH(s, K_DIAG, launch_diag(s->stream, da));
@@ -1491,7 +1475,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         int32_t *moves = s->h_small + p.max_iter + 6;                               // pinned
         unsigned long long *tsw = (unsigned long long *)(s->h_small + ((p.max_iter + 9) & ~1));   // 8-B aligned
         CK(hipMemcpyAsync(moves, s->wflag + nsub, sizeof *moves, hipMemcpyDeviceToHost, s->stream));
-        CK(hipMemcpyAsync(tsw, (unsigned long long *)s->rcount + kMaxRounds, sizeof *tsw, hipMemcpyDeviceToHost,
+        CK(hipMemcpyAsync(tsw, tail_counter(s), sizeof *tsw, hipMemcpyDeviceToHost,
                           s->stream));
         CK(spin_sync(s));
         s->stats.window_moves = *moves;
@@ -1515,6 +1499,7 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
 {
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null session");
+    if (s->failed) return failed_session();
     const int rc = run_impl(s, test_out, weights_out, loops_out, changed_out, nzero_out, n_iter_out, converged_out);
     if (rc && s->comm) s->comm->abort();   // peers must not wait for this shard
     return rc;
@@ -1524,6 +1509,7 @@ int ic_get_residual(void *session, float *out)
 {
     Session *s = (Session *)session;
     if (!s || !out) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
     CK(hipSetDevice(s->device));
     const ic_params &p = s->p;
@@ -1552,6 +1538,7 @@ int ic_set_delays(void *session, const double *delay_bins)
 {
     Session *s = (Session *)session;
     if (!s || !delay_bins) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (!s->fftded) return fail(IC_ESTATE, "ic_set_delays on a session with dedisp_mode %d", s->p.dedisp_mode);
     for (int c = 0; c < s->nchan; ++c)
         if (!isfinite(delay_bins[c])) return fail(IC_EINVAL, "delay[%d] is not finite", c);
@@ -1626,13 +1613,78 @@ int ic_get_bad_fits(void *session, int32_t *per_iter, int n)
     return m;
 }
 
-int ic_set_fit_tail(void *session, int64_t threshold)
+int ic_set_fit_tail(void *session, int64_t threshold) { return ic_set_option(session, IC_OPT_FIT_TAIL, threshold); }
+
+// Schedule options (include/iterative_cleaner.h): validated here, read by the
+// next ic_run; every setting gives the same bits.
+int ic_set_option(void *session, int option, int64_t v)
 {
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null session");
-    if (threshold < 0) return fail(IC_EINVAL, "negative tail threshold");
-    s->tail_threshold = (long)threshold;
-    return IC_OK;
+    if (s->failed) return fail(IC_ESTATE, "session failed (a host wait timed out); destroy it");
+    const bool exact_shift = s->p.fit_mode == IC_FIT_EXACT && !s->fftded;
+    switch (option) {
+    case IC_OPT_FIT_TAIL:
+        if (v < 0) return fail(IC_EINVAL, "IC_OPT_FIT_TAIL=%lld < 0", (long long)v);
+        s->tail_threshold = (long)v;
+        return IC_OK;
+    case IC_OPT_DIAG_FORK:
+        if (v < 0 || v > 64) return fail(IC_EINVAL, "IC_OPT_DIAG_FORK=%lld outside 0..64", (long long)v);
+        if (v > 0 && !exact_shift)
+            return fail(IC_EINVAL, "IC_OPT_DIAG_FORK needs the exact fit with integer dedispersion");
+        s->diag_fork = (int)v;
+        return IC_OK;
+    case IC_OPT_FORK_DELAY:
+        if (v < 0 || v > 8) return fail(IC_EINVAL, "IC_OPT_FORK_DELAY=%lld outside 0..8", (long long)v);
+        s->fork_delay = (int)v;
+        return IC_OK;
+    case IC_OPT_TEMPLATE_INCR:
+        if (v != 0 && v != 1) return fail(IC_EINVAL, "IC_OPT_TEMPLATE_INCR=%lld (0 or 1)", (long long)v);
+        if (v && s->fftded) return fail(IC_EINVAL, "IC_OPT_TEMPLATE_INCR needs integer dedispersion");
+        s->incr = v != 0;
+        return IC_OK;
+    case IC_OPT_FIT_TILED:
+        if (v != 0 && v != 1) return fail(IC_EINVAL, "IC_OPT_FIT_TILED=%lld (0 or 1)", (long long)v);
+        if (v && s->fftded) return fail(IC_EINVAL, "IC_OPT_FIT_TILED needs integer dedispersion");
+        s->dtiled = (int)v;
+        return IC_OK;
+    case IC_OPT_ROWSTAT_WAVES:
+        if (v != 0 && v != 4 && v != 8) return fail(IC_EINVAL, "IC_OPT_ROWSTAT_WAVES=%lld (0, 4 or 8)", (long long)v);
+        s->ls_knobs.grp_waves = (int)v;
+        return IC_OK;
+    case IC_OPT_ROWSTAT_MINLEN:
+        if (v < 1 || v > 16384) return fail(IC_EINVAL, "IC_OPT_ROWSTAT_MINLEN=%lld outside 1..16384", (long long)v);
+        s->ls_knobs.grp_minlen = (int)v;
+        return IC_OK;
+    case IC_OPT_DIAG_CHAIN:
+        if (v != 0 && v != 1) return fail(IC_EINVAL, "IC_OPT_DIAG_CHAIN=%lld (0 or 1)", (long long)v);
+        s->diag_chain = v != 0;
+        return IC_OK;
+    case IC_OPT_SYNC_TIMEOUT_MS:
+        if (v < 1) return fail(IC_EINVAL, "IC_OPT_SYNC_TIMEOUT_MS=%lld < 1", (long long)v);
+        s->sync_timeout_s = (double)v / 1000.0;
+        return IC_OK;
+    default:
+        return fail(IC_EINVAL, "unknown option %d", option);
+    }
+}
+
+int ic_get_option(void *session, int option, int64_t *out)
+{
+    Session *s = (Session *)session;
+    if (!s || !out) return fail(IC_EINVAL, "null argument");
+    switch (option) {
+    case IC_OPT_FIT_TAIL: *out = s->tail_threshold; return IC_OK;
+    case IC_OPT_DIAG_FORK: *out = s->diag_fork; return IC_OK;
+    case IC_OPT_FORK_DELAY: *out = s->fork_delay; return IC_OK;
+    case IC_OPT_TEMPLATE_INCR: *out = s->incr ? 1 : 0; return IC_OK;
+    case IC_OPT_FIT_TILED: *out = s->dtiled; return IC_OK;
+    case IC_OPT_ROWSTAT_WAVES: *out = s->ls_knobs.grp_waves; return IC_OK;
+    case IC_OPT_ROWSTAT_MINLEN: *out = s->ls_knobs.grp_minlen; return IC_OK;
+    case IC_OPT_DIAG_CHAIN: *out = s->diag_chain ? 1 : 0; return IC_OK;
+    case IC_OPT_SYNC_TIMEOUT_MS: *out = (int64_t)(s->sync_timeout_s * 1000.0 + 0.5); return IC_OK;
+    default: return fail(IC_EINVAL, "unknown option %d", option);
+    }
 }
 
 int ic_get_run_stats(void *session, ic_run_stats *out)
@@ -1647,6 +1699,7 @@ int ic_get_template(void *session, float *T)
 {
     Session *s = (Session *)session;
     if (!s || !T) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
     CK(hipMemcpyAsync(T, s->T, sizeof(float) * s->p.nbin, hipMemcpyDeviceToHost, s->stream));
     CK(hipStreamSynchronize(s->stream));
@@ -1657,6 +1710,7 @@ int ic_get_fit(void *session, double *amp, int32_t *info)
 {
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
     if (amp) CK(hipMemcpyAsync(amp, s->amp, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
     if (info) CK(hipMemcpyAsync(info, s->info, sizeof(int32_t) * s->P, hipMemcpyDeviceToHost, s->stream));
@@ -1668,6 +1722,7 @@ int ic_get_diagnostics_f64(void *session, double *std_o, double *mean_o, double 
 {
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
     if (!s->ran) return fail(IC_ESTATE, "no completed iteration");
     if (std_o) CK(hipMemcpyAsync(std_o, s->std_, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
     if (mean_o) CK(hipMemcpyAsync(mean_o, s->mean, sizeof(double) * s->P, hipMemcpyDeviceToHost, s->stream));
@@ -1694,7 +1749,19 @@ int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const floa
                            double chanthresh, double subintthresh, double *test_out, double *std_o, double *mean_o,
                            float *ptp_o, double *fftmax_o)
 {
+    return ic_comprehensive_stats_rowstat(device, nsub, nchan, nbin, data, weights, chanthresh, subintthresh,
+                                          test_out, std_o, mean_o, ptp_o, fftmax_o, 8, 1024);
+}
+
+int ic_comprehensive_stats_rowstat(int device, int nsub, int nchan, int nbin, const float *data,
+                                   const float *weights, double chanthresh, double subintthresh, double *test_out,
+                                   double *std_o, double *mean_o, float *ptp_o, double *fftmax_o, int rowstat_waves,
+                                   int rowstat_minlen)
+{
     if (!data || !weights || !test_out) return fail(IC_EINVAL, "null argument");
+    if (rowstat_waves != 0 && rowstat_waves != 4 && rowstat_waves != 8)
+        return fail(IC_EINVAL, "rowstat_waves=%d (0, 4 or 8)", rowstat_waves);
+    if (rowstat_minlen < 1) return fail(IC_EINVAL, "rowstat_minlen=%d < 1", rowstat_minlen);
     if (nsub <= 0 || nchan <= 0 || nbin <= 0 || nsub > 16384 || nchan > 16384 || nbin > 32768)
         return fail(IC_EINVAL, "bad shape nsub=%d nchan=%d nbin=%d", nsub, nchan, nbin);
     if (diag_lds_bytes(nbin) > 160 * 1024) return fail(IC_EINVAL, "nbin=%d unsupported", nbin);
@@ -1769,7 +1836,8 @@ int ic_comprehensive_stats(int device, int nsub, int nchan, int nbin, const floa
     la.fft_d = ff;
     la.ptp_d = pt;
     la.ptp_f32 = 1;
-    linestats_knobs(la);
+    la.grp_waves = rowstat_waves;
+    la.grp_minlen = rowstat_minlen;
     la.col_med = lstat;
     la.col_mad = lstat + 4 * nchan;
     la.row_med = lstat + 8 * nchan;

@@ -209,3 +209,22 @@ def test_product_has_no_oracle_or_cpu_fallback():
             if f.endswith(".py"):
                 src = open(os.path.join(root, f)).read()
                 assert "oracle" not in src.replace("oracle/", ""), f
+
+
+def test_schedule_options_match_header_and_no_environment_knobs():
+    """Every IC_OPT_* of the header is bound under the same number, the library
+    sources read no environment variable (schedules are session options,
+    validated when set), and a null session is refused without a GPU."""
+    from iterative_cleaner_amd import _native
+    hdr = open(os.path.join(REPO, "include", "iterative_cleaner.h")).read()
+    declared = {m.group(1).lower(): int(m.group(2))
+                for m in re.finditer(r"#define IC_OPT_([A-Z0-9_]+) (\d+)", hdr)}
+    assert declared == _native.OPTIONS
+    csrc = os.path.join(REPO, "iterative_cleaner_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".h")):
+            assert "getenv" not in open(os.path.join(csrc, f)).read(), f
+    lib = _native.load_library()
+    assert lib.ic_set_option(None, 1, 0) == -1
+    v = ctypes.c_int64()
+    assert lib.ic_get_option(None, 1, ctypes.byref(v)) == -1

@@ -100,3 +100,47 @@ def test_run_lanes_error_stops_the_other_lanes():
     assert time.time() - t0 < 5.0
     assert SlowSession.inflight == 0
     assert sum(len(s.ran) for s in sessions) < 300
+
+
+
+class StuckSession(FakeSession):
+    """A run that never returns until released (a hung kernel), except for tag 0."""
+
+    release = threading.Event()
+
+    def __init__(self):
+        super().__init__()
+        self.h = object()   # stands in for the native handle
+
+    def run(self, fetch=True):
+        with self.lock:
+            tag = self.queue[0]
+        if tag != 0:
+            StuckSession.release.wait()
+        return super().run(fetch)
+
+
+def test_run_lanes_stuck_lanes_share_one_deadline():
+    """The consumer stops after the first result while the lanes are stuck
+    inside ic_run: closing waits once for the shared deadline (not once per
+    lane), leaks every stuck session with the arrays it was handed, and drops
+    its handle so that nothing destroys it under the running call."""
+    from iterative_cleaner_amd import batch
+    StuckSession.release.clear()
+    sessions = [StuckSession() for _ in range(3)]
+    items = [(k, "array-%d" % k, None) for k in range(9)]
+    n0 = len(batch._LEAKED)
+    gen = batch.run_lanes(sessions, items, join_timeout=0.6)
+    assert next(gen)["tag"] == 0
+    t0 = time.time()
+    gen.close()
+    dt = time.time() - t0
+    try:
+        assert 0.5 < dt < 1.5, dt          # one shared 0.6-s deadline for three stuck lanes
+        leaked = batch._LEAKED[n0:]
+        assert len(leaked) == 3
+        for sess, handle, arrays in leaked:
+            assert sess._ic_leaked and sess.h is None and handle is not None
+            assert arrays and all(a[1].startswith("array-") for a in arrays)
+    finally:
+        StuckSession.release.set()

@@ -29,7 +29,42 @@ def test_committed_pmc_valu_matches_sources():
         assert 0.0 < v["f64_share_of_valu"] <= 1.0
 
 
+def _run(**kw):
+    run = {"n_iter": 3, "changed": [120000, 900, 0], "fit_profile_sweeps": 1000, "fit_tail_sweeps": 10,
+           "window_moves": 360}
+    run.update(kw)
+    return run
+
+
 def test_algorithmic_bytes_of_the_fit_sweep():
-    stats = {"fit_profile_sweeps": 1000, "fit_tail_sweeps": 10}
-    assert bench.algorithmic_bytes("k_fit_pass", 2, 3, 1024, 30, stats, 1) == 4 * 1024 * 1000
-    assert bench.algorithmic_bytes("k_fit_tail", 2, 3, 1024, 3, stats, 2) == 4 * 1024 * 10 * 2
+    run = _run()
+    assert bench.algorithmic_bytes("k_fit_pass", 2, 3, 1024, 30, run, 1) == 4 * 1024 * 1000
+    assert bench.algorithmic_bytes("k_fit_tail", 2, 3, 1024, 3, run, 2) == 4 * 1024 * 10 * 2
+
+
+def test_template_stage_charges_only_what_it_reads():
+    """C2 (360 x 3200 x 1024, 3 loops): prepare's pass and iteration 1's pass
+    with the fit-cube write read / write whole cubes; the later iterations read
+    the changed channels and the subints whose window moved.  At round 3's
+    measured 3.72 ms per clean for every template-stage launch the rate must
+    sit under the HBM peak (round 3's per-launch model said 8.9 TB/s)."""
+    nsub, nchan, nbin = 360, 3200, 1024
+    N = nsub * nchan * nbin
+    run = _run()
+    b = bench.algorithmic_bytes("k_chan_partials", nsub, nchan, nbin, 6, run, 1)
+    assert b == (4 * N + 8 * N + 4 * nbin * (120000 + 900) + 4 * nchan * nbin * 360
+                 + 16 * nsub * 13 * nbin * 3)
+    assert b / 3.722e-3 / 1e9 < bench.HBM_PEAK_GBS
+    # the fast mode writes no fit cube
+    assert bench.algorithmic_bytes("k_chan_partials", nsub, nchan, nbin, 6, run, 1, exact=False) == b - 4 * N
+    # one diagnostics pass per iteration, however many launches (the fork)
+    assert bench.algorithmic_bytes("k_diag", nsub, nchan, nbin, 6, run, 2) == 2 * 3 * (4 * N + 44 * nsub * nchan)
+
+
+def test_rates_above_peak_refuse_the_line():
+    pk = {"k_chan_partials": {"sweep_gbs": 8936.1}, "k_fit_pass": {"sweep_gbs": 4660.0}, "k_window": {"sweep_gbs": None}}
+    over, resident = bench.check_kernel_rates(pk, 4 * 360 * 3200 * 1024)
+    assert over == {"k_chan_partials": 8936.1} and resident == {}
+    # a cube the Infinity Cache holds may be re-read on-die faster than HBM: reported, not refused
+    over, resident = bench.check_kernel_rates(pk, 4 * 64 * 256 * 256)
+    assert over == {} and resident == {"k_chan_partials": 8936.1}

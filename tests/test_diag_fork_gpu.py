@@ -1,7 +1,7 @@
 """The forked diagnostics of the exact fit (ic_session.hip fork_diag): after a
 fit round the profiles already fitted are measured on a second stream while
 the late rounds and the tail run, the rest after the fit.  Every output must be
-the same bits as the unforked schedule (IC_DIAG_FORK=0), at every fork round,
+the same bits as the unforked schedule (option diag_fork 0), at every fork round,
 with both tail schedules, at the chain-layout profile lengths (1024, 2048,
 4096) and the row-layout ones (256, 512: k_diag_p2), and against the C oracle
 on whole subints."""
@@ -13,14 +13,12 @@ from helpers import bits_equal, nan_equal
 pytestmark = pytest.mark.gpu
 
 
-def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1, grid=0):
+def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1):
     from iterative_cleaner_amd import _native, synth
-    monkeypatch.setenv("IC_DIAG_FORK", str(fork))
-    monkeypatch.setenv("IC_FORK_GRID", str(grid))
     nsub, nchan, nbin = shape
     data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
     raw = np.ascontiguousarray(data[:, 0])
-    with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=0) as s:
+    with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=0, options={"diag_fork": fork}) as s:
         if tail is not None:
             s.set_fit_tail(tail)
         s.upload(raw, w0, shift)
@@ -60,19 +58,3 @@ def test_fork_matches_c_oracle_whole_subints(monkeypatch, oracle_lib):
         assert nan_equal(x, ref[name]) and x.dtype == ref[name].dtype, name
     ff = ref["fft"]
     assert np.all(np.abs(diag[3] - ff) <= 1e-9 * np.abs(ff)), "fftmax"
-
-
-@pytest.mark.parametrize("shape", [(16, 256, 1024), (40, 512, 1024), (6, 256, 2048), (24, 256, 256)])
-@pytest.mark.parametrize("grid", [1, 64, 512])
-def test_fork_shared_counter_is_bit_identical(monkeypatch, shape, grid):
-    """Pass A as a capped grid taking chunks of profiles from a shared counter,
-    the rest taken by a full-grid launch after the fit (IC_FORK_GRID, nbin
-    1024; other nbin ignore the knob): the same bits as the unforked schedule."""
-    ref = _run(monkeypatch, shape, 0, None)
-    for fork in (1, 3):
-        got = _run(monkeypatch, shape, fork, None, grid=grid)
-        assert got[3]["loops"] == ref[3]["loops"]
-        assert bits_equal(got[3]["weights"], ref[3]["weights"]) and bits_equal(got[3]["test"], ref[3]["test"])
-        assert bits_equal(got[4], ref[4]) and bits_equal(got[5], ref[5])
-        for name, x0, x1 in zip(("std", "mean", "ptp", "fftmax"), ref[6], got[6]):
-            assert bits_equal(x1, x0), (fork, grid, name)

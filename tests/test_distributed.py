@@ -169,7 +169,7 @@ def _report_worker(rank, world, port, q):
                   "exchange": {"ms": 99.0, "launches": 7}}
         exch = {"alltoallv": {"ms": 0.5 * (rank + 1), "calls": 6, "bytes": 8_000_000},
                 "allgather": {"ms": 0.25, "calls": 6, "bytes": 4_000_000}}
-        q.put((rank, bench.per_rank_report(ktimes, exch, rank, world, "cpu")))
+        q.put((rank, bench.per_rank_report(ktimes, exch, rank, world, "cpu", 12.0 + rank)))
     finally:
         dist.destroy_process_group()
 
@@ -193,7 +193,11 @@ def test_bench_per_rank_report_two_ranks():
     assert [r["rank"] for r in table] == [0, 1]
     for r in table:
         assert r["world_size_seen"] == 2
-        assert r["compute_ms"] == 15.0 + r["rank"]           # kernels only, not the exchange bucket
+        # the clean's wall time minus its exchanges; the kernels' summed durations
+        # (which overlap when the diagnostics fork) apart
+        assert r["wall_ms"] == 12.0 + r["rank"]
+        assert r["compute_ms"] == 12.0 + r["rank"] - (0.5 * (r["rank"] + 1) + 0.25)
+        assert r["kernel_ms"] == 15.0 + r["rank"]            # kernels only, not the exchange bucket
         assert r["exchange"]["alltoallv"] == {"ms": 0.5 * (r["rank"] + 1), "calls": 6, "MB": 8.0}
         assert r["exchange"]["allgather"]["calls"] == 6
         assert r["exchange"]["allreduce"] == {"ms": 0.0, "calls": 0, "MB": 0.0}

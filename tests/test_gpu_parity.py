@@ -278,15 +278,16 @@ def test_extreme_amplitudes_match_c_oracle(fit_mode, oracle_lib):
 @pytest.mark.parametrize("path", [p for p in clean_fixtures() if "fft" not in os.path.basename(p)][:4],
                          ids=lambda p: os.path.basename(p)[6:-4])
 def test_row_major_fit_cube_matches_tiled(path, monkeypatch):
-    """The fit cube's two layouts (IC_FIT_TILED, read at session creation:
-    tiled by default, row-major as the A/B baseline) give the same bits, and
+    """The fit cube's two layouts (session option fit_tiled: tiled by
+    default, row-major as the A/B baseline) give the same bits, and
     both the reference's: layout moves bytes, never arithmetic."""
     z, meta, raw, w0, shift, args = load_clean_case(path)
     nit = int(z["n_iter"])
     outs = []
-    for tiled in ("1", "0"):
-        monkeypatch.setenv("IC_FIT_TILED", tiled)
+    for tiled in (1, 0):
         with _session(raw.shape, args, data_f64=meta.get("data_f64", False)) as s:
+            s.set_option("fit_tiled", tiled)
+            assert s.get_option("fit_tiled") == tiled
             s.upload(raw, w0, shift)
             out = s.run()
             amp, info = s.fit()

@@ -70,23 +70,22 @@ def test_stats_match_c_oracle_larger(nbin, oracle_lib):
 
 
 @pytest.mark.parametrize("grp", ["0", "4", "8"])
-def test_line_medians_per_block_match(grp, monkeypatch, oracle_lib):
+def test_line_medians_per_block_match(grp, oracle_lib):
     """The per-line median/MAD in its two forms: one wave per line, and a block
     of W waves per line (k_linestats_grp, taken by default for few lines of
-    >= 1024 values; IC_LS_GRP_MINLEN=1 forces it onto every line here).
+    >= 1024 values; rowstat_minlen=1 forces it onto every line here).
     Both must reproduce the reference's selections: the edge cases of
     stats_cases.npz (NaN, empty, tied lines), and long rows (nchan 3000) with
     ties, zapped entries and outliers against the C oracle."""
     from oracle import restated as R
 
     from iterative_cleaner_amd import _native
-    monkeypatch.setenv("IC_LS_GRP", grp)
-    monkeypatch.setenv("IC_LS_GRP_MINLEN", "1")
+    opt = dict(rowstat_waves=int(grp), rowstat_minlen=1)
     z = np.load(os.path.join(GOLDEN, "stats_cases.npz"))
     for i in range(int(z["n"])):
         X, w = z["X_%d" % i], z["w_%d" % i]
         ct, st = thresholds(z, i)
-        test, diags = _native.comprehensive_stats(X, w, ct, st, diagnostics=True)
+        test, diags = _native.comprehensive_stats(X, w, ct, st, diagnostics=True, **opt)
         _check(test, diags, z["test_%d" % i], w != 0)
     rng = np.random.default_rng(77)
     for nsub, nchan, nbin in ((5, 3000, 32), (3, 1999, 16)):
@@ -96,7 +95,7 @@ def test_line_medians_per_block_match(grp, monkeypatch, oracle_lib):
         w = np.ones((nsub, nchan), np.float32)
         w[:, rng.integers(0, nchan, 200)] = 0
         w[2, :nchan // 2] = 0                           # a half-zapped row
-        test, diags = _native.comprehensive_stats(X, w, 5, 5, diagnostics=True)
+        test, diags = _native.comprehensive_stats(X, w, 5, 5, diagnostics=True, **opt)
         Xw = R.weighted_cube(X, w)
         sd, mn, pt, ff = oracle_lib.diagnostics(Xw, w != 0)
         ref = oracle_lib.test_values(w != 0, sd, mn, pt, ff, 5, 5)

@@ -2,7 +2,7 @@
 the window totals and fscrunch partials move through the channels whose weight
 changed, exact where every subset sum of a super-block column is exact
 (k_chan_partials' ExTrack flags), summed again in canonical order elsewhere.
-Every output must be the same bits as the full passes (IC_TEMPLATE_INCR=0),
+Every output must be the same bits as the full passes (option template_incr 0),
 including on data built to make columns inexact (values spanning more than
 2^21 within a column, zeros, subnormals), with fractional weights, channel
 shards, and against the C oracle.  (A non-finite sample makes the template
@@ -32,9 +32,9 @@ def _cube(shape, seed, rough):
 
 def _run(monkeypatch, raw, w0, shift, incr, tail=None, max_iter=5):
     from iterative_cleaner_amd import _native
-    monkeypatch.setenv("IC_TEMPLATE_INCR", "1" if incr else "0")
     nsub, nchan, nbin = raw.shape
-    with _native.GpuSession(nsub, nchan, nbin, max_iter=max_iter, device=0) as s:
+    with _native.GpuSession(nsub, nchan, nbin, max_iter=max_iter, device=0,
+                            options={"template_incr": 1 if incr else 0}) as s:
         if tail is not None:
             s.set_fit_tail(tail)
         s.upload(raw, w0, shift)
@@ -87,7 +87,6 @@ def test_incremental_template_channel_shards(monkeypatch):
     from iterative_cleaner_amd import sharded
     raw, w0, shift = _cube((8, 1024, 256), 5, True)
     ref = _run(monkeypatch, raw, w0, shift, False)
-    monkeypatch.setenv("IC_TEMPLATE_INCR", "1")
     res = sharded.clean_cube_local(raw, w0, shift, 4)
     assert res["loops"] == ref[0]["loops"]
     assert bits_equal(res["weights"], ref[0]["weights"])
