@@ -135,7 +135,7 @@ def s8d_bytes(name, nsub, nchan, nbin, launches, iterations, steps):
     chooses (lmdif's 5.5 sweeps per profile) are NOT algorithmic."""
     P = nsub * nchan
     N = P * nbin
-    per_iter = {"k_chan_partials": 4 * N, "k_fit_pass": 4 * N, "k_diag": 4 * N + 32 * P,
+    per_iter = {"k_chan_partials": 4 * N, "k_fit_pass": 4 * N, "k_fit_lanes": 4 * N, "k_diag": 4 * N + 32 * P,
                 "k_linestats": 16 * P, "k_combine": 16 * P}
     if name not in per_iter:
         return None
@@ -167,7 +167,7 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True)
     nsb = (nchan + 255) // 256
     width = max(1, int(0.15 * nbin))
     n_iter = run["n_iter"]
-    if name == "k_fit_pass":
+    if name in ("k_fit_pass", "k_fit_lanes"):   # the lanes' sweeps are counted in the same field
         return 4 * nbin * run["fit_profile_sweeps"] * steps
     if name == "k_fit_tail":
         return 4 * nbin * run["fit_tail_sweeps"] * steps
@@ -313,7 +313,7 @@ def fast_mode_summary(_native, cube, w0, shift, shape, device, steps, torch, del
                     "mode, not the reference's leastsq arithmetic"}
 
 
-EXCHANGE_KINDS = ("allgather", "alltoallv", "allreduce")
+EXCHANGE_KINDS = ("allgather", "alltoallv", "allreduce", "native")
 
 
 def per_rank_report(ktimes, exch, rank, world, dev, wall_ms):
@@ -447,6 +447,13 @@ def main():
     ap.add_argument("--no-flip-check", action="store_true",
                     help="closed mode: skip the (untimed) exact run that counts zap-mask flips "
                          "(profiling passes, whose kernel tallies it would mix in)")
+    ap.add_argument("--fit-schedule", choices=("rounds", "lanes"), default="rounds",
+                    help="exact fit: rounds of sweep / state kernels over compacted lists (default), or one "
+                         "persistent launch whose lanes each run lmdif for one profile after another")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="a session schedule option (_native.OPTIONS; same bits under every setting), repeatable")
+    ap.add_argument("--lane-waves", type=int, default=0,
+                    help="--fit-schedule lanes: waves of the persistent launch (0: every wave the device holds)")
     ap.add_argument("--dedisp", choices=("shift", "fft"), default="shift",
                     help="shift: integer dedispersion shifts (default); fft: fractional delays, dedispersed by "
                          "psrchive's FFT phase rotation (dedisp_mode IC_DEDISP_FFT)")
@@ -467,6 +474,9 @@ def main():
     # IC_BENCH_BACKEND=gloo rehearses an N-rank run on fewer GPUs (ranks share
     # devices, exchanges staged through the host); the measurement is "nccl" (RCCL)
     backend = os.environ.get("IC_BENCH_BACKEND", "nccl")
+    # channel shards over "nccl" use the library's native RCCL transport;
+    # IC_BENCH_TRANSPORT=torch keeps the torch.distributed callbacks (A/B)
+    native_rccl = backend == "nccl" and os.environ.get("IC_BENCH_TRANSPORT", "rccl") == "rccl"
     gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -492,8 +502,14 @@ def main():
         c0, c1 = chans[rank]
         cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, c0, c1, dev)
         comm = TorchComm(dev)
-        sess = _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm, max_iter=5, device=local,
-                                    fit_mode=fit_mode, delay=None if delay is None else delay[c0:c1])
+        kw = dict(max_iter=5, device=local, fit_mode=fit_mode, delay=None if delay is None else delay[c0:c1])
+        if native_rccl:
+            # the library's own RCCL communicator: every exchange issued from C++
+            # on the session stream (rank 0's unique id shared once)
+            from iterative_cleaner_amd.dist import share_rccl_id
+            sess = _native.ShardSession(nsub, nchan, nbin, rank, world, rccl_id=share_rccl_id(), **kw)
+        else:
+            sess = _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm, **kw)
         per_rank_P = nsub * (c1 - c0)
     else:
         if workload in BLOCKWISE:
@@ -501,6 +517,12 @@ def main():
         else:
             cube, w0, shift = make_cube_device(nsub, nchan, nbin, seed + 7919 * rank, rfi, dev)
         sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local, fit_mode=fit_mode, delay=delay)
+        if a.fit_schedule == "lanes":
+            sess.set_option("fit_schedule", _native.FIT_LANES)
+            sess.set_option("fit_lane_waves", a.lane_waves)
+        for opt in a.option:
+            name, _, value = opt.partition("=")
+            sess.set_option(name, int(value))
         per_rank_P = P_total
         if world > 1:
             P_total = P_total * world          # replicas: every rank cleans its own archive
@@ -542,7 +564,11 @@ def main():
         ktimes_all = sess.kernel_times()
         if sharded:
             comm.timing = False
-            rank_report = per_rank_report(ktimes_all, comm.exchange_report(), rank, world, dev, wall_ms)
+            exch = comm.exchange_report()
+            if native_rccl:   # the session's own exchange timing (one bucket: RCCL calls from C++)
+                e = ktimes_all.get("exchange", {"ms": 0.0, "launches": 0})
+                exch = {"native": {"ms": e["ms"], "calls": e["launches"], "bytes": 0}}
+            rank_report = per_rank_report(ktimes_all, exch, rank, world, dev, wall_ms)
         kk = {k: v for k, v in ktimes_all.items() if k.startswith("k_") and v["launches"]}
         dom = max(kk, key=lambda k: kk[k]["ms"])
         sess.set_timing(True, only=dom)
@@ -670,7 +696,9 @@ def main():
         roof["loop_hbm_frac"] = round(loop_gbs / HBM_PEAK_GBS, 4)
         if sharded:
             parallelism = "channel-sharded x%d (RCCL per iteration: 3 all-to-alls to row owners, " \
-                          "3 all-gathers of owner results, 1 all-reduce)" % world
+                          "3 all-gathers of owner results, 1 all-reduce; %s)" % (
+                              world, "native RCCL communicator, collectives issued from C++" if native_rccl
+                              else "torch.distributed callbacks")
         else:
             parallelism = "replicas" if world > 1 else "single"
         rec = {
@@ -690,6 +718,9 @@ def main():
                        "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"])
                                                        / per_rank_P / max(1, n_iter), 2),
                        "fit_tail_sweeps": stats["fit_tail_sweeps"] // max(1, n_iter),
+                       "fit_schedule": a.fit_schedule,
+                       "fit_lane_use": (round(stats["fit_profile_sweeps"] / stats["fit_lane_slots"], 3)
+                                        if stats.get("fit_lane_slots") else None),
                        "near_threshold_profiles": stats["near_threshold"],
                        "parallelism": parallelism,
                        "loop_hbm_gbs_per_gpu": round(loop_gbs, 1),

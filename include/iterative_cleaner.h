@@ -203,6 +203,9 @@ typedef struct {
     int32_t near_threshold;      /* last iteration: profiles whose test value lies within 1e-9 of
                                     the zap threshold 1.0, where fftmax's last bits (not
                                     bit-identical to numpy's pocketfft) could decide the zap */
+    int64_t fit_lane_slots;      /* IC_FIT_LANES: lane slots the waves swept (64 per wave sweep,
+                                    waiting lanes included); fit_profile_sweeps / this is the
+                                    share of lanes doing work */
 } ic_run_stats;
 int ic_get_run_stats(void *session, ic_run_stats *out);
 
@@ -227,6 +230,15 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  *   IC_OPT_ROWSTAT_MINLEN  shortest row that takes them, 1..16384; 1024
  *   IC_OPT_DIAG_CHAIN      1 = chain-layout diagnostics kernel at nbin 1024,
  *                          2048, 4096; 0 = the row-layout kernel; 1
+ *   IC_OPT_FIT_SCHEDULE    how the exact fit is scheduled (integer dedispersion):
+ *                          IC_FIT_ROUNDS = rounds of a sweep kernel over every
+ *                          profile with a pending data request and a state
+ *                          kernel, compacted lists, k_fit_tail for the last
+ *                          profiles; IC_FIT_LANES = one persistent launch whose
+ *                          lanes each run lmdif for one profile after another
+ *                          from a shared queue; IC_FIT_ROUNDS
+ *   IC_OPT_FIT_LANE_WAVES  waves of the IC_FIT_LANES launch, 0 = every wave the
+ *                          device holds at once (more are capped to that); 0
  *   IC_OPT_SYNC_TIMEOUT_MS longest host wait for the GPU, >= 1 ms; 600000.  A
  *                          wait that runs out fails its call with IC_EHIP and
  *                          marks the session failed: every later call on it
@@ -242,6 +254,10 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
 #define IC_OPT_ROWSTAT_MINLEN 7
 #define IC_OPT_DIAG_CHAIN 8
 #define IC_OPT_SYNC_TIMEOUT_MS 9
+#define IC_OPT_FIT_SCHEDULE 10
+#define IC_OPT_FIT_LANE_WAVES 11
+#define IC_FIT_ROUNDS 0
+#define IC_FIT_LANES 1
 int ic_set_option(void *session, int option, int64_t value);
 int ic_get_option(void *session, int option, int64_t *value);
 /* = ic_set_option(session, IC_OPT_FIT_TAIL, threshold) */
@@ -322,6 +338,18 @@ typedef struct {
  * (copied; ops->ctx must outlive the session). */
 int ic_session_create_shard(const ic_params *params, int device, int rank, int world, const ic_comm_ops *ops,
                             void **session);
+
+/* Native RCCL transport (one process per GPU, RCCL over xGMI): rank 0 calls
+ * ic_rccl_unique_id and the host hands the 128 id bytes to every rank once
+ * (e.g. through the torch.distributed store); each rank then creates its shard
+ * with them on its own device.  Every exchange is an RCCL collective (all-to-all
+ * as grouped sends / receives) issued by the library on the session stream: no
+ * host callback per exchange.  A failing shard aborts its communicator, so its
+ * peers' collectives fail (IC_ECOMM) instead of waiting.  librccl is loaded on
+ * first use (/opt/rocm/lib/librccl.so.1). */
+int ic_rccl_unique_id(void *id_out /* 128 bytes */);
+int ic_session_create_rccl(const ic_params *params, int device, int rank, int world, const void *unique_id,
+                           void **session);
 
 /* In-process shard group: `world` shards driven by `world` host threads of one
  * process (one or several devices), exchanging by device-to-device / peer

@@ -24,12 +24,16 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_session_create_grouped", "ic_upload_async", "ic_host_alloc", "ic_host_free",
            "ic_upload_pols", "ic_comprehensive_stats", "ic_get_bad_fits",
            "ic_fit_profiles", "ic_get_diagnostics_f64", "ic_set_delays", "ic_rotate_profiles",
-           "ic_set_timing_kernel", "ic_set_option", "ic_get_option", "ic_comprehensive_stats_rowstat")
+           "ic_set_timing_kernel", "ic_set_option", "ic_get_option", "ic_comprehensive_stats_rowstat",
+           "ic_rccl_unique_id", "ic_session_create_rccl")
 
 # session schedule options (ic_set_option; include/iterative_cleaner.h): they
 # choose how the loop is scheduled, never its arithmetic
 OPTIONS = {"fit_tail": 1, "diag_fork": 2, "fork_delay": 3, "template_incr": 4, "fit_tiled": 5,
-           "rowstat_waves": 6, "rowstat_minlen": 7, "diag_chain": 8, "sync_timeout_ms": 9}
+           "rowstat_waves": 6, "rowstat_minlen": 7, "diag_chain": 8, "sync_timeout_ms": 9,
+           "fit_schedule": 10, "fit_lane_waves": 11}
+FIT_ROUNDS = 0   # IC_FIT_ROUNDS: sweep / state rounds over compacted lists (k_fit_pass, k_fit_state, k_fit_tail)
+FIT_LANES = 1    # IC_FIT_LANES: one persistent launch, a lane per profile at a time (k_fit_lanes)
 
 FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)
 FIT_CLOSED = 1   # IC_FIT_CLOSED: closed-form amplitude fused with the diagnostics (fast mode)
@@ -52,7 +56,7 @@ class Params(C.Structure):
 class RunStats(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("fit_rounds", C.c_int32),
                 ("fit_profile_sweeps", C.c_int64), ("fit_tail_sweeps", C.c_int64),
-                ("window_moves", C.c_int32), ("near_threshold", C.c_int32)]
+                ("window_moves", C.c_int32), ("near_threshold", C.c_int32), ("fit_lane_slots", C.c_int64)]
 
 
 class KernelTime(C.Structure):
@@ -144,6 +148,8 @@ def load_library(path: str = LIB_PATH):
     lib.ic_group_destroy.argtypes = [vp]
     lib.ic_group_destroy.restype = None
     lib.ic_session_create_grouped.argtypes = [C.POINTER(Params), C.c_int, vp, C.c_int, C.POINTER(vp)]
+    lib.ic_rccl_unique_id.argtypes = [vp]
+    lib.ic_session_create_rccl.argtypes = [C.POINTER(Params), C.c_int, C.c_int, C.c_int, vp, C.POINTER(vp)]
     lib.ic_get_bad_fits.argtypes = [vp, vp, C.c_int]
     lib.ic_fit_profiles.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp]
     lib.ic_set_delays.argtypes = [vp, vp]
@@ -363,7 +369,8 @@ class GpuSession:
         return dict(iterations=st.iterations, fit_rounds=st.fit_rounds,
                     fit_profile_sweeps=int(st.fit_profile_sweeps),
                     fit_tail_sweeps=int(st.fit_tail_sweeps),
-                    window_moves=int(st.window_moves), near_threshold=int(st.near_threshold))
+                    window_moves=int(st.window_moves), near_threshold=int(st.near_threshold),
+                    fit_lane_slots=int(st.fit_lane_slots))
 
     def kernel_times(self):
         buf = (KernelTime * 32)()
@@ -475,6 +482,17 @@ def shard_layout(nsub, nchan, world):
             [(int(rr[2 * r]), int(rr[2 * r + 1])) for r in range(world)])
 
 
+def rccl_unique_id() -> bytes:
+    """128-byte RCCL unique id (ncclGetUniqueId through ic_rccl_unique_id), made
+    by rank 0 and handed once to every rank of a native-RCCL shard group."""
+    lib = load_library()
+    buf = (C.c_char * 128)()
+    rc = lib.ic_rccl_unique_id(C.cast(buf, C.c_void_p))
+    if rc != 0:
+        raise NativeError("ic_rccl_unique_id: %s (rc=%d)" % (_err(lib), rc))
+    return bytes(buf.raw)
+
+
 class ShardGroup:
     """In-process shard group (ic_group_create): `world` shard sessions driven
     by `world` host threads of this process, exchanging by device copies."""
@@ -503,16 +521,20 @@ class ShardGroup:
 class ShardSession(GpuSession):
     """Channel shard `rank` of `world` of one archive (global shape in the
     arguments; uploads and per-profile outputs are the shard's channel slice).
-    Exchanges go through `group` (a ShardGroup: in-process) or `comm` (an
-    object with ``ops()`` returning a CommOps, e.g. dist.TorchComm)."""
+    Exchanges go through `group` (a ShardGroup: in-process), `comm` (an object
+    with ``ops()`` returning a CommOps, e.g. dist.TorchComm: host callbacks) or
+    `rccl_id` (rank 0's rccl_unique_id(): the library's own RCCL communicator,
+    every collective issued from C++ on the session stream)."""
 
     _create_name = "ic_session_create_shard"
 
-    def __init__(self, nsub, nchan, nbin, rank, world, group=None, comm=None, **kw):
-        if (group is None) == (comm is None):
-            raise ValueError("ShardSession needs exactly one of group / comm")
+    def __init__(self, nsub, nchan, nbin, rank, world, group=None, comm=None, rccl_id=None, **kw):
+        if sum(x is not None for x in (group, comm, rccl_id)) != 1:
+            raise ValueError("ShardSession needs exactly one of group / comm / rccl_id")
+        if rccl_id is not None and len(rccl_id) != 128:
+            raise ValueError("rccl_id must be the 128 bytes of rccl_unique_id()")
         self.rank, self.world = int(rank), int(world)
-        self.group, self.comm = group, comm
+        self.group, self.comm, self.rccl_id = group, comm, rccl_id
         chans, rows = shard_layout(nsub, nchan, world)
         self.chan_range = chans[self.rank]
         self.row_range = rows[self.rank]
@@ -532,6 +554,11 @@ class ShardSession(GpuSession):
             self._create_name = "ic_session_create_grouped"
             return self.lib.ic_session_create_grouped(C.byref(self.params), device, self.group.h,
                                                       self.rank, C.byref(h))
+        if self.rccl_id is not None:
+            self._create_name = "ic_session_create_rccl"
+            self._id_buf = C.create_string_buffer(self.rccl_id, 128)
+            return self.lib.ic_session_create_rccl(C.byref(self.params), device, self.rank, self.world,
+                                                   C.cast(self._id_buf, C.c_void_p), C.byref(h))
         self._ops = self.comm.ops()
         return self.lib.ic_session_create_shard(C.byref(self.params), device, self.rank,
                                                 self.world, C.byref(self._ops), C.byref(h))

@@ -8,8 +8,12 @@
 // stream; no host synchronisation is implied.
 //
 // Transports:
+//   RcclComm     — native RCCL over xGMI (one process per GPU): a
+//                  communicator per shard session, every collective issued
+//                  from C++ on the session stream; the host only hands the
+//                  unique id of rank 0 to the other ranks once.
 //   CallbackComm — the host's ic_comm_ops (one process per GPU; the Python
-//                  host binds torch.distributed, i.e. RCCL over xGMI).
+//                  host binds torch.distributed: gloo in the CPU tests).
 //   LocalComm    — shards of one process (threads), device-to-device / peer
 //                  copies ordered by HIP events and a host barrier.
 #pragma once
@@ -37,6 +41,11 @@ public:
 };
 
 Comm *make_callback_comm(const ic_comm_ops &ops, int rank, int world);
+
+// RCCL: 128-byte unique id (rank 0's, handed to every rank); the communicator
+// is created on the current device.  nullptr + message in *err on failure.
+int rccl_unique_id(void *id, const char **err);
+Comm *make_rccl_comm(const void *unique_id, int rank, int world, const char **err);
 
 struct LocalGroup;
 LocalGroup *local_group_create(int world);

@@ -1,4 +1,7 @@
 // ic_comm.hip — shard exchange transports (see ic_comm.h).
+#include <dlfcn.h>
+#include <string.h>
+
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -239,6 +242,162 @@ Comm *make_local_comm(LocalGroup *g, int rank, int device, const char **err)
     if (c->init()) {
         delete c;
         *err = "hipEventCreate failed";
+        return nullptr;
+    }
+    return c;
+}
+
+// ------------------------------------------------------------ native RCCL
+
+// librccl is opened on first use (dlopen, RTLD_LOCAL, the ROCm install's copy):
+// a process that never asks for the native transport never loads it, and
+// torch's own bundled RCCL, if loaded, stays a separate instance.
+namespace {
+typedef struct ncclComm *nccl_comm_t;
+typedef struct {
+    char internal[128];
+} nccl_id_t;
+enum { kNcclInt8 = 0, kNcclUint8 = 1, kNcclInt32 = 2, kNcclSum = 0 };
+struct RcclApi {
+    void *h = nullptr;
+    const char *err = nullptr;
+    int (*GetUniqueId)(nccl_id_t *) = nullptr;
+    int (*CommInitRank)(nccl_comm_t *, int, nccl_id_t, int) = nullptr;
+    int (*CommDestroy)(nccl_comm_t) = nullptr;
+    int (*CommAbort)(nccl_comm_t) = nullptr;
+    int (*AllGather)(const void *, void *, size_t, int, nccl_comm_t, hipStream_t) = nullptr;
+    int (*AllReduce)(const void *, void *, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
+    int (*Send)(const void *, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
+    int (*Recv)(void *, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
+    int (*GroupStart)() = nullptr;
+    int (*GroupEnd)() = nullptr;
+    const char *(*GetErrorString)(int) = nullptr;
+};
+
+RcclApi *rccl_api()
+{
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char *paths[] = {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"};
+        for (const char *p : paths)
+            if ((api.h = dlopen(p, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!api.h) {
+            api.err = "librccl.so.1 not found (dlopen)";
+            return;
+        }
+#define SYM(F)                                                   \
+    *(void **)(&api.F) = dlsym(api.h, "nccl" #F);                \
+    if (!api.F) {                                                \
+        api.err = "librccl lacks nccl" #F;                       \
+        return;                                                  \
+    }
+        SYM(GetUniqueId) SYM(CommInitRank) SYM(CommDestroy) SYM(CommAbort) SYM(AllGather) SYM(AllReduce)
+        SYM(Send) SYM(Recv) SYM(GroupStart) SYM(GroupEnd) SYM(GetErrorString)
+#undef SYM
+    });
+    return api.err ? nullptr : &api;
+}
+}  // namespace
+
+int rccl_unique_id(void *id, const char **err)
+{
+    RcclApi *a = rccl_api();
+    if (!a) {
+        *err = "librccl unavailable (dlopen of /opt/rocm/lib/librccl.so.1 failed)";
+        return -1;
+    }
+    nccl_id_t u;
+    const int rc = a->GetUniqueId(&u);
+    if (rc != 0) {
+        *err = a->GetErrorString(rc);
+        return -1;
+    }
+    memcpy(id, &u, sizeof u);
+    return 0;
+}
+
+// One RCCL communicator per shard session, on the session's device; every
+// exchange is issued from here on the session stream (no host callbacks):
+// all-gathers and the counter all-reduce as RCCL collectives, the all-to-alls
+// as one group of per-peer sends and receives.
+class RcclComm final : public Comm {
+public:
+    ~RcclComm() override
+    {
+        if (comm) {
+            if (aborted)
+                (void)api->CommAbort(comm);
+            else
+                (void)api->CommDestroy(comm);
+        }
+    }
+    int alloc(void **p, size_t bytes) override { return hipMalloc(p, bytes ? bytes : 8) == hipSuccess ? 0 : -1; }
+    void release(void *p) override
+    {
+        if (p) (void)hipFree(p);
+    }
+    int allgather(const void *send, void *recv, size_t bytes, hipStream_t st) override
+    {
+        return check(api->AllGather(send, recv, bytes, kNcclUint8, comm, st));
+    }
+    int alltoallv(const void *send, const size_t *sb, void *recv, const size_t *rb, hipStream_t st) override
+    {
+        if (api->GroupStart() != 0) return -1;
+        size_t so = 0, ro = 0;
+        int rc = 0;
+        for (int p = 0; p < world && rc == 0; ++p) {
+            if (sb[p]) rc = api->Send((const char *)send + so, sb[p], kNcclUint8, p, comm, st);
+            if (rc == 0 && rb[p]) rc = api->Recv((char *)recv + ro, rb[p], kNcclUint8, p, comm, st);
+            so += sb[p];
+            ro += rb[p];
+        }
+        const int rc2 = api->GroupEnd();
+        return check(rc ? rc : rc2);
+    }
+    int allreduce_sum_i32(int32_t *buf, size_t n, hipStream_t st) override
+    {
+        return check(api->AllReduce(buf, buf, n, kNcclInt32, kNcclSum, comm, st));
+    }
+    void abort() override
+    {
+        if (comm && !aborted) {
+            aborted = true;
+            (void)api->CommAbort(comm);
+            comm = nullptr;
+        }
+    }
+
+private:
+    RcclApi *api = nullptr;
+    nccl_comm_t comm = nullptr;
+    bool aborted = false;
+    int check(int rc)
+    {
+        if (rc != 0) abort();
+        return rc == 0 ? 0 : -1;
+    }
+    friend Comm *make_rccl_comm(const void *, int, int, const char **);
+};
+
+Comm *make_rccl_comm(const void *unique_id, int rank, int world, const char **err)
+{
+    RcclApi *a = rccl_api();
+    if (!a) {
+        *err = "librccl unavailable (dlopen of /opt/rocm/lib/librccl.so.1 failed)";
+        return nullptr;
+    }
+    nccl_id_t u;
+    memcpy(&u, unique_id, sizeof u);
+    auto *c = new RcclComm();
+    c->api = a;
+    c->rank = rank;
+    c->world = world;
+    const int rc = a->CommInitRank(&c->comm, world, u, rank);   // on the current (session) device
+    if (rc != 0) {
+        c->comm = nullptr;
+        *err = a->GetErrorString(rc);
+        delete c;
         return nullptr;
     }
     return c;

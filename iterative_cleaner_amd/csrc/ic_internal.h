@@ -105,6 +105,7 @@ enum KernelId {
     K_EXCHANGE,       // the collectives themselves (host transport or peer copies)
     K_TNORM,          // fit_mode 1: sum(T*T)
     K_ROTATE,         // fractional dedispersion (FFT phase rotation)
+    K_FIT_LANES,      // the exact fit as one persistent launch (IC_FIT_LANES)
     K_COUNT
 };
 
@@ -216,6 +217,22 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
                             const unsigned long long *nctr, long bound, double *amp, int32_t *info,
                             int32_t *next_list, unsigned long long *ctr, unsigned *done, int32_t *host_n,
                             uint8_t *late = nullptr);
+// The whole exact fit in one persistent launch (k_fit_lanes): `waves` waves of
+// 64 lanes, each lane taking profiles from *qhead (zeroed) until P are taken.
+// ls: lmdif state of the lane slots, kLaneFieldsMax f64 fields of `lst` >=
+// waves * 64 slots; U: k_fit_prep's shared qrfac; dummy_row: a zero row of D
+// (waiting lanes' DMA reads it); sweeps[0] += the profile sweeps made,
+// sweeps[1] += 64 x the wave sweeps (lane slots swept, waiting lanes included).
+// phase 0: to completion; 1: until the queue runs out, then every profile in
+// flight is saved in its slot, flagged in late[] and appended to flist (count
+// in *fctr, RoundList's packed form: nA = count); 2: resume those to completion.
+constexpr int kLaneFieldsMax = 25;
+hipError_t launch_fit_lanes(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
+                            int dtiled, int dummy_row, int waves, double *ls, long lst, const double *U,
+                            unsigned *qhead, double *amp, int32_t *info, unsigned long long *sweeps, int phase = 0,
+                            uint8_t *late = nullptr, int32_t *flist = nullptr, unsigned long long *fctr = nullptr);
+// waves of k_fit_lanes resident at once on `device` (occupancy x CUs), 0 on error
+int fit_lanes_max_waves(int device);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
                            const FitStateArrays &S, double *amp, int32_t *info, unsigned long long *sweeps);

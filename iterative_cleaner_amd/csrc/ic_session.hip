@@ -60,7 +60,7 @@ const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",
                                      "k_fscrunch",      "k_tscrunch",  "k_fit_pass", "k_fit_state",
                                      "k_diag",          "k_linestats", "k_combine",  "k_residual",
                                      "k_fit_tail",      "k_sb_tree",   "k_shard_pack", "exchange",
-                                     "k_tnorm",         "k_rotate"};
+                                     "k_tnorm",         "k_rotate",    "k_fit_lanes"};
 
 constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
 
@@ -133,6 +133,10 @@ struct Session {
     LineStatsArgs ls_knobs;     // row-median form (IC_OPT_ROWSTAT_*)
     long tail_threshold = kTailProfiles;   // IC_OPT_FIT_TAIL
     bool diag_chain = true;     // IC_OPT_DIAG_CHAIN: k_diag_cl at nbin 1024/2048/4096
+    int fit_schedule = IC_FIT_ROUNDS;   // IC_OPT_FIT_SCHEDULE
+    int lane_waves = 0;         // IC_OPT_FIT_LANE_WAVES (0: every wave the device holds at once)
+    int lane_waves_max = 0;     // lane slots / 64 of `lanes` (k_fit_lanes' state)
+    double *lanes = nullptr;    // k_fit_lanes' lmdif state, kLaneFieldsMax x lane_slots
     double sync_timeout_s = 600.0;   // IC_OPT_SYNC_TIMEOUT_MS
     // a host wait timed out with kernels of this session possibly still in
     // flight: every later call but ic_session_destroy fails (IC_ESTATE), and
@@ -361,7 +365,8 @@ void free_all(Session *s)
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
-                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph, s->T2, s->fs.U};
+                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph, s->T2, s->fs.U,
+                    s->lanes};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     void *rbufs[] = {s->std_r, s->mean_r, s->fft_r, s->ptp_r, s->valid_r};
@@ -710,8 +715,12 @@ int shard_rowstats(Session *s, const LineStatsArgs &la)
 // already fitted run on s->dstream (fork_diag); the survivors of that round
 // are kept in the third list buffer for the main stream's second pass.
 int fork_diag(Session *s, const DiagArgs &da, int r);
-// the tail's sweep counter, after the round counters (accumulates over a run)
-unsigned long long *tail_counter(Session *s) { return (unsigned long long *)(s->rcount + kRoundWords); }
+// after the round counters: k_fit_lanes' queue head (u32, zeroed with them by
+// k_fit_init), then the tail's and k_fit_lanes' sweep counters (u64 each,
+// accumulating over a run)
+unsigned *lane_queue(Session *s) { return (unsigned *)(s->rcount + kRoundWords); }
+unsigned long long *tail_counter(Session *s) { return (unsigned long long *)(s->rcount + kRoundWords + 2); }
+unsigned long long *lane_counter(Session *s) { return (unsigned long long *)(s->rcount + kRoundWords + 4); }
 
 int run_fit(Session *s, const DiagArgs *fork)
 {
@@ -721,7 +730,7 @@ int run_fit(Session *s, const DiagArgs *fork)
     // zeroes too: per round, blocks done << 32 | survivors (the tail's sweep
     // counter after them accumulates over the run: zeroed and read once per
     // run by ic_run), and the late flags the fork round's state kernel sets
-    CK(launch_fit_init(s->stream, s->fs, P, s->rcount, kRoundWords, fork ? s->late : nullptr));
+    CK(launch_fit_init(s->stream, s->fs, P, s->rcount, kRoundWords + 2, fork ? s->late : nullptr));
     CK(launch_fit_prep(s->stream, s->fs, s->T64, nbin));
     unsigned long long *ctr = (unsigned long long *)s->rcount;
     unsigned *done = (unsigned *)(s->rcount + 2 * kMaxRounds);
@@ -786,6 +795,41 @@ int run_fit(Session *s, const DiagArgs *fork)
     s->fit_rounds = effective;
     s->stats.fit_rounds += effective;
     s->stats.fit_profile_sweeps += swept;
+    return 0;
+}
+
+// The exact fit as one persistent launch (IC_FIT_LANES, k_fit_lanes): every
+// lane runs lmdif for one profile after another from a shared queue.
+// fork != nullptr: the launch stops once the queue has run out (phase 1),
+// leaving the profiles in flight flagged in s->late and listed in the third
+// list buffer (count in round word 0); the diagnostics of all the others run
+// on dstream (fork_diag) while phase 2 finishes the ones in flight, and the
+// main stream's pass B measures those after it (run_impl).
+int run_fit_lanes(Session *s, const DiagArgs *fork)
+{
+    s->fork_round = -1;
+    const long P = (long)s->P;
+    if (fork) CK(hipMemsetAsync(s->late, 0, P, s->stream));
+    CK(launch_fit_init(s->stream, s->fs, 0, s->rcount, kRoundWords + 2, nullptr));   // round words, queue head
+    CK(launch_fit_prep(s->stream, s->fs, s->T64, s->p.nbin));
+    const int waves = s->lane_waves > 0 ? std::min(s->lane_waves, s->lane_waves_max) : s->lane_waves_max;
+    const long lst = (long)s->lane_waves_max * 64;
+    if (!fork) {
+        LAUNCH(s, K_FIT_LANES, launch_fit_lanes(s->stream, s->D, s->T64, P, s->p.nbin, s->ldD, s->dtiled,
+                                                (int)s->Ppad, waves, s->lanes, lst, s->fs.U, lane_queue(s), s->amp,
+                                                s->info, lane_counter(s)));
+    } else {
+        LAUNCH(s, K_FIT_LANES, launch_fit_lanes(s->stream, s->D, s->T64, P, s->p.nbin, s->ldD, s->dtiled,
+                                                (int)s->Ppad, waves, s->lanes, lst, s->fs.U, lane_queue(s), s->amp,
+                                                s->info, lane_counter(s), 1, s->late, s->lists + 2 * s->P,
+                                                (unsigned long long *)s->rcount));
+        if (int rc = fork_diag(s, *fork, 0)) return rc;
+        LAUNCH(s, K_FIT_LANES, launch_fit_lanes(s->stream, s->D, s->T64, P, s->p.nbin, s->ldD, s->dtiled,
+                                                (int)s->Ppad, waves, s->lanes, lst, s->fs.U, lane_queue(s), s->amp,
+                                                s->info, lane_counter(s), 2));
+    }
+    s->fit_rounds = 1;
+    s->stats.fit_rounds += 1;
     return 0;
 }
 
@@ -932,9 +976,10 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     s->raw = s->slot_raw[0];
     // the closed-form fit reads the raw cube (no fit cube, no lmdif state), unless
     // the dedispersion is the FFT rotation: then the rotated fit cube is kept
+    // + one group of 64 zero rows (row Ppad on: the rows k_fit_lanes' waiting lanes read)
     if (exact || p.dedisp_mode == IC_DEDISP_FFT) {
-        AL(s->D, s->Ppad * (size_t)s->ldD);
-        if (hipMemset(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD) != hipSuccess)
+        AL(s->D, (s->Ppad + 64) * (size_t)s->ldD);
+        if (hipMemset(s->D, 0, sizeof(float) * (s->Ppad + 64) * (size_t)s->ldD) != hipSuccess)
             return bail(fail(IC_EHIP, "hipMemset(D) failed"));
     }
     AL(s->TT, 1);
@@ -992,7 +1037,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     if (exact) AL(s->lists, 3 * P);   // two ping-pong round lists + the fork round's survivors
-    AL(s->rcount, (size_t)kRoundWords + 2);   // + the tail's sweep counter (u64)
+    AL(s->rcount, (size_t)kRoundWords + 8);   // + the lanes' queue, the tail's and the lanes' sweep counters
     if (exact && !s->fftded) AL(s->late, P);
     if (sharded) {
         const char *cerr = nullptr;
@@ -1058,7 +1103,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
             return bail(fail(IC_EHIP, "hipEventCreate failed"));
     if (hipEventCreateWithFlags(&s->sev, hipEventDisableTiming) != hipSuccess)
         return bail(fail(IC_EHIP, "hipEventCreate failed"));
-    if (hipHostMalloc((void **)&s->h_small, sizeof(int32_t) * ((size_t)p.max_iter + 16)) != hipSuccess)
+    if (hipHostMalloc((void **)&s->h_small, sizeof(int32_t) * ((size_t)p.max_iter + 20)) != hipSuccess)
         return bail(fail(IC_ENOMEM, "hipHostMalloc(readback) failed"));
     if (exact) {
         // fit state: 23 double arrays + 5 int arrays, each padded to 256 B
@@ -1075,6 +1120,13 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         for (auto *q : ip) { *q = (int32_t *)b; b += istride; }
         // k_fit_prep's 4 scalars
         if (dalloc(&s->fs.U, 8) != hipSuccess) return bail(fail(IC_ENOMEM, "hipMalloc(fit prep) failed"));
+        // k_fit_lanes' lane slots: every wave the device holds at once, at most one per 64 profiles
+        if (!s->fftded) {
+            const int mw = fit_lanes_max_waves(device);
+            s->lane_waves_max = (int)std::min<size_t>(mw > 0 ? (size_t)mw : 1024, s->Ppad / 64);
+            if (dalloc(&s->lanes, (size_t)kLaneFieldsMax * 64 * s->lane_waves_max) != hipSuccess)
+                return bail(fail(IC_ENOMEM, "hipMalloc(lane state) failed"));
+        }
     }
     // twiddles exp(-2 pi i q / n) and the pairwise plan
     std::vector<double2> tw(nbin);
@@ -1120,6 +1172,23 @@ int ic_session_create_shard(const ic_params *params, int device, int rank, int w
     const ic_comm_ops o = *ops;
     return create_session(params, device, rank, world, true,
                           [&](const char **) -> Comm * { return make_callback_comm(o, rank, world); }, out);
+}
+
+int ic_rccl_unique_id(void *id_out)
+{
+    if (!id_out) return fail(IC_EINVAL, "null argument");
+    const char *err = nullptr;
+    if (rccl_unique_id(id_out, &err)) return fail(IC_ECOMM, "ncclGetUniqueId: %s", err ? err : "failed");
+    return IC_OK;
+}
+
+int ic_session_create_rccl(const ic_params *params, int device, int rank, int world, const void *unique_id,
+                           void **out)
+{
+    if (!unique_id) return fail(IC_EINVAL, "null unique id");
+    return create_session(params, device, rank, world, true,
+                          [&](const char **err) -> Comm * { return make_rccl_comm(unique_id, rank, world, err); },
+                          out);
 }
 
 int ic_group_create(int world, void **group)
@@ -1198,7 +1267,7 @@ int ic_upload_pols(void *session, const float *data, int npol, const float *w0, 
                                         hipMemcpyHostToDevice, s->stream);
         if (e == hipSuccess) e = launch_pscrunch(s->stream, s->raw, pol1, s->N);
         if (e == hipSuccess && s->D)
-            e = hipMemsetAsync(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD, s->stream);
+            e = hipMemsetAsync(s->D, 0, sizeof(float) * (s->Ppad + 64) * (size_t)s->ldD, s->stream);
         if (!s->D) {
             if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
             (void)hipFree(pol1);
@@ -1403,7 +1472,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     s->bad_fits.clear();
     int x = 0, loops = -1, n_iter = 0, converged = 0;
     // k_fit_tail's sweep counter (after the per-round counters): one run's total
-    CK(hipMemsetAsync(tail_counter(s), 0, sizeof(unsigned long long), s->stream));
+    CK(hipMemsetAsync(tail_counter(s), 0, 3 * sizeof(unsigned long long), s->stream));   // + lane sweeps, slots
     while (x < p.max_iter) {
         x += 1;
         ++n_iter;
@@ -1411,7 +1480,11 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         DiagArgs da = diag_args(s, pr_start, pr_end);
         if (p.fit_mode == IC_FIT_EXACT) {
             const bool fork = s->diag_fork > 0 && s->dstream && s->late && diag_list_supported(da);
-            if (int rc = run_fit(s, fork ? &da : nullptr)) return rc;
+            if (s->fit_schedule == IC_FIT_LANES) {
+                if (int rc = run_fit_lanes(s, fork ? &da : nullptr)) return rc;
+            } else {
+                if (int rc = run_fit(s, fork ? &da : nullptr)) return rc;
+            }
         } else {
             LAUNCH(s, K_TNORM, launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
         }
@@ -1475,11 +1548,12 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         int32_t *moves = s->h_small + p.max_iter + 6;                               // pinned
         unsigned long long *tsw = (unsigned long long *)(s->h_small + ((p.max_iter + 9) & ~1));   // 8-B aligned
         CK(hipMemcpyAsync(moves, s->wflag + nsub, sizeof *moves, hipMemcpyDeviceToHost, s->stream));
-        CK(hipMemcpyAsync(tsw, tail_counter(s), sizeof *tsw, hipMemcpyDeviceToHost,
-                          s->stream));
+        CK(hipMemcpyAsync(tsw, tail_counter(s), 3 * sizeof *tsw, hipMemcpyDeviceToHost, s->stream));
         CK(spin_sync(s));
         s->stats.window_moves = *moves;
-        s->stats.fit_tail_sweeps += (int64_t)*tsw;
+        s->stats.fit_tail_sweeps += (int64_t)tsw[0];
+        s->stats.fit_profile_sweeps += (int64_t)tsw[1];   // k_fit_lanes' sweeps (0 under rounds)
+        s->stats.fit_lane_slots += (int64_t)tsw[2];
     }
     // timing events are read when asked for (ic_get_kernel_times), not here
     if (loops_out) *loops_out = loops;
@@ -1664,6 +1738,17 @@ int ic_set_option(void *session, int option, int64_t v)
         if (v < 1) return fail(IC_EINVAL, "IC_OPT_SYNC_TIMEOUT_MS=%lld < 1", (long long)v);
         s->sync_timeout_s = (double)v / 1000.0;
         return IC_OK;
+    case IC_OPT_FIT_SCHEDULE:
+        if (v != IC_FIT_ROUNDS && v != IC_FIT_LANES)
+            return fail(IC_EINVAL, "IC_OPT_FIT_SCHEDULE=%lld (IC_FIT_ROUNDS or IC_FIT_LANES)", (long long)v);
+        if (v == IC_FIT_LANES && !(exact_shift && s->lanes))
+            return fail(IC_EINVAL, "IC_OPT_FIT_SCHEDULE=IC_FIT_LANES needs the exact fit with integer dedispersion");
+        s->fit_schedule = (int)v;
+        return IC_OK;
+    case IC_OPT_FIT_LANE_WAVES:
+        if (v < 0 || v > 1 << 20) return fail(IC_EINVAL, "IC_OPT_FIT_LANE_WAVES=%lld outside 0..2^20", (long long)v);
+        s->lane_waves = (int)v;
+        return IC_OK;
     default:
         return fail(IC_EINVAL, "unknown option %d", option);
     }
@@ -1683,6 +1768,8 @@ int ic_get_option(void *session, int option, int64_t *out)
     case IC_OPT_ROWSTAT_MINLEN: *out = s->ls_knobs.grp_minlen; return IC_OK;
     case IC_OPT_DIAG_CHAIN: *out = s->diag_chain ? 1 : 0; return IC_OK;
     case IC_OPT_SYNC_TIMEOUT_MS: *out = (int64_t)(s->sync_timeout_s * 1000.0 + 0.5); return IC_OK;
+    case IC_OPT_FIT_SCHEDULE: *out = s->fit_schedule; return IC_OK;
+    case IC_OPT_FIT_LANE_WAVES: *out = s->lane_waves; return IC_OK;
     default: return fail(IC_EINVAL, "unknown option %d", option);
     }
 }

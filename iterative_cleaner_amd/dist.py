@@ -275,3 +275,15 @@ class TorchComm:
                      nat.ALLREDUCE_FN(guard(c_allreduce)))
         self._ops = nat.CommOps(None, *self._fns)
         return self._ops
+
+
+def share_rccl_id(group=None) -> bytes:
+    """Rank 0's RCCL unique id (_native.rccl_unique_id) on every rank of the
+    process group, for ShardSession(rccl_id=...): the one host exchange the
+    native RCCL transport needs (torch.distributed object broadcast)."""
+    import torch.distributed as dist
+
+    from . import _native
+    obj = [_native.rccl_unique_id() if dist.get_rank(group) == 0 else None]
+    dist.broadcast_object_list(obj, src=0 if group is None else dist.get_global_rank(group, 0), group=group)
+    return obj[0]

@@ -23,8 +23,15 @@
  *                     irfft(rfft(x) * phasor) within one f32 ulp
  *   orc_clean_loop    the while loop, :83-146
  *
- * Build: gcc -O2 -fPIC -shared -ffp-contract=off -fno-fast-math (oracle/Makefile)
+ * Build: gcc -O2 -fPIC -shared -ffp-contract=off -fno-fast-math -fopenmp (oracle/Makefile)
  * Pinned against the tests/golden npz fixtures (reference outputs) and live scipy.
+ *
+ * Threads (OpenMP, OMP_NUM_THREADS): the loops over profiles, subints and
+ * median lines are split over threads.  Every item is computed by one thread
+ * with the same operations in the same order as the serial loop, so the bits
+ * do not depend on the thread count; only the order in which independent
+ * items finish does.  The whole-archive checks at BASELINE.json's sizes
+ * (tests/test_wholearchive_gpu.py) need that parallelism to run in seconds.
  */
 #include <float.h>
 #include <math.h>
@@ -325,7 +332,10 @@ void orc_fit_residual(int P, int m, const float *T, const float *D,
                       int pr_on, double pr_factor, int pr_start, int pr_end,
                       double *amp, int32_t *info, float *R)
 {
+#pragma omp parallel
+    {
     double *work = (double *)malloc(sizeof(double) * 3 * (size_t)m);
+#pragma omp for schedule(dynamic, 64)
     for (int k = 0; k < P; ++k) {
         const float *p = D + (size_t)k * m;
         double x;
@@ -345,6 +355,7 @@ void orc_fit_residual(int P, int m, const float *T, const float *D,
         }
     }
     free(work);
+    }
 }
 
 /* ------------------------------------------------------- archive stand-in */
@@ -363,8 +374,11 @@ void orc_baseline(int nsub, int nchan, int n, const float *raw, const float *W,
     int width = (int)(duty * (double)n);
     if (width < 1) width = 1;
     const int nsb = (nchan + SUPER_BLOCK - 1) / SUPER_BLOCK;
+#pragma omp parallel
+    {
     double *tot = (double *)malloc(sizeof(double) * (size_t)n);
     double *part = (double *)malloc(sizeof(double) * (size_t)n * nsb);
+#pragma omp for schedule(dynamic, 1)
     for (int s = 0; s < nsub; ++s) {
         for (int b0 = 0; b0 < nchan; b0 += SUPER_BLOCK) {
             double *pb = part + (size_t)(b0 / SUPER_BLOCK) * n;
@@ -401,6 +415,7 @@ void orc_baseline(int nsub, int nchan, int n, const float *raw, const float *W,
     }
     free(tot);
     free(part);
+    }
 }
 
 /* fit cube (iterative_cleaner.py:96-100): D = f32(ded - base(w0)). */
@@ -409,6 +424,7 @@ void orc_fit_cube(int nsub, int nchan, int n, const float *raw, const float *w0,
 {
     float *base = (float *)malloc(sizeof(float) * (size_t)nsub * nchan);
     orc_baseline(nsub, nchan, n, raw, w0, shift, duty, base, NULL);
+#pragma omp parallel for schedule(static)
     for (int s = 0; s < nsub; ++s)
         for (int c = 0; c < nchan; ++c) {
             const float *prof = raw + ((size_t)s * nchan + c) * n;
@@ -439,10 +455,14 @@ static void orc_scrunch(int nsub, int nchan, int n, const float *raw, const floa
 {
     const int nsb = (nchan + SUPER_BLOCK - 1) / SUPER_BLOCK;
     double *num = (double *)malloc(sizeof(double) * (size_t)n);
-    double *part = (double *)malloc(sizeof(double) * (size_t)n * nsb);
-    double *wpart = (double *)malloc(sizeof(double) * (size_t)nsb);
     float *F = (float *)malloc(sizeof(float) * (size_t)nsub * n);
     float *wf = (float *)malloc(sizeof(float) * (size_t)nsub);
+#pragma omp parallel
+    {
+    double *num = (double *)malloc(sizeof(double) * (size_t)n);
+    double *part = (double *)malloc(sizeof(double) * (size_t)n * nsb);
+    double *wpart = (double *)malloc(sizeof(double) * (size_t)nsb);
+#pragma omp for schedule(dynamic, 1)
     for (int s = 0; s < nsub; ++s) {
         for (int b0 = 0; b0 < nchan; b0 += SUPER_BLOCK) {
             int b1 = b0 + SUPER_BLOCK < nchan ? b0 + SUPER_BLOCK : nchan;
@@ -466,6 +486,8 @@ static void orc_scrunch(int nsub, int nchan, int n, const float *raw, const floa
         for (int i = 0; i < n; ++i) F[(size_t)s * n + i] = (wsum != 0.0) ? (float)(num[i] / wsum) : 0.0f;
         wf[s] = (float)wsum;
     }
+    free(num); free(part); free(wpart);
+    }
     double wt = 0.0;
     for (int i = 0; i < n; ++i) num[i] = 0.0;
     for (int s = 0; s < nsub; ++s) {
@@ -477,7 +499,7 @@ static void orc_scrunch(int nsub, int nchan, int n, const float *raw, const floa
         float t = (wt != 0.0) ? (float)(num[i] / wt) : 0.0f;
         T[i] = t * 10000.0f;
     }
-    free(num); free(part); free(wpart); free(F); free(wf);
+    free(num); free(F); free(wf);
 }
 
 /* ------------------------------------------- fractional dedispersion (FFT) */
@@ -607,13 +629,19 @@ void orc_rotate(int nsub, int nchan, int n, const float *in, const float *base, 
     double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
     orc_twiddles(n, tw);
     orc_phasors(n, nchan, delay, ph);
-    for (int s = 0; s < nsub; ++s)
-        for (int c = 0; c < nchan; ++c) {
-            const size_t k = (size_t)s * nchan + c;
-            rotate1(n, in + k * n, base ? base[k] : 0.0f, ph + (size_t)c * (m + 1) * 2, sign, tw, work,
-                    out + k * n);
-        }
-    free(tw); free(ph); free(work);
+    free(work);
+#pragma omp parallel
+    {
+    double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
+#pragma omp for schedule(dynamic, 64)
+    for (long k = 0; k < (long)nsub * nchan; ++k) {
+        const int c = (int)(k % nchan);
+        rotate1(n, in + (size_t)k * n, base ? base[k] : 0.0f, ph + (size_t)c * (m + 1) * 2, sign, tw, work,
+                out + (size_t)k * n);
+    }
+    free(work);
+    }
+    free(tw); free(ph);
 }
 
 /* ------------------------------------------------------ pairwise sums */
@@ -701,7 +729,20 @@ void orc_fit_closed(int P, int m, const float *T, const float *D,
 /* max_k |DFT(x)_k| for k = 0..n/2 (np.fft.rfft magnitude; tolerance-level
  * agreement with pocketfft).  Radix-2 iterative for powers of two, direct
  * DFT otherwise.  work: 4*n doubles. */
-static double fftmax(const double *x, int n, double *work)
+/* the radix-2 twiddles cos / -sin(2 pi idx / n), idx < n/2, exactly as the
+ * butterflies below computed them per use: [2 * idx] = c, [2 * idx + 1] = s */
+static double *fft_table(int n)
+{
+    if (n < 2 || (n & (n - 1))) return NULL;
+    double *t = (double *)malloc(sizeof(double) * (size_t)n);
+    for (int idx = 0; idx < n / 2; ++idx) {
+        t[2 * idx] = cos(2.0 * M_PI * (double)idx / (double)n);
+        t[2 * idx + 1] = -sin(2.0 * M_PI * (double)idx / (double)n);
+    }
+    return t;
+}
+
+static double fftmax(const double *x, int n, double *work, const double *tab)
 {
     double best = 0.0;
     int pow2 = n > 0 && (n & (n - 1)) == 0;
@@ -723,8 +764,8 @@ static double fftmax(const double *x, int n, double *work)
                 for (int k = 0; k < half; ++k) {
                     /* twiddle exp(-2 pi i k/len) = exp(-2 pi i (k*step)/n) */
                     int idx = k * step;
-                    double c = cos(2.0 * M_PI * (double)idx / (double)n);
-                    double s = -sin(2.0 * M_PI * (double)idx / (double)n);
+                    double c = tab[2 * idx];
+                    double s = tab[2 * idx + 1];
                     double ur = re[st + k], ui = im[st + k];
                     double vr = re[st + k + half] * c - im[st + k + half] * s;
                     double vi = re[st + k + half] * s + im[st + k + half] * c;
@@ -760,9 +801,13 @@ static double fftmax(const double *x, int n, double *work)
 void orc_diagnostics(int P, int n, const float *X, const uint8_t *valid,
                      double *std_o, double *mean_o, float *ptp_o, double *fft_o)
 {
+    double *tab = fft_table(n);
+#pragma omp parallel
+    {
     double *d = (double *)malloc(sizeof(double) * (size_t)n);
     double *sq = (double *)malloc(sizeof(double) * (size_t)n);
     double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
+#pragma omp for schedule(dynamic, 256)
     for (int k = 0; k < P; ++k) {
         const float *x = X + (size_t)k * n;
         if (!valid[k]) {
@@ -770,7 +815,7 @@ void orc_diagnostics(int P, int n, const float *X, const uint8_t *valid,
             mean_o[k] = 0.0;
             ptp_o[k] = 1e20f;
             for (int i = 0; i < n; ++i) d[i] = (double)x[i];
-            fft_o[k] = fftmax(d, n, work);
+            fft_o[k] = fftmax(d, n, work, tab);
             continue;
         }
         float s32 = orc_sum_f32(x, n);
@@ -790,9 +835,11 @@ void orc_diagnostics(int P, int n, const float *X, const uint8_t *valid,
         std_o[k] = sqrt(var);
         mean_o[k] = mean;
         ptp_o[k] = nan ? NAN : (mx - mn);
-        fft_o[k] = fftmax(d, n, work);
+        fft_o[k] = fftmax(d, n, work, tab);
     }
     free(d); free(sq); free(work);
+    }
+    free(tab);
 }
 
 /* f64 data (psrchive get_data returning f64; ic_params.data_f64): X is the f64
@@ -801,9 +848,13 @@ void orc_diagnostics(int P, int n, const float *X, const uint8_t *valid,
 void orc_diagnostics_f64(int P, int n, const double *X, const uint8_t *valid,
                          double *std_o, double *mean_o, double *ptp_o, double *fft_o)
 {
+    double *tab = fft_table(n);
+#pragma omp parallel
+    {
     double *d = (double *)malloc(sizeof(double) * (size_t)n);
     double *sq = (double *)malloc(sizeof(double) * (size_t)n);
     double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
+#pragma omp for schedule(dynamic, 256)
     for (int k = 0; k < P; ++k) {
         const double *x = X + (size_t)k * n;
         if (!valid[k]) {
@@ -811,7 +862,7 @@ void orc_diagnostics_f64(int P, int n, const double *X, const uint8_t *valid,
             mean_o[k] = 0.0;
             ptp_o[k] = 1e20;    /* numpy.ma's f64 fill value (f32 data: f32(1e20)) */
             for (int i = 0; i < n; ++i) d[i] = x[i];
-            fft_o[k] = fftmax(d, n, work);
+            fft_o[k] = fftmax(d, n, work, tab);
             continue;
         }
         double mean = orc_sum_f64(x, n) / (double)n;
@@ -830,9 +881,11 @@ void orc_diagnostics_f64(int P, int n, const double *X, const uint8_t *valid,
         std_o[k] = sqrt(var);
         mean_o[k] = mean;
         ptp_o[k] = nan ? NAN : (mx - mn);
-        fft_o[k] = fftmax(d, n, work);
+        fft_o[k] = fftmax(d, n, work, tab);
     }
     free(d); free(sq); free(work);
+    }
+    free(tab);
 }
 
 /* ------------------------------------------------------ medians + scalers */
@@ -1032,9 +1085,12 @@ static void test_impl(int nsub, int nchan, const uint8_t *valid, const double *s
     double *ch = (double *)malloc(sizeof(double) * P);
     double *sb = (double *)malloc(sizeof(double) * P);
     double *S = (double *)malloc(sizeof(double) * 4 * P);
-    double *bufd = (double *)malloc(sizeof(double) * (size_t)L);
-    float *buff = (float *)malloc(sizeof(float) * (size_t)L);
     for (int which = 0; which < 4; ++which) {
+#pragma omp parallel
+        {
+        double *bufd = (double *)malloc(sizeof(double) * (size_t)L);
+        float *buff = (float *)malloc(sizeof(float) * (size_t)L);
+#pragma omp for schedule(dynamic, 8)
         for (int c = 0; c < nchan; ++c) {
             if (which == 0) scale_line_masked_d(nsub, std_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, bufd);
             if (which == 1) scale_line_masked_d(nsub, mean_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, bufd);
@@ -1042,6 +1098,7 @@ static void test_impl(int nsub, int nchan, const uint8_t *valid, const double *s
             if (which == 2 && !ptp64) scale_line_masked_f(nsub, ptp_d + c, valid + c, nchan, nchan, chanthresh, ch + c, nchan, buff);
             if (which == 3) scale_line_plain(nsub, fft_d + c, nchan, chanthresh, ch + c, nchan, bufd);
         }
+#pragma omp for schedule(dynamic, 1)
         for (int s = 0; s < nsub; ++s) {
             size_t o = (size_t)s * nchan;
             if (which == 0) scale_line_masked_d(nchan, std_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, bufd);
@@ -1049,6 +1106,8 @@ static void test_impl(int nsub, int nchan, const uint8_t *valid, const double *s
             if (which == 2 && ptp64) scale_line_masked_d(nchan, ptp64 + o, valid + o, 1, 1, subintthresh, sb + o, 1, bufd);
             if (which == 2 && !ptp64) scale_line_masked_f(nchan, ptp_d + o, valid + o, 1, 1, subintthresh, sb + o, 1, buff);
             if (which == 3) scale_line_plain(nchan, fft_d + o, 1, subintthresh, sb + o, 1, bufd);
+        }
+        free(bufd); free(buff);
         }
         for (size_t k = 0; k < P; ++k) S[which * P + k] = nanmax2(ch[k], sb[k]);
     }
@@ -1058,7 +1117,7 @@ static void test_impl(int nsub, int nchan, const uint8_t *valid, const double *s
         qsort(v, 4, sizeof(double), cmp_d);
         test[k] = ((0.0 + v[1]) + v[2]) / 2.0;
     }
-    free(ch); free(sb); free(S); free(bufd); free(buff);
+    free(ch); free(sb); free(S);
 }
 
 /* --------------------------------------------------------- the loop */
@@ -1143,6 +1202,7 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
             orc_fit_residual((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
         /* dededisperse + apply_weights */
         if (fftded) orc_rotate(nsub, nchan, n, Rd, NULL, delay, -1, Rx);
+#pragma omp parallel for schedule(static)
         for (int s = 0; s < nsub; ++s)
             for (int c = 0; c < nchan; ++c) {
                 size_t k = (size_t)s * nchan + c;

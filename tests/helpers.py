@@ -70,3 +70,35 @@ def thresholds(z, i):
     """(chanthresh, subintthresh) of a stats fixture case, int where the reference had an int."""
     thr, isint = z["thr_%d" % i], z["thr_is_int_%d" % i]
     return (int(thr[0]) if isint[0] else float(thr[0]), int(thr[1]) if isint[1] else float(thr[1]))
+
+
+def check_whole_loop(oracle_lib, raw, w0, shift, one, max_iter=5, residual=False):
+    """The whole cleaning loop of a full-size archive run independently by the
+    (threaded) C oracle, compared with the GPU run `one` (ic_run + ic_get_fit /
+    diagnostics / template [/ residual]) profile by profile: the loop count, the
+    per-iteration change and zero counts, the final template, every profile's
+    leastsq amplitude and status, std / mean / ptp and the weights bit for bit,
+    fftmax within 1e-9 relative, and the test values - the oracle's own, from the
+    oracle's diagnostics - within 1e-9 (only fftmax's last bits differ).  The
+    reference: iterative_cleaner.py:83-146 (fit :259-288, statistics :181-226)."""
+    ref = oracle_lib.clean_loop(raw, w0, shift, max_iter=max_iter, want_details=True, want_residual=residual)
+    assert one["loops"] == ref["loops"] and one["n_iter"] == len(one["changed"])
+    k = one["n_iter"]
+    assert np.array_equal(one["changed"], ref["changed"][:k]), "changed weights per loop"
+    assert np.array_equal(one["nzero"], ref["nzero"][:k]), "zero weights per loop"
+    assert bits_equal(one["T"], ref["T"][k - 1]), "final template"
+    assert bits_equal(one["amp"], ref["amp"]), "leastsq amplitudes (%d differ)" % int((one["amp"] != ref["amp"]).sum())
+    assert bits_equal(one["info"], ref["info"]), "leastsq status"
+    for name in ("std", "mean", "ptp"):
+        a, b = one[name], ref[name]
+        assert a.dtype == b.dtype and nan_equal(a, b), name
+        fin = ~np.isnan(b)
+        assert bits_equal(a[fin], b[fin]), name
+    g, f = one["fft"], ref["fft"]
+    assert np.all((g == f) | (np.abs(g - f) <= 1e-9 * np.abs(f)) | (np.isnan(g) & np.isnan(f))), "fftmax"
+    t, u = one["test"], ref["test"]
+    assert np.all((t == u) | (np.abs(t - u) <= 1e-9) | (np.isnan(t) & np.isnan(u))), "test values"
+    assert bits_equal(one["weights"], ref["weights"]), "weights (%d differ)" % int((one["weights"] != ref["weights"]).sum())
+    if residual:
+        assert nan_equal(one["residual"], ref["residual"]), "residual cube (-u)"
+    return ref

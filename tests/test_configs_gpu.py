@@ -7,18 +7,20 @@ make_block_cube_device):
   (whole archive), sampled-subint oracle checks of the exact
   fit and the diagnostics, whole-archive oracle test values and weights;
 * C4  128 x 1024 x 512 archives through batch.clean_batch (one lane and two):
-  every archive bit-equal to its own single session, oracle stage checks on one;
+  every archive bit-equal to its own single session, and one of them against
+  the whole loop of the C oracle (helpers.check_whole_loop);
 * C5  256 x 1024 x 4096, 30 % RFI, a seed whose loop runs to max_iter: the
-  residual cube (ic_get_residual, what -u unloads) and the fit / diagnostics of
-  sampled subints against the oracle, test values and weights whole-archive.
+  whole loop against the C oracle, the residual cube (ic_get_residual, what -u
+  unloads) included.
 
-Stage checks follow tests/test_fullsize_gpu.py: the whole-loop C oracle would
-take minutes at these sizes, so each stage of the final iteration is checked
-on its own (a subint's fit cube depends on nothing outside it)."""
+C3's sampled checks: the whole-loop oracle at 34 GB would need ~140 GB of host
+memory, so each stage of its final iteration is checked on its own (a subint's
+fit cube depends on nothing outside it) for sampled subints, and the test
+values of the GPU's diagnostics on the whole archive."""
 import numpy as np
 import pytest
 
-from helpers import bits_equal
+from helpers import bits_equal, check_whole_loop
 
 pytestmark = pytest.mark.gpu
 
@@ -154,10 +156,8 @@ def test_c4_batch_equals_single_sessions(c4, lanes, oracle_lib):
             one = _details(s)
         assert got[k]["loops"] == one["loops"] and np.array_equal(got[k]["changed"], one["changed"])
         assert bits_equal(got[k]["weights"], one["weights"]) and bits_equal(got[k]["test"], one["test"])
-        if k == 1:
-            subs = np.sort(np.random.default_rng(4).choice(nsub, size=8, replace=False))
-            _check_sampled_subints(oracle_lib, raw, w0, shift, one, subs)
-            _check_test_values(oracle_lib, w0, one)
+        if k == 1 and lanes == 1:
+            check_whole_loop(oracle_lib, raw, w0, shift, one)
 
 
 # ----------------------------------------------------------------------- C5
@@ -186,8 +186,6 @@ def test_c5_runs_to_max_iter(c5):
     assert one["weights"].size == 256 * 1024 and (one["weights"] == 0).sum() > 0.05 * one["weights"].size
 
 
-def test_c5_residual_fit_and_diagnostics(c5, oracle_lib):
+def test_c5_whole_loop_against_oracle(c5, oracle_lib):
     (raw, w0, shift), one = c5
-    subs = np.sort(np.random.default_rng(5).choice(raw.shape[0], size=6, replace=False))
-    _check_sampled_subints(oracle_lib, raw, w0, shift, one, subs)
-    _check_test_values(oracle_lib, w0, one)
+    check_whole_loop(oracle_lib, raw, w0, shift, one, residual=True)

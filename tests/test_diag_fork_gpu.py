@@ -13,12 +13,14 @@ from helpers import bits_equal, nan_equal
 pytestmark = pytest.mark.gpu
 
 
-def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1):
+def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1, schedule=0, lane_waves=0):
     from iterative_cleaner_amd import _native, synth
     nsub, nchan, nbin = shape
     data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
     raw = np.ascontiguousarray(data[:, 0])
-    with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=0, options={"diag_fork": fork}) as s:
+    with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=0,
+                            options={"diag_fork": fork, "fit_schedule": schedule,
+                                     "fit_lane_waves": lane_waves}) as s:
         if tail is not None:
             s.set_fit_tail(tail)
         s.upload(raw, w0, shift)
@@ -58,3 +60,23 @@ def test_fork_matches_c_oracle_whole_subints(monkeypatch, oracle_lib):
         assert nan_equal(x, ref[name]) and x.dtype == ref[name].dtype, name
     ff = ref["fft"]
     assert np.all(np.abs(diag[3] - ff) <= 1e-9 * np.abs(ff)), "fftmax"
+
+
+@pytest.mark.parametrize("shape", [(16, 256, 1024), (40, 512, 1024), (6, 256, 2048), (4, 192, 4096),
+                                   (24, 256, 256), (16, 300, 512)])
+@pytest.mark.parametrize("lane_waves", [0, 3])
+def test_lanes_fork_is_bit_identical(monkeypatch, shape, lane_waves):
+    """The persistent-lanes fit (IC_FIT_LANES) with the fork: phase 1 stops when
+    the queue runs out, the diagnostics of the finished profiles run beside
+    phase 2, the profiles it finishes are measured after it.  The same bits as
+    the unforked rounds schedule, with every wave the device holds and with 3
+    waves (most profiles then pass through lanes that were refilled)."""
+    from iterative_cleaner_amd import _native
+    ref = _run(monkeypatch, shape, 0, None)
+    for fork in (0, 3):
+        got = _run(monkeypatch, shape, fork, None, schedule=_native.FIT_LANES, lane_waves=lane_waves)
+        assert got[3]["loops"] == ref[3]["loops"]
+        assert bits_equal(got[3]["weights"], ref[3]["weights"]) and bits_equal(got[3]["test"], ref[3]["test"])
+        assert bits_equal(got[4], ref[4]) and bits_equal(got[5], ref[5])
+        for name, x0, x1 in zip(("std", "mean", "ptp", "fftmax"), ref[6], got[6]):
+            assert bits_equal(x1, x0), (fork, name)

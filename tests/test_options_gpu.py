@@ -16,10 +16,11 @@ def test_option_ranges_and_modes():
         defaults = {name: s.get_option(name) for name in _native.OPTIONS}
         assert defaults == {"fit_tail": 8192, "diag_fork": 3, "fork_delay": 1, "template_incr": 1,
                             "fit_tiled": 1, "rowstat_waves": 8, "rowstat_minlen": 1024, "diag_chain": 1,
-                            "sync_timeout_ms": 600000}
+                            "sync_timeout_ms": 600000, "fit_schedule": 0, "fit_lane_waves": 0}
         for name, bad in (("fit_tail", -1), ("diag_fork", 65), ("diag_fork", -1), ("fork_delay", 9),
                           ("template_incr", 2), ("fit_tiled", -1), ("rowstat_waves", 2),
-                          ("rowstat_minlen", 0), ("diag_chain", 3), ("sync_timeout_ms", 0)):
+                          ("rowstat_minlen", 0), ("diag_chain", 3), ("sync_timeout_ms", 0),
+                          ("fit_schedule", 2), ("fit_lane_waves", -1)):
             with pytest.raises(_native.NativeError, match="IC_OPT"):
                 s.set_option(name, bad)
             assert s.get_option(name) == defaults[name]
@@ -32,8 +33,12 @@ def test_option_ranges_and_modes():
     with _native.GpuSession(4, 64, 256, device=0, fit_mode=_native.FIT_CLOSED) as s:
         with pytest.raises(_native.NativeError, match="DIAG_FORK"):
             s.set_option("diag_fork", 3)
+        with pytest.raises(_native.NativeError, match="FIT_SCHEDULE"):
+            s.set_option("fit_schedule", _native.FIT_LANES)
         s.set_option("diag_fork", 0)
     with _native.GpuSession(4, 64, 256, device=0, delay=np.zeros(64)) as s:
+        with pytest.raises(_native.NativeError, match="FIT_SCHEDULE"):
+            s.set_option("fit_schedule", _native.FIT_LANES)
         with pytest.raises(_native.NativeError, match="TEMPLATE_INCR"):
             s.set_option("template_incr", 1)
         with pytest.raises(_native.NativeError, match="FIT_TILED"):

@@ -109,3 +109,36 @@ def test_torch_comm_one_rank_shard_session(backend):
         assert len(comm.bufs) == 0          # every exchange buffer released on close
     finally:
         dist.destroy_process_group()
+
+
+def test_native_rccl_one_rank_shard_session():
+    """The library's own RCCL transport (ic_session_create_rccl, the path
+    bench.py --gpus N takes on "nccl"): a one-rank communicator whose every
+    exchange is issued from C++ on the session stream, the unique id shared
+    through a one-rank process group as the multi-rank runs share it.  Must
+    equal the unsharded session bit for bit, on both fit schedules."""
+    import torch
+    import torch.distributed as dist
+
+    from iterative_cleaner_amd import _native, synth
+    from iterative_cleaner_amd.dist import share_rccl_id
+    data, w0, shift = synth.make_cube(8, 600, 256, 37, 0.2)
+    raw = np.ascontiguousarray(data[:, 0])
+    one = _single(raw, w0, shift)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    try:
+        for schedule in (_native.FIT_ROUNDS, _native.FIT_LANES):
+            rid = share_rccl_id()          # one unique id per communicator
+            assert len(rid) == 128
+            with _native.ShardSession(8, 600, 256, 0, 1, rccl_id=rid, device=0,
+                                      options={"fit_schedule": schedule}) as s:
+                s.upload(raw, w0, shift)
+                out = s.run()
+                amp, _ = s.fit()
+                T = s.template()
+            assert out["loops"] == one["loops"] and np.array_equal(out["changed"], one["changed"])
+            assert bits_equal(out["weights"], one["weights"]) and bits_equal(out["test"], one["test"])
+            assert bits_equal(amp, one["amp"]) and bits_equal(T, one["T"])
+    finally:
+        dist.destroy_process_group()
