@@ -138,7 +138,9 @@ def test_run_lanes_stuck_lanes_share_one_deadline():
     try:
         assert 0.5 < dt < 1.5, dt          # one shared 0.6-s deadline for three stuck lanes
         leaked = batch._LEAKED[n0:]
-        assert len(leaked) == 3
+        # the lanes stuck in a run (the one that ran tag 0 may have stopped at
+        # the close instead of entering its next run)
+        assert 2 <= len(leaked) <= 3
         for sess, handle, arrays in leaked:
             assert sess._ic_leaked and sess.h is None and handle is not None
             assert arrays and all(a[1].startswith("array-") for a in arrays)
