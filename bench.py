@@ -146,9 +146,10 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True)
     """Bytes a kernel's launches actually move, summed over the timed region
     (kernel table) - the implementation's own traffic model, not
     §8(d)'s.  `run`: one clean's counts, {"n_iter", "changed" (per iteration),
-    "fit_profile_sweeps", "fit_tail_sweeps", "window_moves"} (ic_run /
+    "fit_profile_sweeps", "fit_tail_sweeps", "fit_lane_sweeps", "window_moves"} (ic_run /
     ic_get_run_stats); every clean of the timed region is the same work.
-      k_fit_pass       every profile-sweep reads its 4*nbin-byte profile once;
+      k_fit_pass       every profile-sweep reads its 4*nbin-byte profile once
+                       (k_fit_tail, k_fit_lanes: their own sweeps, the same);
       k_fit_state      ~2 x 204 B of lmdif state per profile of a round (the
                        rounds' inputs are the sweeps of k_fit_pass);
       k_chan_partials  (every template-stage launch, k_chan_delta included)
@@ -167,8 +168,10 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True)
     nsb = (nchan + 255) // 256
     width = max(1, int(0.15 * nbin))
     n_iter = run["n_iter"]
-    if name in ("k_fit_pass", "k_fit_lanes"):   # the lanes' sweeps are counted in the same field
+    if name == "k_fit_pass":
         return 4 * nbin * run["fit_profile_sweeps"] * steps
+    if name == "k_fit_lanes":
+        return 4 * nbin * run.get("fit_lane_sweeps", 0) * steps
     if name == "k_fit_tail":
         return 4 * nbin * run["fit_tail_sweeps"] * steps
     if name == "k_fit_state":
@@ -715,11 +718,12 @@ def main():
                        "fit_mode": a.fit_mode, "dedisp": a.dedisp,
                        "profiles_per_archive": nsub * nchan, "loops": loops[-1], "iterations": n_iter,
                        "fit_rounds": stats["fit_rounds"],
-                       "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"])
+                       "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"]
+                                                        + stats["fit_lane_sweeps"])
                                                        / per_rank_P / max(1, n_iter), 2),
                        "fit_tail_sweeps": stats["fit_tail_sweeps"] // max(1, n_iter),
                        "fit_schedule": a.fit_schedule,
-                       "fit_lane_use": (round(stats["fit_profile_sweeps"] / stats["fit_lane_slots"], 3)
+                       "fit_lane_use": (round(stats["fit_lane_sweeps"] / stats["fit_lane_slots"], 3)
                                         if stats.get("fit_lane_slots") else None),
                        "near_threshold_profiles": stats["near_threshold"],
                        "parallelism": parallelism,

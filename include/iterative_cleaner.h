@@ -203,9 +203,11 @@ typedef struct {
     int32_t near_threshold;      /* last iteration: profiles whose test value lies within 1e-9 of
                                     the zap threshold 1.0, where fftmax's last bits (not
                                     bit-identical to numpy's pocketfft) could decide the zap */
-    int64_t fit_lane_slots;      /* IC_FIT_LANES: lane slots the waves swept (64 per wave sweep,
-                                    waiting lanes included); fit_profile_sweeps / this is the
+    int64_t fit_lane_slots;      /* k_fit_lanes: lane slots the waves swept (64 per wave sweep,
+                                    waiting lanes included); fit_lane_sweeps / this is the
                                     share of lanes doing work */
+    int64_t fit_lane_sweeps;     /* profile sweeps done by k_fit_lanes (IC_FIT_LANES, or the
+                                    late profiles under IC_OPT_FIT_LATE_LANES) */
 } ic_run_stats;
 int ic_get_run_stats(void *session, ic_run_stats *out);
 
@@ -239,6 +241,11 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  *                          from a shared queue; IC_FIT_ROUNDS
  *   IC_OPT_FIT_LANE_WAVES  waves of the IC_FIT_LANES launch, 0 = every wave the
  *                          device holds at once (more are capped to that); 0
+ *   IC_OPT_FIT_LATE_LANES  IC_FIT_ROUNDS: once at most this many profiles are
+ *                          still fitting (after round 1 or later, and above
+ *                          IC_OPT_FIT_TAIL), one k_fit_lanes launch resumes
+ *                          them from the rounds' state and finishes the fit,
+ *                          >= 0, 0 = never; 0
  *   IC_OPT_SYNC_TIMEOUT_MS longest host wait for the GPU, >= 1 ms; 600000.  A
  *                          wait that runs out fails its call with IC_EHIP and
  *                          marks the session failed: every later call on it
@@ -256,6 +263,7 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
 #define IC_OPT_SYNC_TIMEOUT_MS 9
 #define IC_OPT_FIT_SCHEDULE 10
 #define IC_OPT_FIT_LANE_WAVES 11
+#define IC_OPT_FIT_LATE_LANES 12
 #define IC_FIT_ROUNDS 0
 #define IC_FIT_LANES 1
 int ic_set_option(void *session, int option, int64_t value);

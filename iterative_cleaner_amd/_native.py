@@ -31,7 +31,7 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
 # choose how the loop is scheduled, never its arithmetic
 OPTIONS = {"fit_tail": 1, "diag_fork": 2, "fork_delay": 3, "template_incr": 4, "fit_tiled": 5,
            "rowstat_waves": 6, "rowstat_minlen": 7, "diag_chain": 8, "sync_timeout_ms": 9,
-           "fit_schedule": 10, "fit_lane_waves": 11}
+           "fit_schedule": 10, "fit_lane_waves": 11, "fit_late_lanes": 12}
 FIT_ROUNDS = 0   # IC_FIT_ROUNDS: sweep / state rounds over compacted lists (k_fit_pass, k_fit_state, k_fit_tail)
 FIT_LANES = 1    # IC_FIT_LANES: one persistent launch, a lane per profile at a time (k_fit_lanes)
 
@@ -56,7 +56,8 @@ class Params(C.Structure):
 class RunStats(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("fit_rounds", C.c_int32),
                 ("fit_profile_sweeps", C.c_int64), ("fit_tail_sweeps", C.c_int64),
-                ("window_moves", C.c_int32), ("near_threshold", C.c_int32), ("fit_lane_slots", C.c_int64)]
+                ("window_moves", C.c_int32), ("near_threshold", C.c_int32), ("fit_lane_slots", C.c_int64),
+                ("fit_lane_sweeps", C.c_int64)]
 
 
 class KernelTime(C.Structure):
@@ -370,7 +371,8 @@ class GpuSession:
                     fit_profile_sweeps=int(st.fit_profile_sweeps),
                     fit_tail_sweeps=int(st.fit_tail_sweeps),
                     window_moves=int(st.window_moves), near_threshold=int(st.near_threshold),
-                    fit_lane_slots=int(st.fit_lane_slots))
+                    fit_lane_slots=int(st.fit_lane_slots),
+                    fit_lane_sweeps=int(st.fit_lane_sweeps))
 
     def kernel_times(self):
         buf = (KernelTime * 32)()

@@ -225,12 +225,16 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
 // sweeps[1] += 64 x the wave sweeps (lane slots swept, waiting lanes included).
 // phase 0: to completion; 1: until the queue runs out, then every profile in
 // flight is saved in its slot, flagged in late[] and appended to flist (count
-// in *fctr, RoundList's packed form: nA = count); 2: resume those to completion.
+// in *fctr, RoundList's packed form: nA = count); 2: resume those to completion;
+// 3: the queue runs over a round list (list, nctr; at most `bound` entries),
+// every profile resumed from the state k_fit_state left in *S.
 constexpr int kLaneFieldsMax = 25;
 hipError_t launch_fit_lanes(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                             int dtiled, int dummy_row, int waves, double *ls, long lst, const double *U,
                             unsigned *qhead, double *amp, int32_t *info, unsigned long long *sweeps, int phase = 0,
-                            uint8_t *late = nullptr, int32_t *flist = nullptr, unsigned long long *fctr = nullptr);
+                            uint8_t *late = nullptr, int32_t *flist = nullptr, unsigned long long *fctr = nullptr,
+                            const FitStateArrays *S = nullptr, const int32_t *list = nullptr,
+                            const unsigned long long *nctr = nullptr, long bound = 0);
 // waves of k_fit_lanes resident at once on `device` (occupancy x CUs), 0 on error
 int fit_lanes_max_waves(int device);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,

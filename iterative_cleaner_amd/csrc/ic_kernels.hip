@@ -2308,7 +2308,7 @@ __device__ __attribute__((noinline)) LaneNext lane_transition(double *ls, long l
 }
 
 #ifndef IC_LANE_MINW
-#define IC_LANE_MINW 4   // waves per SIMD the register allocation must allow (MINPACK's logic spills to scratch)
+#define IC_LANE_MINW 3   // waves per SIMD the register allocation must allow
 #endif
 __global__ __launch_bounds__(64, IC_LANE_MINW) void k_fit_lanes(const float *__restrict__ D, const double *__restrict__ T64,
                                                   long P, int nbin, int ldD, int nsw, int dtiled, int dummy_row,
@@ -2317,7 +2317,9 @@ __global__ __launch_bounds__(64, IC_LANE_MINW) void k_fit_lanes(const float *__r
                                                   int32_t *__restrict__ info_o,
                                                   unsigned long long *__restrict__ sweeps, int phase,
                                                   uint8_t *__restrict__ late, int32_t *__restrict__ flist,
-                                                  unsigned long long *__restrict__ fctr)
+                                                  unsigned long long *__restrict__ fctr, FitStateArrays S,
+                                                  const int32_t *__restrict__ list,
+                                                  const unsigned long long *__restrict__ nctr)
 {
     __shared__ __attribute__((aligned(16))) char lbuf[2 * FIT_BUF];
     const int lane = threadIdx.x;
@@ -2332,6 +2334,10 @@ __global__ __launch_bounds__(64, IC_LANE_MINW) void k_fit_lanes(const float *__r
     int slow = 0;           // J at x came from an exact sweep: the B sweep is exact too
     bool qdone = false;     // the queue is exhausted (wave-uniform)
     unsigned long long nsweeps = 0, nslots = 0;
+    // phase 3: the queue runs over a round list (the profiles still fitting
+    // after the rounds), each taken with the state k_fit_state left in S
+    const RoundList rl(phase == 3 ? list : nullptr, nctr, P);
+    const long nq = rl.n();
     if (phase == 2) {   // resume the profiles phase 1 left in flight in these slots
         const double sk = ls[kLaneK * lst + g];
         if (sk >= 0.0) {
@@ -2363,7 +2369,7 @@ __global__ __launch_bounds__(64, IC_LANE_MINW) void k_fit_lanes(const float *__r
                 unsigned base = 0;
                 if (lane == 0) base = atomicAdd(qhead, nfree);
                 base = __builtin_amdgcn_readfirstlane(base);
-                if ((long)base + nfree >= P) qdone = true;
+                if ((long)base + nfree >= nq) qdone = true;
                 if (phase == 1 && qdone) {
                     // the queue ran out: leave every profile in flight to phase 2
                     // (saved in the slot), flagged for the second diagnostics pass
@@ -2394,7 +2400,20 @@ __global__ __launch_bounds__(64, IC_LANE_MINW) void k_fit_lanes(const float *__r
                 }
                 if (emp) {
                     const long kk = (long)base + __popcll(m & ((1ull << lane) - 1ull));
-                    if (kk < P) {
+                    if (kk < nq && phase == 3) {   // resume a profile the rounds left
+                        k = (int)rl.at(kk);
+                        st = S.mode[k];
+                        xa = S.xa[k];
+                        xb = S.x[k];
+                        ajb = S.aj[k];
+                        slow = S.slow[k];
+                        const double *f17[17] = {S.x, S.fnorm, S.par, S.delta, S.diag, S.xnorm, S.acnorm, S.J0, S.f0,
+                                                 S.aj, S.r, S.Jn0, S.qtf, S.gnorm, S.x2, S.pnorm, S.wa1};
+#pragma unroll
+                        for (int f = 0; f < 17; ++f) ls[f * lst + g] = f17[f][k];
+                        ls[17 * lst + g] = (double)S.iter[k];
+                        ls[18 * lst + g] = (double)S.nfev[k];
+                    } else if (kk < nq) {
                         k = (int)kk;
                         st = ST_A0;
                         xa = 1.0;
@@ -5095,16 +5114,21 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
 hipError_t launch_fit_lanes(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                             int dtiled, int dummy_row, int waves, double *ls, long lst, const double *U,
                             unsigned *qhead, double *amp, int32_t *info, unsigned long long *sweeps, int phase,
-                            uint8_t *late, int32_t *flist, unsigned long long *fctr)
+                            uint8_t *late, int32_t *flist, unsigned long long *fctr, const FitStateArrays *S,
+                            const int32_t *list, const unsigned long long *nctr, long bound)
 {
-    if (phase < 0 || phase > 2 || (phase == 1 && (!late || !flist || !fctr))) return hipErrorInvalidValue;
+    if (phase < 0 || phase > 3 || (phase == 1 && (!late || !flist || !fctr)) ||
+        (phase == 3 && (!S || !list || !nctr)))
+        return hipErrorInvalidValue;
+    const FitStateArrays S0{};
+    const long nprof = phase == 3 ? std::min(bound, P) : P;
     if ((long)waves * 64 > lst) return hipErrorInvalidValue;
     if (P <= 0) return hipSuccess;
     const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
     if (ldD % 4 != 0 || ldD < nsw || (dtiled && ldD % 32 != 0) || waves < 1) return hipErrorInvalidValue;
-    const long g = std::min<long>(cdiv(P, 64), waves);
+    const long g = std::min<long>(cdiv(nprof, 64), waves);
     IC_GGL(k_fit_lanes, dim3((unsigned)g), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled, dummy_row, ls,
-           lst, (const double *)U, qhead, amp, info, sweeps, phase, late, flist, fctr);
+           lst, (const double *)U, qhead, amp, info, sweeps, phase, late, flist, fctr, S ? *S : S0, list, nctr);
     return hipGetLastError();
 }
 

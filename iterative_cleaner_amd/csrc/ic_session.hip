@@ -132,6 +132,7 @@ struct Session {
     int plan_ub = 0;            // max(leaves, ops) of the pairwise plan (k_tnorm scratch)
     LineStatsArgs ls_knobs;     // row-median form (IC_OPT_ROWSTAT_*)
     long tail_threshold = kTailProfiles;   // IC_OPT_FIT_TAIL
+    long late_lanes = 0;                   // IC_OPT_FIT_LATE_LANES
     bool diag_chain = true;     // IC_OPT_DIAG_CHAIN: k_diag_cl at nbin 1024/2048/4096
     int fit_schedule = IC_FIT_ROUNDS;   // IC_OPT_FIT_SCHEDULE
     int lane_waves = 0;         // IC_OPT_FIT_LANE_WAVES (0: every wave the device holds at once)
@@ -744,6 +745,21 @@ int run_fit(Session *s, const DiagArgs *fork)
     int flagged = -1;   // the fork round, once its survivors are flagged and pass A not yet queued
     for (int r = 0;; ++r) {
         if (r >= kMaxRounds) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", r);
+        if (r >= 1 && s->late_lanes > 0 && s->lanes && bound <= s->late_lanes && bound > s->tail_threshold) {
+            // the late rounds as one persistent launch: k_fit_lanes takes the
+            // round list with the state k_fit_state left (phase 3)
+            if (flagged >= 0) {
+                if (int rc = fork_diag(s, *fork, flagged)) return rc;
+                flagged = -1;
+            }
+            const int waves = s->lane_waves > 0 ? std::min(s->lane_waves, s->lane_waves_max) : s->lane_waves_max;
+            LAUNCH(s, K_FIT_LANES, launch_fit_lanes(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, (int)s->Ppad,
+                                                    waves, s->lanes, (long)s->lane_waves_max * 64, s->fs.U,
+                                                    lane_queue(s), s->amp, s->info, lane_counter(s), 3, nullptr,
+                                                    nullptr, nullptr, &s->fs, cur, cin, bound));
+            tail = true;
+            break;
+        }
         if (bound <= s->tail_threshold) {
             if (flagged >= 0) {
                 if (int rc = fork_diag(s, *fork, flagged)) return rc;
@@ -1552,7 +1568,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         CK(spin_sync(s));
         s->stats.window_moves = *moves;
         s->stats.fit_tail_sweeps += (int64_t)tsw[0];
-        s->stats.fit_profile_sweeps += (int64_t)tsw[1];   // k_fit_lanes' sweeps (0 under rounds)
+        s->stats.fit_lane_sweeps += (int64_t)tsw[1];
         s->stats.fit_lane_slots += (int64_t)tsw[2];
     }
     // timing events are read when asked for (ic_get_kernel_times), not here
@@ -1749,6 +1765,12 @@ int ic_set_option(void *session, int option, int64_t v)
         if (v < 0 || v > 1 << 20) return fail(IC_EINVAL, "IC_OPT_FIT_LANE_WAVES=%lld outside 0..2^20", (long long)v);
         s->lane_waves = (int)v;
         return IC_OK;
+    case IC_OPT_FIT_LATE_LANES:
+        if (v < 0) return fail(IC_EINVAL, "IC_OPT_FIT_LATE_LANES=%lld < 0", (long long)v);
+        if (v > 0 && !(exact_shift && s->lanes))
+            return fail(IC_EINVAL, "IC_OPT_FIT_LATE_LANES needs the exact fit with integer dedispersion");
+        s->late_lanes = (long)v;
+        return IC_OK;
     default:
         return fail(IC_EINVAL, "unknown option %d", option);
     }
@@ -1770,6 +1792,7 @@ int ic_get_option(void *session, int option, int64_t *out)
     case IC_OPT_SYNC_TIMEOUT_MS: *out = (int64_t)(s->sync_timeout_s * 1000.0 + 0.5); return IC_OK;
     case IC_OPT_FIT_SCHEDULE: *out = s->fit_schedule; return IC_OK;
     case IC_OPT_FIT_LANE_WAVES: *out = s->lane_waves; return IC_OK;
+    case IC_OPT_FIT_LATE_LANES: *out = s->late_lanes; return IC_OK;
     default: return fail(IC_EINVAL, "unknown option %d", option);
     }
 }
