@@ -147,9 +147,12 @@ hipError_t launch_chan_partials(hipStream_t st, int mode, const float *raw, cons
 // condition for launch_chan_delta.  Iteration >= 2 (Wn = this iteration's weights, Wo = the
 // previous one's): part, part2 (carried levels) and wpart moved from Wo to Wn
 // through the changed channels only; inexact columns summed again in full.
+// rawF (FFT dedispersion): part2's terms are f32(rawF - base) instead of
+// f32(raw - base) (part's stay raw's).
 hipError_t launch_chan_delta(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
                              const float *Wn, const float *Wo, int nsub, int nchan, int nbin, double *part,
-                             double *part2, double *wpart, const uint8_t *exA, const uint8_t *exF);
+                             double *part2, double *wpart, const uint8_t *exA, const uint8_t *exF,
+                             const float *rawF = nullptr);
 // flags != nullptr: flags[s] = window of subint s moved (win updated in place)
 // element (s, leaf, i) of `part` is part[s*ss + leaf*sl + i]; the leaves are
 // combined with `plan` (single device: the nsb super-blocks; sharded: the
@@ -302,9 +305,11 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
 // out[p] = rot(f32(in[p] - base[p])) by the channel's phasors, sign +1 =
 // dedisperse, -1 = dededisperse.  Rows p = s*nchan + c of ld_in / ldo floats;
 // out2 (optional) receives a second copy (row strides multiples of 4:
-// 16-byte row accesses); flags: only subints with
-// flags[s] != 0.  in may equal out (each row is read whole before it is
-// written).  nbin a power of two, 64 .. 4096.
+// 16-byte row accesses); in and out2 may be fit cubes in the tiled layout
+// (in_tiled / out2_tiled: d_ofs, strides multiples of 32); flags: only subints
+// with flags[s] != 0; late: only profiles with (late[p] != 0) == late_sel (the
+// diagnostics fork's two passes).  in may equal out (each row is read whole
+// before it is written).  nbin a power of two, 64 .. 4096.
 struct RotateArgs {
     const float *in;
     long ld_in;
@@ -326,6 +331,9 @@ struct RotateArgs {
     int pr_on;
     double pr_factor;
     int pr_start, pr_end;
+    int in_tiled, out2_tiled;
+    const uint8_t *late;
+    int late_sel;
 };
 hipError_t launch_rotate(hipStream_t st, const RotateArgs &a);
 bool rotate_supported(int nbin);

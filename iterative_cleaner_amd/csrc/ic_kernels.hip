@@ -256,9 +256,13 @@ __global__ __launch_bounds__(256) void k_chan_partials(
 // super-block has no changed channel does nothing.
 // BPT bins per thread (bin i0 + 256 b, b < BPT): the change list and the
 // block's fixed costs serve BPT times the columns, and BPT times the loads are
-// in flight per batch of channels
-template <int BPT>
-__global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ raw, const int32_t *__restrict__ shift,
+// in flight per batch of channels.
+// SPLIT (FFT dedispersion): part's terms come from raw (the rotated raw cube)
+// and part2's from rawF (the rotated baselined rows Tc, base = 0); otherwise
+// both from raw, part2's as f32(raw - base).
+template <int BPT, bool SPLIT>
+__global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ raw, const float *__restrict__ rawF,
+                                                    const int32_t *__restrict__ shift,
                                                     const float *__restrict__ base, const float *__restrict__ Wn,
                                                     const float *__restrict__ Wo, int nchan, int nbin, int nsb,
                                                     double *__restrict__ part, double *__restrict__ part2,
@@ -317,12 +321,12 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                     if (j >= nbin) j -= nbin;
                     xv[q] = raw[(krow + c + q) * nbin + j];
                     wv[q] = Wn[krow + c + q];
-                    bv[q] = base[krow + c + q];
+                    bv[q] = SPLIT ? rawF[(krow + c + q) * nbin + j] - base[krow + c + q] : base[krow + c + q];
                 }
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
                     const double w = (double)wv[q];
-                    const float d = xv[q] - bv[q];
+                    const float d = SPLIT ? bv[q] : xv[q] - bv[q];
                     acc = acc + w * (double)xv[q];
                     acc2 = acc2 + w * (double)d;
                 }
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                 if (j >= nbin) j -= nbin;
                 const float x = raw[(krow + c) * nbin + j];
                 const double w = (double)Wn[krow + c];
-                const float d = x - base[krow + c];
+                const float d = (SPLIT ? rawF[(krow + c) * nbin + j] : x) - base[krow + c];
                 acc = acc + w * (double)x;
                 acc2 = acc2 + w * (double)d;
             }
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
             dA[b] = dF[b] = 0.0;
         }
         for (int q0 = 0; q0 < n; q0 += B) {
-            float xv[B][BPT], bv[B], wnv[B], wov[B];
+            float xv[B][BPT], fv[SPLIT ? B : 1][BPT], bv[B], wnv[B], wov[B];
 #pragma unroll
             for (int q = 0; q < B; ++q) {
                 const int c = chg[min(q0 + q, n - 1)];
@@ -365,6 +369,7 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                     int j = i + sc;
                     if (j >= nbin) j -= nbin;
                     xv[q][b] = row[j];
+                    if (SPLIT) fv[SPLIT ? q : 0][b] = rawF[(krow + c) * nbin + j];
                 }
             }
 #pragma unroll
@@ -373,7 +378,7 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                     const double wn = (double)wnv[q], wo = (double)wov[q];
 #pragma unroll
                     for (int b = 0; b < BPT; ++b) {
-                        const float d = xv[q][b] - bv[q];
+                        const float d = (SPLIT ? fv[SPLIT ? q : 0][b] : xv[q][b]) - bv[q];
                         dA[b] = dA[b] + (wn * (double)xv[q][b] - wo * (double)xv[q][b]);
                         dF[b] = dF[b] + (wn * (double)d - wo * (double)d);
                     }
@@ -413,7 +418,7 @@ __global__ __launch_bounds__(256) void k_chan_delta(const float *__restrict__ ra
                 if (j >= nbin) j -= nbin;
                 const float x = raw[(krow + c) * nbin + j];
                 const double w = (double)Wn[krow + c];
-                const float d = x - base[krow + c];
+                const float d = (SPLIT ? rawF[(krow + c) * nbin + j] : x) - base[krow + c];
                 tA[threadIdx.x] = w * (double)x;
                 tF[threadIdx.x] = w * (double)d;
             }
@@ -4070,12 +4075,18 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_r
     // per profile, not one per row (or per flag / fit lookup)
     auto load_rows = [&](size_t it, float4 (&xr)[NJ]) {
         const unsigned c = (unsigned)(it / nsub), s = (unsigned)(it % nsub);
-        const float *x = a.in + ((size_t)s * nchan + c) * (size_t)a.ld_in;
+        const size_t k = (size_t)s * nchan + c;
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
             const int j2 = t + u * TB;
-            if ((M / 2) % TB == 0 || j2 < M / 2) xr[u] = *(const float4 *)(x + 4 * j2);
+            if ((M / 2) % TB == 0 || j2 < M / 2)
+                xr[u] = *(const float4 *)(a.in + d_ofs(k, 4 * j2, (int)a.ld_in, a.in_tiled));
         }
+    };
+    // the profile is left out (uniform over the block): its subint's flag is 0,
+    // or its late flag is not the one selected
+    auto skip = [&](size_t p, unsigned s) {
+        return (a.flags && a.flags[s] == 0) || (a.late && ((a.late[p] != 0) != (a.late_sel != 0)));
     };
     float4 xnext[NJ];
     if (IC_ROT_NEXTPF && blockIdx.x < P) load_rows(blockIdx.x, xnext);
@@ -4087,10 +4098,11 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_r
 #pragma unroll
             for (int u = 0; u < NJ; ++u) xin[u] = xnext[u];
             if (item + gridDim.x < P) load_rows(item + gridDim.x, xnext);   // lands during this profile
+            if (skip(p, s)) continue;
         } else {
+            if (skip(p, s)) continue;
             load_rows(item, xin);
         }
-        if (a.flags && a.flags[s] == 0) continue;            // uniform over the block
         if (a.amp) {
             // the residual of the exact fit (k_residual's arithmetic), formed on the fly
             const int st = a.info[p];
@@ -4178,7 +4190,6 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_r
         gsync<TB / 64>();
         rot_fft<N>(v, twr, t);
         float *o = a.out + p * (size_t)a.ldo;
-        float *o2 = a.out2 ? a.out2 + p * (size_t)a.ldo2 : nullptr;
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
             const int j2 = t + u * TB;
@@ -4187,7 +4198,7 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_r
             const float4 y = make_float4((float)(r0.x * inv), (float)((-r0.y) * inv), (float)(r1.x * inv),
                                          (float)((-r1.y) * inv));
             *(float4 *)(o + 4 * j2) = y;
-            if (o2) *(float4 *)(o2 + 4 * j2) = y;
+            if (a.out2) *(float4 *)(a.out2 + d_ofs(p, 4 * j2, (int)a.ldo2, a.out2_tiled)) = y;
         }
         gsync<TB / 64>();   // v is reused by the block's next profile
     }
@@ -4951,7 +4962,8 @@ size_t window_lds_bytes(int nbin) { return (size_t)nbin * 8 + kWindowThreads * (
 
 hipError_t launch_chan_delta(hipStream_t st, const float *raw, const int32_t *shift, const float *base,
                              const float *Wn, const float *Wo, int nsub, int nchan, int nbin, double *part,
-                             double *part2, double *wpart, const uint8_t *exA, const uint8_t *exF)
+                             double *part2, double *wpart, const uint8_t *exA, const uint8_t *exF,
+                             const float *rawF)
 {
     const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
     if (!exA || !exF) return hipErrorInvalidValue;
@@ -4960,12 +4972,18 @@ hipError_t launch_chan_delta(hipStream_t st, const float *raw, const int32_t *sh
 #define IC_CD_BPT 0   // bins per thread of k_chan_delta; 0: by nbin
 #endif
     const int bpt = IC_CD_BPT > 0 ? IC_CD_BPT : (nbin >= 1024 ? 4 : (nbin >= 512 ? 2 : 1));
-#define IC_CD(BP)                                                                                                 \
-    IC_GGL(k_chan_delta<BP>, dim3(cdiv(nbin, 256 * BP), nsb, nsub), dim3(256), 0, st, raw, shift, base, Wn, Wo, \
-           nchan, nbin, nsb, part, part2, wpart, exA, exF)
-    if (bpt == 4) IC_CD(4);
-    else if (bpt == 2) IC_CD(2);
-    else IC_CD(1);
+#define IC_CD(BP, SP)                                                                                   \
+    IC_GGL((k_chan_delta<BP, SP>), dim3(cdiv(nbin, 256 * BP), nsb, nsub), dim3(256), 0, st, raw, rawF, shift, \
+           base, Wn, Wo, nchan, nbin, nsb, part, part2, wpart, exA, exF)
+    if (rawF) {
+        if (bpt == 4) IC_CD(4, true);
+        else if (bpt == 2) IC_CD(2, true);
+        else IC_CD(1, true);
+    } else {
+        if (bpt == 4) IC_CD(4, false);
+        else if (bpt == 2) IC_CD(2, false);
+        else IC_CD(1, false);
+    }
 #undef IC_CD
     return hipGetLastError();
 }
@@ -5204,11 +5222,13 @@ static bool uses_cl(const DiagArgs &a)
            (a.nbin == 1024 || a.nbin == 2048 || a.nbin == 4096) && a.chain;
 }
 
-// profile lists / skips: k_diag_cl, and k_diag_p2 in the exact mode
+// profile lists / skips: k_diag_cl, and k_diag_p2 in the exact mode and on
+// given rows (the FFT mode's rotated residuals)
 bool diag_list_supported(const DiagArgs &a)
 {
     const int n = a.nbin;
-    return uses_cl(a) || (a.mode == DIAG_EXACT && n >= 64 && n <= 4096 && (n & (n - 1)) == 0);
+    return uses_cl(a) ||
+           ((a.mode == DIAG_EXACT || a.mode == DIAG_STATS) && n >= 64 && n <= 4096 && (n & (n - 1)) == 0);
 }
 
 hipError_t launch_diag(hipStream_t st, const DiagArgs &a)
@@ -5349,7 +5369,7 @@ hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
     if (P == 0) return hipSuccess;
     if (!rotate_supported(a.nbin) || !a.in || !a.out || !a.ph || !a.tw || a.ld_in < a.nbin || a.ldo < a.nbin ||
         (a.ld_in & 3) || (a.ldo & 3) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 3))) ||
-        (a.amp && (!a.T64 || !a.info)))
+        (a.amp && (!a.T64 || !a.info)) || (a.in_tiled && (a.ld_in & 31)) || (a.out2_tiled && (a.ldo2 & 31)))
         return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<size_t>(P, 16384);
 #define IC_ROT(NN)                                                                                 \

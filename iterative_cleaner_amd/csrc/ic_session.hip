@@ -151,6 +151,7 @@ struct Session {
     // clean): no fork 28.70-28.77, fork 3 / delay 1 27.99-28.06, 3 / 0
     // 28.53-28.61, 3 / 2 28.41-28.46, 4 / 0 28.01-28.19, 4 / 1 28.45-28.52
     int diag_fork = 3;
+    int pr_lo = 0, pr_hi = 0;   // this run's clamped pulse region (the FFT mode's forked residual rotation)
     // incremental template stage (integer dedispersion, iteration >= 2):
     // column exactness flags [nsub][nsb][nbin] of part (exA, set once per run
     // by prepare) and part2 (exF, set by every full fscrunch pass);
@@ -566,6 +567,7 @@ RotateArgs residual_rotate_args(Session *s, int pr_start, int pr_end)
     a.pr_factor = s->p.pr_factor;
     a.pr_start = pr_start;
     a.pr_end = pr_end;
+    a.in_tiled = s->dtiled;
     return a;
 }
 
@@ -593,13 +595,14 @@ int prepare(Session *s)
         LAUNCH(s, K_ROTATE, launch_rotate(s->stream, rotate_args(s, s->raw, nullptr, +1, nullptr, s->dr, nbin)));
         LAUNCH(s, K_CHAN_PARTIALS,
                launch_chan_partials(s->stream, 0, s->dr, s->w0, s->zshift, nullptr, nullptr, nsub, nchan, nbin,
-                                    s->part, nullptr, nullptr));
+                                    s->part, nullptr, nullptr, nullptr, 0, 0, s->exA, nullptr));
         if (int rc = window_stage(s, nullptr)) return rc;
         LAUNCH(s, K_BASE,
                launch_base(s->stream, s->dr, s->zshift, s->win, nullptr, nsub, nchan, nbin, s->width, s->base0));
         RotateArgs ra = rotate_args(s, s->raw, s->base0, +1, nullptr, s->Tc, nbin);
         ra.out2 = s->D;
         ra.ldo2 = s->ldD;
+        ra.out2_tiled = s->dtiled;
         LAUNCH(s, K_ROTATE, launch_rotate(s->stream, ra));
         CK(hipMemcpyAsync(s->base, s->base0, sizeof(float) * s->P, hipMemcpyDeviceToDevice, s->stream));
         CK(hipMemsetAsync(s->wflag + nsub, 0, sizeof(int32_t), s->stream));
@@ -632,11 +635,22 @@ int iteration_template(Session *s, int iter)
     if (s->fftded) {
         // FFT dedispersion: the window totals and levels read rot(raw); the rows
         // rot(f32(raw - base)) of subints whose window moved are re-rotated, and
-        // the fscrunch partials are taken over those rows (no shift, no level)
+        // the fscrunch partials are taken over those rows (no shift, no level).
+        // Incremental (IC_OPT_TEMPLATE_INCR): both sums move through the changed
+        // channels (k_chan_delta, part from rot(raw), part2 from the rows), the
+        // subints whose window moved are summed again after their re-rotation.
+        const bool incr = iter > 1 && s->incr;
         if (iter > 1) {
-            LAUNCH(s, K_CHAN_PARTIALS,
-                   launch_chan_partials(s->stream, 0, s->dr, s->W, s->zshift, nullptr, nullptr, nsub, nchan, nbin,
-                                        s->part, nullptr, nullptr));
+            if (incr) {
+                const float *Wo = s->hist + (size_t)(iter - 2) * s->P;
+                LAUNCH(s, K_CHAN_PARTIALS,
+                       launch_chan_delta(s->stream, s->dr, s->zshift, s->zbase, s->W, Wo, nsub, nchan, nbin, s->part,
+                                         s->part2, s->wpart, s->exA, s->exF, s->Tc));
+            } else {
+                LAUNCH(s, K_CHAN_PARTIALS,
+                       launch_chan_partials(s->stream, 0, s->dr, s->W, s->zshift, nullptr, nullptr, nsub, nchan, nbin,
+                                            s->part, nullptr, nullptr, nullptr, 0, 0, s->exA, nullptr));
+            }
             if (int rc = window_stage(s, s->wflag)) return rc;
             LAUNCH(s, K_BASE,
                    launch_base(s->stream, s->dr, s->zshift, s->win, s->wflag, nsub, nchan, nbin, s->width, s->base));
@@ -644,8 +658,8 @@ int iteration_template(Session *s, int iter)
                    launch_rotate(s->stream, rotate_args(s, s->raw, s->base, +1, s->wflag, s->Tc, nbin)));
         }
         LAUNCH(s, K_CHAN_PARTIALS,
-               launch_chan_partials(s->stream, 1, s->Tc, s->W, s->zshift, s->zbase, nullptr, nsub, nchan, nbin,
-                                    nullptr, s->part2, s->wpart));
+               launch_chan_partials(s->stream, 1, s->Tc, s->W, s->zshift, s->zbase, incr ? s->wflag : nullptr, nsub,
+                                    nchan, nbin, nullptr, s->part2, s->wpart, nullptr, 0, 0, nullptr, s->exF));
         return scrunch_stage(s);
     }
     if (iter == 1) {   // W == w0: the carried baseline is exactly prepare()'s; also writes D (exact fit)
@@ -860,6 +874,12 @@ int fork_diag(Session *s, const DiagArgs &da, int r)
 {
     CK(hipEventRecord(s->fork_ev, s->stream));
     CK(hipStreamWaitEvent(s->dstream, s->fork_ev, 0));
+    if (s->fftded) {   // their residual rows, rotated back (run_impl: the rest after the fit)
+        RotateArgs ra = residual_rotate_args(s, s->pr_lo, s->pr_hi);
+        ra.late = s->late;
+        ra.late_sel = 0;
+        LAUNCH_ON(s, K_ROTATE, s->dstream, launch_rotate(s->dstream, ra));
+    }
     DiagArgs a = da;
     a.skip = s->late;
     LAUNCH_ON(s, K_DIAG, s->dstream, launch_diag(s->dstream, a));
@@ -975,7 +995,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         return bail(fail(IC_EHIP, "hipStreamCreate failed"));
     // the diagnostics fork's stream exists for every session it can serve
     // (IC_OPT_DIAG_FORK may switch it on or off before any run)
-    if (p.fit_mode == IC_FIT_EXACT && p.dedisp_mode == IC_DEDISP_SHIFT) {
+    if (p.fit_mode == IC_FIT_EXACT) {
         // (a higher priority for the fit's stream measured no different)
         if (hipStreamCreateWithFlags(&s->dstream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming) != hipSuccess ||
@@ -1000,9 +1020,10 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     }
     AL(s->TT, 1);
     s->fftded = p.dedisp_mode == IC_DEDISP_FFT;
-    // the fit cube written by k_chan_partials mode 3 is tiled (k_rotate's, in
-    // the FFT mode, is row-major); IC_OPT_FIT_TILED = 0: row-major
-    s->dtiled = s->fftded ? 0 : 1;
+    // the fit cube (written by k_chan_partials mode 3, or by k_rotate in the FFT
+    // mode) is tiled; IC_OPT_FIT_TILED = 0: row-major.  The closed-form fit of
+    // the FFT mode reads its rotated fit cube row by row (k_diag DIAG_FIT).
+    s->dtiled = (s->fftded && !exact) ? 0 : 1;
     if (s->fftded) {
         AL(s->dr, N);
         AL(s->Tc, N);
@@ -1025,12 +1046,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->win, (size_t)nsub);
     AL(s->wflag, (size_t)nsub + 1);   // + window-moves counter
     AL(s->part, (size_t)nsub * s->nsb * nbin);
-    if (!s->fftded) {   // the incremental template stage's column flags (IC_OPT_TEMPLATE_INCR)
-        AL(s->exA, (size_t)nsub * s->nsb * nbin);
-        AL(s->exF, (size_t)nsub * s->nsb * nbin);
-    } else {
-        s->incr = false;
-    }
+    // the incremental template stage's column flags (IC_OPT_TEMPLATE_INCR)
+    AL(s->exA, (size_t)nsub * s->nsb * nbin);
+    AL(s->exF, (size_t)nsub * s->nsb * nbin);
     AL(s->part2, (size_t)nsub * s->nsb * nbin);
     AL(s->wpart, (size_t)nsub * s->nsb);
     AL(s->F, (size_t)nsub * nbin);
@@ -1054,7 +1072,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->plan, 1);
     if (exact) AL(s->lists, 3 * P);   // two ping-pong round lists + the fork round's survivors
     AL(s->rcount, (size_t)kRoundWords + 8);   // + the lanes' queue, the tail's and the lanes' sweep counters
-    if (exact && !s->fftded) AL(s->late, P);
+    if (exact) AL(s->late, P);
     if (sharded) {
         const char *cerr = nullptr;
         s->comm = make_comm(&cerr);
@@ -1494,12 +1512,23 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         ++n_iter;
         if (int rc = iteration_template(s, n_iter)) return rc;
         DiagArgs da = diag_args(s, pr_start, pr_end);
+        // the statistics pass: FFT dedispersion measures the residual rows
+        // rotated back to the dispersed frame (R), written by k_rotate
+        DiagArgs ds = da;
+        if (s->fftded) {
+            ds.mode = DIAG_STATS;
+            ds.D = s->R;
+            ds.ldD = nbin;
+            ds.dtiled = 0;
+        }
+        s->pr_lo = pr_start;
+        s->pr_hi = pr_end;
         if (p.fit_mode == IC_FIT_EXACT) {
-            const bool fork = s->diag_fork > 0 && s->dstream && s->late && diag_list_supported(da);
+            const bool fork = s->diag_fork > 0 && s->dstream && s->late && diag_list_supported(ds);
             if (s->fit_schedule == IC_FIT_LANES) {
-                if (int rc = run_fit_lanes(s, fork ? &da : nullptr)) return rc;
+                if (int rc = run_fit_lanes(s, fork ? &ds : nullptr)) return rc;
             } else {
-                if (int rc = run_fit(s, fork ? &da : nullptr)) return rc;
+                if (int rc = run_fit(s, fork ? &ds : nullptr)) return rc;
             }
         } else {
             LAUNCH(s, K_TNORM, launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
@@ -1512,11 +1541,15 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             }
             // residual in the dedispersed frame, dededispersed by the inverse
             // rotation (ic.py:101-104), then comprehensive_stats of those rows
-            LAUNCH(s, K_ROTATE, launch_rotate(s->stream, residual_rotate_args(s, pr_start, pr_end)));
-            da.mode = DIAG_STATS;
-            da.D = s->R;
-            da.ldD = nbin;
-            da.dtiled = 0;
+            // (after a fork: the profiles still fitting at it, the others were
+            // rotated on dstream)
+            RotateArgs ra = residual_rotate_args(s, pr_start, pr_end);
+            if (s->fork_round >= 0) {
+                ra.late = s->late;
+                ra.late_sel = 1;
+            }
+            LAUNCH(s, K_ROTATE, launch_rotate(s->stream, ra));
+            da = ds;
         }
         if (s->fork_round >= 0) {
             // pass B: the profiles still fitting at the fork, then join pass A
@@ -1720,8 +1753,7 @@ int ic_set_option(void *session, int option, int64_t v)
         return IC_OK;
     case IC_OPT_DIAG_FORK:
         if (v < 0 || v > 64) return fail(IC_EINVAL, "IC_OPT_DIAG_FORK=%lld outside 0..64", (long long)v);
-        if (v > 0 && !exact_shift)
-            return fail(IC_EINVAL, "IC_OPT_DIAG_FORK needs the exact fit with integer dedispersion");
+        if (v > 0 && s->p.fit_mode != IC_FIT_EXACT) return fail(IC_EINVAL, "IC_OPT_DIAG_FORK needs the exact fit");
         s->diag_fork = (int)v;
         return IC_OK;
     case IC_OPT_FORK_DELAY:
@@ -1730,12 +1762,12 @@ int ic_set_option(void *session, int option, int64_t v)
         return IC_OK;
     case IC_OPT_TEMPLATE_INCR:
         if (v != 0 && v != 1) return fail(IC_EINVAL, "IC_OPT_TEMPLATE_INCR=%lld (0 or 1)", (long long)v);
-        if (v && s->fftded) return fail(IC_EINVAL, "IC_OPT_TEMPLATE_INCR needs integer dedispersion");
         s->incr = v != 0;
         return IC_OK;
     case IC_OPT_FIT_TILED:
         if (v != 0 && v != 1) return fail(IC_EINVAL, "IC_OPT_FIT_TILED=%lld (0 or 1)", (long long)v);
-        if (v && s->fftded) return fail(IC_EINVAL, "IC_OPT_FIT_TILED needs integer dedispersion");
+        if (v && s->fftded && s->p.fit_mode != IC_FIT_EXACT)
+            return fail(IC_EINVAL, "IC_OPT_FIT_TILED: the closed-form fit of the FFT mode reads a row-major cube");
         s->dtiled = (int)v;
         return IC_OK;
     case IC_OPT_ROWSTAT_WAVES:

@@ -106,6 +106,60 @@ def test_fft_loop_matches_c_oracle(case, fit_tail, oracle_lib):
     assert _same(R, ref["residual"])
 
 
+SCHEDULES = [
+    # (diag_fork, template_incr, fit_tiled, fit_tail): the round-3 schedule on
+    # the FFT mode against its plain form
+    (0, 0, 0, None),
+    (1, 1, 1, 0),
+    (3, 1, 0, 512),
+    (5, 0, 1, None),
+]
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[4], CASES[5], CASES[7]],
+                         ids=lambda c: "%dx%dx%d" % c[:3])
+def test_fft_schedules_are_bit_identical(case, oracle_lib):
+    """The diagnostics fork (the residual rotation of the fitted profiles on the
+    second stream), the incremental template stage (k_chan_delta on rot(raw)
+    and the rotated rows) and the tiled fit cube in the FFT mode: every output
+    the same bits under every setting, and the default setting equal to the
+    C oracle."""
+    from iterative_cleaner_amd import _native, synth
+    nsub, nchan, nbin, seed, rfi, extra = case
+    data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
+    delay = synth.fractional_delays(shift, nbin)
+    raw = np.ascontiguousarray(data[:, 0])
+    args = dict(max_iter=5, chanthresh=5.0, subintthresh=5.0, pulse_region=[0, 0, 1])
+    args.update(extra)
+
+    def run(opts, tail):
+        with _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"], args["subintthresh"],
+                                args["pulse_region"], device=0, delay=delay, options=opts) as s:
+            if tail is not None:
+                s.set_fit_tail(tail)
+            s.upload(raw, w0, np.zeros(nchan, np.int32))
+            out = s.run()
+            out["T"] = s.template()
+            out["amp"], out["info"] = s.fit()
+            out["diag"] = s.diagnostics()
+            out["R"] = s.residual()
+        return out
+
+    base = run({}, None)
+    ref = oracle_lib.clean_loop(raw, w0, shift, args["chanthresh"], args["subintthresh"], args["max_iter"],
+                                _pr(args, nbin), want_residual=True, want_details=True, delay=delay)
+    assert base["loops"] == ref["loops"] and bits_equal(base["weights"], ref["weights"])
+    assert bits_equal(base["amp"], ref["amp"]) and _same(base["R"], ref["residual"])
+    for fork, incr, tiled, tail in SCHEDULES:
+        got = run({"diag_fork": fork, "template_incr": incr, "fit_tiled": tiled}, tail)
+        assert got["loops"] == base["loops"] and np.array_equal(got["changed"], base["changed"])
+        for key in ("weights", "test", "T", "amp", "info"):
+            assert bits_equal(got[key], base[key]), (fork, incr, tiled, key)
+        for x0, x1 in zip(base["diag"], got["diag"]):
+            assert bits_equal(x1, x0), (fork, incr, tiled)
+        assert _same(got["R"], base["R"])
+
+
 @pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[4], CASES[6]], ids=lambda c: "%dx%dx%d" % c[:3])
 def test_fft_closed_form_loop_matches_c_oracle(case, oracle_lib):
     """fit_mode 1 (closed-form amplitude) with fractional dedispersion: the
