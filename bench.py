@@ -142,7 +142,7 @@ def s8d_bytes(name, nsub, nchan, nbin, launches, iterations, steps):
     return per_iter[name] * iterations * steps
 
 
-def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True):
+def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True, fft=False):
     """Bytes a kernel's launches actually move, summed over the timed region
     (kernel table) - the implementation's own traffic model, not
     §8(d)'s.  `run`: one clean's counts, {"n_iter", "changed" (per iteration),
@@ -159,6 +159,10 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True)
                        of the profiles whose weight changed in the iteration
                        before, and the flagged pass the subints whose baseline
                        window moved; plus the super-block partials written;
+                       FFT dedispersion (fft): the passes read the rotated cubes
+                       (rot(raw) for the window totals, the rotated rows for the
+                       fscrunch sums) and write no fit cube (k_rotate does); the
+                       delta reads a changed channel's row from both;
       k_base           the window samples of every profile (prepare) and of
                        the subints whose window moved (later iterations);
       k_diag           one full pass per iteration whatever the launches (the
@@ -178,7 +182,7 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True)
         return 2 * 204 * run["fit_profile_sweeps"] * steps
     if name == "k_chan_partials":
         changed = sum(int(c) for c in run["changed"][:max(0, n_iter - 1)])
-        per_run = (4 * N + (8 * N if exact else 4 * N) + 4 * nbin * changed
+        per_run = (4 * N + (8 * N if exact and not fft else 4 * N) + (8 if fft else 4) * nbin * changed
                    + 4 * nchan * nbin * run["window_moves"] + 16 * nsub * nsb * nbin * n_iter)
         return per_run * steps
     if name == "k_base":
@@ -617,7 +621,8 @@ def main():
         avg_s = dk["ms"] / 1000.0 / max(1, dk["launches"])
         # implementation bytes (every sweep the kernel makes) and SURVEY §8(d) bytes
         exact_mode = fit_mode == _native.FIT_EXACT
-        total_bytes = algorithmic_bytes(dom, nsub, lnchan, nbin, dk["launches"], run_counts, a.steps, exact_mode)
+        total_bytes = algorithmic_bytes(dom, nsub, lnchan, nbin, dk["launches"], run_counts, a.steps, exact_mode,
+                                        delay is not None)
         sweep_launch = total_bytes / max(1, dk["launches"]) if total_bytes else None
         s8d_total = s8d_bytes(dom, nsub, lnchan, nbin, dk["launches"], n_iter, a.steps)
         s8d_launch = s8d_total / max(1, dk["launches"]) if s8d_total else None
@@ -627,7 +632,8 @@ def main():
         for kname, kv in ktimes.items():
             if kv["launches"] == 0:
                 continue
-            tb = algorithmic_bytes(kname, nsub, lnchan, nbin, kv["launches"], run_counts, a.steps, exact_mode)
+            tb = algorithmic_bytes(kname, nsub, lnchan, nbin, kv["launches"], run_counts, a.steps, exact_mode,
+                                   delay is not None)
             pk = {"ms_per_step": round(kv["ms"] / a.steps, 3), "launches_per_step": kv["launches"] // a.steps,
                   "sweep_gbs": round(tb / (kv["ms"] / 1000.0) / 1e9, 1) if tb else None}
             sb = s8d_bytes(kname, nsub, lnchan, nbin, kv["launches"], n_iter, a.steps)
