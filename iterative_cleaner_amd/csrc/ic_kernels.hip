@@ -3545,11 +3545,6 @@ constexpr int p2_tw_entries(int N)
 #ifndef IC_CL_PSTAGE
 #define IC_CL_PSTAGE 0
 #endif
-// closed mode: the next profile's dedispersed-order gather issued with its
-// row prefetch (1) instead of at its use (0; A/B knob)
-#ifndef IC_CL_PIPF
-#define IC_CL_PIPF 0
-#endif
 // Stage and spectrum twiddles derived from one base twiddle per butterfly /
 // lane (p2_stage DER; tw[t + L j] = tw[t] exp(-2 pi i j / 16)) instead of one
 // read each: for the multi-wave groups (N >= 2048), whose table is read
@@ -3632,16 +3627,6 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
 #pragma unroll
         for (int q = 0; q < 16; ++q) pv[q] = IC_CL_PROBE == 2 ? (float)(q + kk) : pn[8 * q];
     };
-    constexpr bool pipf = closed && IC_CL_PIPF && !IC_CL_PSTAGE;
-    float pin[pipf ? 16 : 1];
-    auto loadpi = [&](unsigned kk, int shk) {   // row kk at (jb + shk + 8q) mod N
-        if constexpr (pipf) {
-            const float *row = a.raw + (size_t)kk * N;
-            const unsigned j0 = (unsigned)(jb + shk);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) pin[q] = row[(j0 + 8u * q) & (unsigned)(N - 1)];
-        }
-    };
     unsigned slot = next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
     unsigned k = slot < nslot ? (unsigned)rl.at(slot) : 0u;
     double nx = 0.0;
@@ -3656,7 +3641,6 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
         nb = a.base[k];
         nw = a.w0[k];
         nsh = a.shift[k % nchan];
-        loadpi(k, ufirst(nsh));
     }
     for (unsigned snext; slot < nslot; slot = snext) {
         // multi-wave groups: keep the FFT's LDS addresses inside the loop (hoisted,
@@ -3696,9 +3680,6 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
                     const int j = (int)((j0 + 8u * q) & (unsigned)(N - 1));
                     pi[q] = pst[j ^ (((j >> 7) & 7) << 3)];
                 }
-            } else if constexpr (pipf) {
-#pragma unroll
-                for (int q = 0; q < 16; ++q) pi[q] = pin[q];
             } else {
                 const float *row = a.raw + (size_t)k * N;
 #pragma unroll
@@ -3753,7 +3734,6 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
             nb = a.base[kn];
             nw = a.w0[kn];
             nsh = a.shift[kn % nchan];
-            loadpi(kn, ufirst(nsh));
         }
         double mean = 0.0, sd = 0.0, fftv = 0.0, ptp = (double)1e20f;
         if (valid) {
