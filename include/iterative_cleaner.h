@@ -222,7 +222,8 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  *                          fit (one wave per profile), >= 0, 0 = never; 8192
  *   IC_OPT_DIAG_FORK       fit round after which the diagnostics of the fitted
  *                          profiles run on a second stream, 0..64, 0 = no fork;
- *                          3 (exact fit, integer dedispersion only)
+ *                          3 with integer dedispersion, 0 with the FFT rotation
+ *                          (exact fit only)
  *   IC_OPT_FORK_DELAY      rounds between that round and the forked pass, 0..8; 1
  *   IC_OPT_TEMPLATE_INCR   1 = incremental template stage (integer
  *                          dedispersion), 0 = full template passes; 1

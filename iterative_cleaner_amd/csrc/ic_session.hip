@@ -1020,6 +1020,10 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     }
     AL(s->TT, 1);
     s->fftded = p.dedisp_mode == IC_DEDISP_FFT;
+    // the FFT mode's forked pass (its residual rotations with the statistics)
+    // slows the late fit rounds more than it hides: off by default there
+    // (C2 --dedisp fft: 56.7-56.9 ms per clean forked, 55.4-55.5 unforked)
+    if (s->fftded) s->diag_fork = 0;
     // the fit cube (written by k_chan_partials mode 3, or by k_rotate in the FFT
     // mode) is tiled; IC_OPT_FIT_TILED = 0: row-major.  The closed-form fit of
     // the FFT mode reads its rotated fit cube row by row (k_diag DIAG_FIT).

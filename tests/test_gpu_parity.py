@@ -193,7 +193,8 @@ def test_loop_matches_c_oracle(case, fit_mode, oracle_lib):
     if fit_mode == "rounds":
         assert st["fit_tail_sweeps"] == 0
     elif fit_mode == "lanes":
-        assert st["fit_rounds"] == out["n_iter"] and st["fit_tail_sweeps"] == 0 and st["fit_profile_sweeps"] > 0
+        assert st["fit_rounds"] == out["n_iter"] and st["fit_tail_sweeps"] == 0
+        assert st["fit_profile_sweeps"] == 0 and st["fit_lane_sweeps"] > 0 and st["fit_lane_slots"] > 0
     else:
         assert st["fit_profile_sweeps"] == 0 and st["fit_tail_sweeps"] > 0
     assert out["loops"] == ref["loops"]

@@ -41,7 +41,7 @@ def test_option_ranges_and_modes():
             s.set_option("fit_late_lanes", 1000)
         s.set_option("diag_fork", 0)
     with _native.GpuSession(4, 64, 256, device=0, delay=np.zeros(64)) as s:
-        assert s.get_option("diag_fork") == 3 and s.get_option("template_incr") == 1
+        assert s.get_option("diag_fork") == 0 and s.get_option("template_incr") == 1
         assert s.get_option("fit_tiled") == 1
         with pytest.raises(_native.NativeError, match="FIT_SCHEDULE"):
             s.set_option("fit_schedule", _native.FIT_LANES)
