@@ -13,7 +13,7 @@ for wl in $WLS; do
         --no-cpu-baseline --no-flip-check --no-fast-summary > $f.json 2> $f.err || exit 1
     python3 -c "
 import json; d=json.loads(open('$f.json').read().splitlines()[-1]); pk=d['roofline']['per_kernel']
-print('$wl $v $r', d['ms_per_step'], {k: round(v['ms_per_step'], 4) for k, v in pk.items() if k in ('k_chan_partials', 'k_base', 'k_fit_pass')})"
+print('$wl $v $r', d['ms_per_step'], {k: round(v['ms_per_step'], 4) for k, v in pk.items() if k in ('k_chan_partials', 'k_fit_pass', 'k_fit_tail', 'k_diag')})"
   done
  done
 done
