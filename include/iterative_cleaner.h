@@ -242,6 +242,12 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  *                          from a shared queue; IC_FIT_ROUNDS
  *   IC_OPT_FIT_LANE_WAVES  waves of the IC_FIT_LANES launch, 0 = every wave the
  *                          device holds at once (more are capped to that); 0
+ *   IC_OPT_TAIL_SPLIT      with the fork: at the hand-over to k_fit_tail the
+ *                          fork round's survivors already fitted are measured
+ *                          on the second stream beside the tail, only the
+ *                          tail's profiles after it: IC_TAIL_SPLIT_OFF, _ON, or
+ *                          _AUTO (on unless nbin is 1024 with the chain-layout
+ *                          statistics kernel); IC_TAIL_SPLIT_AUTO
  *   IC_OPT_FIT_LATE_LANES  IC_FIT_ROUNDS: once at most this many profiles are
  *                          still fitting (after round 1 or later, and above
  *                          IC_OPT_FIT_TAIL), one k_fit_lanes launch resumes
@@ -265,6 +271,10 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
 #define IC_OPT_FIT_SCHEDULE 10
 #define IC_OPT_FIT_LANE_WAVES 11
 #define IC_OPT_FIT_LATE_LANES 12
+#define IC_OPT_TAIL_SPLIT 13
+#define IC_TAIL_SPLIT_OFF 0
+#define IC_TAIL_SPLIT_ON 1
+#define IC_TAIL_SPLIT_AUTO 2
 #define IC_FIT_ROUNDS 0
 #define IC_FIT_LANES 1
 int ic_set_option(void *session, int option, int64_t value);

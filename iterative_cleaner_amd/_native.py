@@ -31,7 +31,8 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
 # choose how the loop is scheduled, never its arithmetic
 OPTIONS = {"fit_tail": 1, "diag_fork": 2, "fork_delay": 3, "template_incr": 4, "fit_tiled": 5,
            "rowstat_waves": 6, "rowstat_minlen": 7, "diag_chain": 8, "sync_timeout_ms": 9,
-           "fit_schedule": 10, "fit_lane_waves": 11, "fit_late_lanes": 12}
+           "fit_schedule": 10, "fit_lane_waves": 11, "fit_late_lanes": 12,
+           "tail_split": 13}
 FIT_ROUNDS = 0   # IC_FIT_ROUNDS: sweep / state rounds over compacted lists (k_fit_pass, k_fit_state, k_fit_tail)
 FIT_LANES = 1    # IC_FIT_LANES: one persistent launch, a lane per profile at a time (k_fit_lanes)
 

@@ -210,6 +210,9 @@ constexpr int kRoundWords = 3 * kMaxRounds;
 // previous round's k_fit_state, partitioned by request: nctr -> its packed
 // counts (above), their sum <= bound (the host sizes grids from a count it
 // already knows: counts only shrink).
+// m[k] = v for the profiles of a round list (at most `bound` entries)
+hipError_t launch_mark_list(hipStream_t st, const int32_t *list, const unsigned long long *nctr, long P, long bound,
+                            uint8_t *m, uint8_t v);
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
                            const FitStateArrays &S);

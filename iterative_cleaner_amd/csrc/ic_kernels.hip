@@ -1643,6 +1643,17 @@ struct RoundList {
     }
 };
 
+// m[k] = v for every profile k of a round list (the second fork: the profiles
+// handed to k_fit_tail)
+__global__ __launch_bounds__(256) void k_mark_list(const int32_t *__restrict__ list,
+                                                   const unsigned long long *__restrict__ nctr, long P,
+                                                   uint8_t *__restrict__ m, uint8_t v)
+{
+    const RoundList rl(list, nctr, P);
+    const long slot = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot < rl.n()) m[rl.at(slot)] = v;
+}
+
 // request encoding in S.mode: ST_A0 / ST_A2 -> sweep A at S.xa; ST_B -> sweep B
 // at (S.x, S.aj); ST_DONE -> nothing.  S.slow: J at x came from an exact sweep.
 // also zeroes the round counters (nz32 words) and the late flags (P bytes, optional)
@@ -5126,6 +5137,15 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
     else
         IC_GGL(k_fit_pass<false>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw,
                            dtiled, list, nctr, S, (const double *)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_mark_list(hipStream_t st, const int32_t *list, const unsigned long long *nctr, long P, long bound,
+                            uint8_t *m, uint8_t v)
+{
+    if (!list || !nctr || !m) return hipErrorInvalidValue;
+    if (bound <= 0) return hipSuccess;
+    IC_GGL(k_mark_list, dim3(cdiv(std::min(bound, P), 256)), dim3(256), 0, st, list, nctr, P, m, v);
     return hipGetLastError();
 }
 

@@ -162,6 +162,14 @@ struct Session {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     uint8_t *late = nullptr;       // [P] 1: still fitting after round diag_fork (pass A skips them)
     int fork_round = -1;           // this iteration's fork round (-1: none)
+    // the second fork (run_fit): the tail's list, marked in tmark, measured after the fit
+    bool tail_split = false;
+    int tail_split_mode = IC_TAIL_SPLIT_AUTO;   // IC_OPT_TAIL_SPLIT
+    const int32_t *tail_list = nullptr;
+    const unsigned long long *tail_cin = nullptr;
+    long tail_bound = 0;
+    uint8_t *tmark = nullptr;
+    hipEvent_t fork2_ev = nullptr;
     int fork_delay = 1;            // rounds between the flags and pass A (IC_OPT_FORK_DELAY)
     ic_run_stats stats{};
     std::vector<int32_t> bad_fits;   // per iteration of the last run: fit statuses outside 1-4
@@ -363,6 +371,7 @@ void free_all(Session *s)
     if (s->dstream) (void)hipStreamDestroy(s->dstream);
     if (s->fork_ev) (void)hipEventDestroy(s->fork_ev);
     if (s->join_ev) (void)hipEventDestroy(s->join_ev);
+    if (s->fork2_ev) (void)hipEventDestroy(s->fork2_ev);
     void *bufs[] = {s->late, s->exA, s->exF, s->D,     s->W,   s->base, s->base0, s->F,   s->wf,
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
@@ -740,6 +749,7 @@ unsigned long long *lane_counter(Session *s) { return (unsigned long long *)(s->
 int run_fit(Session *s, const DiagArgs *fork)
 {
     s->fork_round = -1;
+    s->tail_split = false;
     const long P = (long)s->P;
     const int nbin = s->p.nbin;
     // zeroes too: per round, blocks done << 32 | survivors (the tail's sweep
@@ -778,6 +788,29 @@ int run_fit(Session *s, const DiagArgs *fork)
             if (flagged >= 0) {
                 if (int rc = fork_diag(s, *fork, flagged)) return rc;
                 flagged = -1;
+            }
+            // (auto: not when the statistics run the one-wave chain-layout kernel,
+            // nbin 1024, whose 8-wave blocks beside the tail stretch its critical
+            // path: C2 25.50-25.62 ms unsplit against 26.02; C5 48.9-49.3 split
+            // against 50.7-50.8, C4 2.91-2.93 against 2.94-2.96)
+            const bool split = fork && (s->tail_split_mode == IC_TAIL_SPLIT_ON ||
+                                        (s->tail_split_mode == IC_TAIL_SPLIT_AUTO && !(nbin == 1024 && fork->chain)));
+            if (split && s->fork_round >= 0 && cur && !s->fftded) {
+                // the second fork: the fork round's survivors fitted by now (not in
+                // the tail's list, marked here) are measured on dstream beside the tail
+                CK(launch_mark_list(s->stream, cur, cin, P, bound, s->tmark, 1));
+                CK(hipEventRecord(s->fork2_ev, s->stream));
+                CK(hipStreamWaitEvent(s->dstream, s->fork2_ev, 0));
+                DiagArgs b1 = *fork;
+                b1.list = s->lists + 2 * P;
+                b1.nctr = ctr + s->fork_round;
+                b1.skip = s->tmark;
+                LAUNCH_ON(s, K_DIAG, s->dstream, launch_diag(s->dstream, b1));
+                CK(hipEventRecord(s->join_ev, s->dstream));
+                s->tail_split = true;
+                s->tail_list = cur;
+                s->tail_cin = cin;
+                s->tail_bound = bound;
             }
             LAUNCH(s, K_FIT_TAIL, launch_fit_tail(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
                                                   s->fs, s->amp, s->info, tail_sweeps));
@@ -999,7 +1032,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         // (a higher priority for the fit's stream measured no different)
         if (hipStreamCreateWithFlags(&s->dstream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&s->fork_ev, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s->join_ev, hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&s->join_ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s->fork2_ev, hipEventDisableTiming) != hipSuccess)
             return bail(fail(IC_EHIP, "diagnostics stream / events failed"));
     }
     const size_t P = s->P, N = s->N;
@@ -1077,6 +1111,10 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (exact) AL(s->lists, 3 * P);   // two ping-pong round lists + the fork round's survivors
     AL(s->rcount, (size_t)kRoundWords + 8);   // + the lanes' queue, the tail's and the lanes' sweep counters
     if (exact) AL(s->late, P);
+    if (exact) {
+        AL(s->tmark, P);
+        if (hipMemset(s->tmark, 0, P) != hipSuccess) return bail(fail(IC_EHIP, "hipMemset(tail marks) failed"));
+    }
     if (sharded) {
         const char *cerr = nullptr;
         s->comm = make_comm(&cerr);
@@ -1555,7 +1593,16 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             LAUNCH(s, K_ROTATE, launch_rotate(s->stream, ra));
             da = ds;
         }
-        if (s->fork_round >= 0) {
+        if (s->tail_split) {
+            // the tail's profiles (the rest of pass B ran beside the tail), then
+            // join dstream and clear the marks for the next iteration
+            DiagArgs b = da;
+            b.list = s->tail_list;
+            b.nctr = s->tail_cin;
+            LAUNCH(s, K_DIAG, launch_diag(s->stream, b));
+            CK(hipStreamWaitEvent(s->stream, s->join_ev, 0));
+            CK(launch_mark_list(s->stream, s->tail_list, s->tail_cin, (long)s->P, s->tail_bound, s->tmark, 0));
+        } else if (s->fork_round >= 0) {
             // pass B: the profiles still fitting at the fork, then join pass A
             DiagArgs b = da;
             b.list = s->lists + 2 * s->P;
@@ -1801,6 +1848,10 @@ int ic_set_option(void *session, int option, int64_t v)
         if (v < 0 || v > 1 << 20) return fail(IC_EINVAL, "IC_OPT_FIT_LANE_WAVES=%lld outside 0..2^20", (long long)v);
         s->lane_waves = (int)v;
         return IC_OK;
+    case IC_OPT_TAIL_SPLIT:
+        if (v < 0 || v > 2) return fail(IC_EINVAL, "IC_OPT_TAIL_SPLIT=%lld (0, 1 or 2)", (long long)v);
+        s->tail_split_mode = (int)v;
+        return IC_OK;
     case IC_OPT_FIT_LATE_LANES:
         if (v < 0) return fail(IC_EINVAL, "IC_OPT_FIT_LATE_LANES=%lld < 0", (long long)v);
         if (v > 0 && !(exact_shift && s->lanes))
@@ -1829,6 +1880,7 @@ int ic_get_option(void *session, int option, int64_t *out)
     case IC_OPT_FIT_SCHEDULE: *out = s->fit_schedule; return IC_OK;
     case IC_OPT_FIT_LANE_WAVES: *out = s->lane_waves; return IC_OK;
     case IC_OPT_FIT_LATE_LANES: *out = s->late_lanes; return IC_OK;
+    case IC_OPT_TAIL_SPLIT: *out = s->tail_split_mode; return IC_OK;
     default: return fail(IC_EINVAL, "unknown option %d", option);
     }
 }

@@ -13,7 +13,7 @@ from helpers import bits_equal, nan_equal
 pytestmark = pytest.mark.gpu
 
 
-def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1, schedule=0, lane_waves=0, late_lanes=0):
+def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1, schedule=0, lane_waves=0, late_lanes=0, split=2):
     from iterative_cleaner_amd import _native, synth
     nsub, nchan, nbin = shape
     data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
@@ -21,7 +21,7 @@ def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1, schedule=0, lane_waves
     with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=0,
                             options={"diag_fork": fork, "fit_schedule": schedule,
                                      "fit_lane_waves": lane_waves,
-                                     "fit_late_lanes": late_lanes}) as s:
+                                     "fit_late_lanes": late_lanes, "tail_split": split}) as s:
         if tail is not None:
             s.set_fit_tail(tail)
         s.upload(raw, w0, shift)
@@ -100,3 +100,21 @@ def test_late_lanes_are_bit_identical(monkeypatch, shape, late):
             assert bits_equal(x1, x0), (fork, tail, name)
         if late > 1 << 30 and tail == 0:
             assert got[7]["fit_lane_slots"] > 0
+
+
+@pytest.mark.parametrize("shape", [(40, 512, 1024), (30, 512, 512), (12, 512, 2048), (24, 300, 256)])
+@pytest.mark.parametrize("split", [0, 1])
+def test_tail_split_is_bit_identical(monkeypatch, shape, split):
+    """Option tail_split: at the hand-over to k_fit_tail the fork round's
+    survivors that are already fitted are measured on the second stream beside
+    the tail (their list minus the tail's, marked), the tail's after it.  The
+    same bits as the unforked schedule, with the hand-over before and after the
+    fork round."""
+    ref = _run(monkeypatch, shape, 0, None)
+    for fork, tail in ((1, 4096), (3, None), (2, 1024)):
+        got = _run(monkeypatch, shape, fork, tail, split=split)
+        assert got[3]["loops"] == ref[3]["loops"]
+        assert bits_equal(got[3]["weights"], ref[3]["weights"]) and bits_equal(got[3]["test"], ref[3]["test"])
+        assert bits_equal(got[4], ref[4]) and bits_equal(got[5], ref[5])
+        for name, x0, x1 in zip(("std", "mean", "ptp", "fftmax"), ref[6], got[6]):
+            assert bits_equal(x1, x0), (fork, tail, name)

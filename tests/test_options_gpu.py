@@ -17,11 +17,11 @@ def test_option_ranges_and_modes():
         assert defaults == {"fit_tail": 8192, "diag_fork": 3, "fork_delay": 1, "template_incr": 1,
                             "fit_tiled": 1, "rowstat_waves": 8, "rowstat_minlen": 1024, "diag_chain": 1,
                             "sync_timeout_ms": 600000, "fit_schedule": 0, "fit_lane_waves": 0,
-                            "fit_late_lanes": 0}
+                            "fit_late_lanes": 0, "tail_split": 2}
         for name, bad in (("fit_tail", -1), ("diag_fork", 65), ("diag_fork", -1), ("fork_delay", 9),
                           ("template_incr", 2), ("fit_tiled", -1), ("rowstat_waves", 2),
                           ("rowstat_minlen", 0), ("diag_chain", 3), ("sync_timeout_ms", 0),
-                          ("fit_schedule", 2), ("fit_lane_waves", -1), ("fit_late_lanes", -1)):
+                          ("fit_schedule", 2), ("fit_lane_waves", -1), ("fit_late_lanes", -1), ("tail_split", 3)):
             with pytest.raises(_native.NativeError, match="IC_OPT"):
                 s.set_option(name, bad)
             assert s.get_option(name) == defaults[name]
