@@ -246,8 +246,7 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  *                          fork round's survivors already fitted are measured
  *                          on the second stream beside the tail, only the
  *                          tail's profiles after it: IC_TAIL_SPLIT_OFF, _ON, or
- *                          _AUTO (on unless nbin is 1024 with the chain-layout
- *                          statistics kernel); IC_TAIL_SPLIT_AUTO
+ *                          _AUTO (on for nbin >= 2048); IC_TAIL_SPLIT_AUTO
  *   IC_OPT_FIT_LATE_LANES  IC_FIT_ROUNDS: once at most this many profiles are
  *                          still fitting (after round 1 or later, and above
  *                          IC_OPT_FIT_TAIL), one k_fit_lanes launch resumes

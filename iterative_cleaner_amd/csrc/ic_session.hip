@@ -789,12 +789,13 @@ int run_fit(Session *s, const DiagArgs *fork)
                 if (int rc = fork_diag(s, *fork, flagged)) return rc;
                 flagged = -1;
             }
-            // (auto: not when the statistics run the one-wave chain-layout kernel,
-            // nbin 1024, whose 8-wave blocks beside the tail stretch its critical
-            // path: C2 25.50-25.62 ms unsplit against 26.02; C5 48.9-49.3 split
-            // against 50.7-50.8, C4 2.91-2.93 against 2.94-2.96)
+            // (auto: profiles of >= 2048 bins, whose tail and statistics are long
+            // enough to share the chip: C5 48.9-49.3 ms split against 50.7-50.8;
+            // at 1024 bins the statistics' 8-wave blocks beside the tail stretch
+            // its critical path, C2 26.0 against 25.5-25.6, C3 173.0 against
+            // 171.7; C1 1.29-1.31 against 1.26-1.27; C4 2.91-2.93 against 2.94-2.96)
             const bool split = fork && (s->tail_split_mode == IC_TAIL_SPLIT_ON ||
-                                        (s->tail_split_mode == IC_TAIL_SPLIT_AUTO && !(nbin == 1024 && fork->chain)));
+                                        (s->tail_split_mode == IC_TAIL_SPLIT_AUTO && nbin >= 2048));
             if (split && s->fork_round >= 0 && cur && !s->fftded) {
                 // the second fork: the fork round's survivors fitted by now (not in
                 // the tail's list, marked here) are measured on dstream beside the tail
