@@ -380,6 +380,10 @@ def batch_main(a, workload, rank, world, local, dev):
         pinned.append(trio)
         items.append(tuple(p.array for p in trio))
     sessions = [_native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local) for _ in range(a.lanes)]
+    for sess in sessions:
+        for opt in a.option:
+            name, _, value = opt.partition("=")
+            sess.set_option(name, int(value))
     stream = [items[k % 3] for k in range(a.batch)]
     for _ in range(a.warmup):
         for _out in batch.run_lanes(sessions, stream, fetch=False):

@@ -52,6 +52,9 @@ def pipeline(session, items, fetch=True):
     yield session.run(fetch)
 
 
+_EXITED = -2   # a worker's last message (run_lanes)
+
+
 def run_lanes(sessions, items, fetch=True, stop=None, join_timeout=None):
     """Clean every (cube, w0, shift) of `items` on `len(sessions)` sessions of one
     shape concurrently (one host thread per session, shared work queue; each
@@ -103,6 +106,8 @@ def run_lanes(sessions, items, fetch=True, stop=None, join_timeout=None):
         except BaseException as e:  # noqa: BLE001 - re-raised by the consumer
             stop.set()
             done.put((-1, e))
+        finally:
+            done.put((_EXITED, lane))   # the consumer counts the live workers down without polling
 
     threads = [threading.Thread(target=worker, args=(q, sess), daemon=True) for q, sess in enumerate(sessions)]
     for th in threads:
@@ -143,12 +148,12 @@ def run_lanes(sessions, items, fetch=True, stop=None, join_timeout=None):
                 yield ready.pop(nxt)
                 nxt += 1
                 continue
-            if live == 0 and not feeder.is_alive():
+            if live == 0:
+                feeder.join()   # past its items (or stopped): it returns within one put timeout
                 break
-            try:
-                idx, out = done.get(timeout=0.5)
-            except queue.Empty:
-                live = sum(th.is_alive() for th in threads)
+            idx, out = done.get()
+            if idx == _EXITED:
+                live -= 1
                 continue
             if idx < 0:
                 raise out
