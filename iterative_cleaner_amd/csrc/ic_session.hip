@@ -261,13 +261,6 @@ static hipError_t take_event(Session *s, hipEvent_t *e)
 // up with hipErrorLaunchTimeOut and marks the session failed, so a kernel
 // that never finishes fails the run instead of hanging its caller, and no
 // later call reuses buffers its kernels may still be using.
-// Queries are spaced (IC_POLL_NS of clock reads between two hipEventQuery
-// calls while spinning, a yield and 8x that after): every query takes the HIP
-// runtime's locks, and sessions polling back to back from several host
-// threads (the batch lanes) starved each other's launches.
-#ifndef IC_POLL_NS
-#define IC_POLL_NS 2000
-#endif
 static hipError_t poll_event(Session *s, hipEvent_t ev)
 {
     using clk = std::chrono::steady_clock;
@@ -276,17 +269,12 @@ static hipError_t poll_event(Session *s, hipEvent_t ev)
     const auto limit = std::chrono::duration<double>(s->sync_timeout_s);
     hipError_t e;
     while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
-        const auto t = clk::now();
-        const auto dt = t - t0;
+        const auto dt = clk::now() - t0;
         if (dt > limit) {
             s->failed = true;
             return hipErrorLaunchTimeOut;
         }
-        const bool late = dt > spin;
-        if (late) sched_yield();
-        const auto gap = std::chrono::nanoseconds(late ? 8 * IC_POLL_NS : IC_POLL_NS);
-        while (clk::now() - t < gap) {
-        }
+        if (dt > spin) sched_yield();
     }
     return e;
 }
