@@ -1059,6 +1059,13 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     // slows the late fit rounds more than it hides: off by default there
     // (C2 --dedisp fft: 56.7-56.9 ms per clean forked, 55.4-55.5 unforked)
     if (s->fftded) s->diag_fork = 0;
+    // long profiles take more rounds before their late phase: C5 (4096 bins)
+    // 49.7-49.9 ms per clean forked after round 3 / delay 1, 48.2 after
+    // round 4 / delay 2 (round 5: 48.4-48.7, 6: 49.1)
+    if (!s->fftded && nbin >= 2048) {
+        s->diag_fork = 4;
+        s->fork_delay = 2;
+    }
     // the fit cube (written by k_chan_partials mode 3, or by k_rotate in the FFT
     // mode) is tiled; IC_OPT_FIT_TILED = 0: row-major.  The closed-form fit of
     // the FFT mode reads its rotated fit cube row by row (k_diag DIAG_FIT).
