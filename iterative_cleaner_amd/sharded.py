@@ -31,7 +31,7 @@ def _loop_kwargs(args):
                 subintthresh=args.get("subintthresh", 5.0),
                 pulse_region=args.get("pulse_region", (0, 0, 1)),
                 baseline_duty=args.get("baseline_duty", 0.15), fit_mode=args.get("fit_mode", 0),
-                data_f64=args.get("data_f64", False))
+                data_f64=args.get("data_f64", False), options=args.get("options"))
 
 
 def clean_cube_local(cube, w0, shift, world, devices=None, want_details=False, fit_tail=None, **args):

@@ -68,6 +68,21 @@ def test_local_shards_moving_window_and_pulse_region():
         assert out["loops"] == one["loops"]
 
 
+@pytest.mark.parametrize("opts", [{"tail_split": 1, "diag_fork": 2}, {"fit_late_lanes": 1 << 40},
+                                  {"fit_schedule": 1, "diag_fork": 3}])
+def test_local_shards_under_schedule_options(opts):
+    """Schedule options on every shard (the second fork at the tail, the late
+    lanes, the lanes schedule): the same bits as one default session."""
+    from iterative_cleaner_amd import sharded, synth
+    data, w0, shift = synth.make_cube(12, 2048, 256, 34, 0.2)
+    raw = np.ascontiguousarray(data[:, 0])
+    one = _single(raw, w0, shift)
+    out = sharded.clean_cube_local(raw, w0, shift, 4, want_details=True, fit_tail=1024, options=opts)
+    assert out["loops"] == one["loops"] and np.array_equal(out["changed"], one["changed"])
+    for key in ("weights", "test", "amp", "info", "std", "mean", "ptp", "fft", "T"):
+        assert bits_equal(out[key], one[key]), key
+
+
 def test_shard_layout_rejects_bad_worlds():
     from iterative_cleaner_amd import _native
     with pytest.raises(_native.NativeError):
