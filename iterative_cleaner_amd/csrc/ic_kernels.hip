@@ -1801,10 +1801,14 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 // independent).  The append is aggregated per block (one atomic per 512
 // profiles), and the last block to finish publishes the final count to
 // host-mapped memory (host_n), so the host needs no copy dispatch to learn it.
-#ifndef FIT_STATE_BS
-#define FIT_STATE_BS 512
+// BS threads per block: 512 for large sessions, 256 below IC_STATE_SMALL_P
+// profiles (twice the blocks: C5 47.8 -> 45.6-46.3 ms per clean; C2 with 256
+// 26.55 against 26.44-26.49)
+#ifndef IC_STATE_SMALL_P
+#define IC_STATE_SMALL_P 524288
 #endif
-__global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
+template <int BS>
+__global__ __launch_bounds__(BS) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
                                                             const unsigned long long *__restrict__ nctr,
                                                             double *__restrict__ amp_o, int32_t *__restrict__ info_o,
                                                             int32_t *__restrict__ next_list,
@@ -1812,10 +1816,10 @@ __global__ __launch_bounds__(FIT_STATE_BS) void k_fit_state(FitStateArrays S, lo
                                                             unsigned *__restrict__ done, int32_t *host_n,
                                                             uint8_t *__restrict__ late)
 {
-    __shared__ int wcnt[FIT_STATE_BS / 64];
-    __shared__ int woff[FIT_STATE_BS / 64];
-    __shared__ int wcntB[FIT_STATE_BS / 64];
-    __shared__ int woffB[FIT_STATE_BS / 64];
+    __shared__ int wcnt[BS / 64];
+    __shared__ int woff[BS / 64];
+    __shared__ int wcntB[BS / 64];
+    __shared__ int woffB[BS / 64];
     const long slot = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const RoundList rl(list, nctr, P);
     const long nact = rl.n();
@@ -5185,8 +5189,12 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
-    IC_GGL(k_fit_state, dim3(cdiv(n, FIT_STATE_BS)), dim3(FIT_STATE_BS), 0, st, S, P, list, nctr, amp,
-                       info, next_list, ctr, done, host_n, late);
+    if (P < (long)IC_STATE_SMALL_P)
+        IC_GGL(k_fit_state<256>, dim3(cdiv(n, 256)), dim3(256), 0, st, S, P, list, nctr, amp, info, next_list, ctr,
+               done, host_n, late);
+    else
+        IC_GGL(k_fit_state<512>, dim3(cdiv(n, 512)), dim3(512), 0, st, S, P, list, nctr, amp, info, next_list, ctr,
+               done, host_n, late);
     return hipGetLastError();
 }
 
