@@ -63,6 +63,7 @@ const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",
                                      "k_tnorm",         "k_rotate",    "k_fit_lanes"};
 
 constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
+constexpr long kTailProfilesLarge = 4096;   // the same for sessions of >= 2^20 profiles
 
 struct Timed {
     int kid;
@@ -1059,6 +1060,10 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     // slows the late fit rounds more than it hides: off by default there
     // (C2 --dedisp fft: 56.7-56.9 ms per clean forked, 55.4-55.5 unforked)
     if (s->fftded) s->diag_fork = 0;
+    // large sessions hand over later: C2 (1.15 M profiles) 26.49-26.56 ms per
+    // clean at 8192, 26.19-26.23 at 4096 (2048: 26.23-26.28, 6144: 26.30-26.34),
+    // C3 flat; C4 and C5 lose at 4096 (2.90 -> 3.02-3.04, 46.5 -> 46.9)
+    if (P >= ((size_t)1 << 20)) s->tail_threshold = kTailProfilesLarge;
     // long profiles take more rounds before their late phase: C5 (4096 bins)
     // 49.7-49.9 ms per clean forked after round 3 / delay 1, 48.2 after
     // round 4 / delay 2 (round 5: 48.4-48.7, 6: 49.1)
