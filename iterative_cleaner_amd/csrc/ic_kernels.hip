@@ -1801,9 +1801,10 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 // independent).  The append is aggregated per block (one atomic per 512
 // profiles), and the last block to finish publishes the final count to
 // host-mapped memory (host_n), so the host needs no copy dispatch to learn it.
-// BS threads per block: 512 for large sessions, 256 below IC_STATE_SMALL_P
-// profiles (twice the blocks: C5 47.8 -> 45.6-46.3 ms per clean; C2 with 256
-// 26.55 against 26.44-26.49)
+// BS threads per block: 512 for rounds of IC_STATE_SMALL_P profiles or more,
+// 256 below (twice the blocks: C5 47.8 -> 45.6-46.3 ms per clean; C2's late
+// rounds 25.41-25.43 -> 25.29-25.31; 256 for C2's full rounds too: 26.55
+// against 26.44-26.49)
 #ifndef IC_STATE_SMALL_P
 #define IC_STATE_SMALL_P 524288
 #endif
@@ -1969,7 +1970,7 @@ __global__ __launch_bounds__(BS) void k_fit_state(FitStateArrays S, long P, cons
 // the exact path (true divisions, branchy enorm), so it matches k_fit_pass
 // bit for bit whatever the lane's range.
 #define TAIL_CH 256
-#define TAIL_WAVES 4
+#define TAIL_WAVES 2   // waves (profiles) per block: C4 2.88-2.92 -> 2.85-2.90 ms against 4; C2, C5 the same
 
 // s += a[0], s += a[1], ... in order (and t over b, a second chain interleaved
 // with it).  The terms are read from LDS in register blocks of SB, the next
@@ -5189,7 +5190,7 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
-    if (P < (long)IC_STATE_SMALL_P)
+    if (n < (long)IC_STATE_SMALL_P)
         IC_GGL(k_fit_state<256>, dim3(cdiv(n, 256)), dim3(256), 0, st, S, P, list, nctr, amp, info, next_list, ctr,
                done, host_n, late);
     else
