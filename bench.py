@@ -488,6 +488,7 @@ def main():
     # channel shards over "nccl" use the library's native RCCL transport;
     # IC_BENCH_TRANSPORT=torch keeps the torch.distributed callbacks (A/B)
     native_rccl = backend == "nccl" and os.environ.get("IC_BENCH_TRANSPORT", "rccl") == "rccl"
+    native_error, transport_note = None, None
     gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -514,12 +515,28 @@ def main():
         cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, c0, c1, dev)
         comm = TorchComm(dev)
         kw = dict(max_iter=5, device=local, fit_mode=fit_mode, delay=None if delay is None else delay[c0:c1])
+        sess = None
         if native_rccl:
             # the library's own RCCL communicator: every exchange issued from C++
-            # on the session stream (rank 0's unique id shared once)
+            # on the session stream (rank 0's unique id shared once).  Every rank
+            # agrees on the transport: if any rank could not create its native
+            # communicator (e.g. librccl not loadable), all fall back to the
+            # torch.distributed callbacks, and the line says so.
             from iterative_cleaner_amd.dist import share_rccl_id
-            sess = _native.ShardSession(nsub, nchan, nbin, rank, world, rccl_id=share_rccl_id(), **kw)
-        else:
+            try:
+                sess = _native.ShardSession(nsub, nchan, nbin, rank, world, rccl_id=share_rccl_id(), **kw)
+            except _native.NativeError as e:
+                native_error = str(e)[:200]
+            ok = torch.tensor([1 if sess is not None else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0:
+                if sess is not None:
+                    sess.close()
+                    sess = None
+                native_rccl = False
+                transport_note = "native RCCL unavailable on some rank (%s): torch.distributed callbacks" % (
+                    native_error or "see the other ranks")
+        if sess is None:
             sess = _native.ShardSession(nsub, nchan, nbin, rank, world, comm=comm, **kw)
         per_rank_P = nsub * (c1 - c0)
     else:
@@ -711,7 +728,7 @@ def main():
             parallelism = "channel-sharded x%d (RCCL per iteration: 3 all-to-alls to row owners, " \
                           "3 all-gathers of owner results, 1 all-reduce; %s)" % (
                               world, "native RCCL communicator, collectives issued from C++" if native_rccl
-                              else "torch.distributed callbacks")
+                              else (transport_note or "torch.distributed callbacks"))
         else:
             parallelism = "replicas" if world > 1 else "single"
         rec = {
