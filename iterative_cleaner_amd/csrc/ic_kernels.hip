@@ -4065,7 +4065,7 @@ __device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
 // A/B knobs: waves per SIMD at N <= 1024; prefetch of the post step's
 // twiddles/phasors one pair ahead; prefetch of the next profile's rows
 #ifndef IC_ROT_OCC
-#define IC_ROT_OCC 4
+#define IC_ROT_OCC 3   // round 4: 4 spilled 21 VGPRs; 3 (154 VGPRs, none spilled): C2 fft 57.0 -> 56.4 ms
 #endif
 #ifndef IC_ROT_POSTPF
 #define IC_ROT_POSTPF 0
