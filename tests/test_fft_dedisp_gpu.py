@@ -193,6 +193,33 @@ def test_fft_closed_form_loop_matches_c_oracle(case, oracle_lib):
     assert _same(R, ref["residual"])
 
 
+@pytest.mark.parametrize("opts", [{"diag_fork": 3}, {"diag_fork": 1, "template_incr": 0, "fit_tiled": 0}])
+def test_fft_local_shards_under_schedule_options(opts):
+    """FFT-mode channel shards with the fork (each shard's forked residual
+    rotation) and the plain schedule: the same bits as one default session."""
+    from iterative_cleaner_amd import sharded, synth
+    nsub, nchan, nbin = 8, 1100, 256
+    data, w0, shift = synth.make_cube(nsub, nchan, nbin, 91, 0.2)
+    delay = synth.fractional_delays(shift, nbin)
+    raw = np.ascontiguousarray(data[:, 0])
+    zero = np.zeros(nchan, np.int32)
+    with _native_session(nsub, nchan, nbin, delay) as s:
+        s.upload(raw, w0, zero)
+        one = s.run()
+        one["amp"], one["info"] = s.fit()
+        one["std"], one["mean"], one["ptp"], one["fft"] = s.diagnostics()
+    out = sharded.clean_cube_local(raw, w0, zero, 4, want_details=True, fit_tail=512, delay=delay,
+                                   options=opts)
+    assert out["loops"] == one["loops"] and np.array_equal(out["changed"], one["changed"])
+    for key in ("weights", "test", "amp", "info", "std", "mean", "ptp", "fft"):
+        assert bits_equal(out[key], one[key]), key
+
+
+def _native_session(nsub, nchan, nbin, delay):
+    from iterative_cleaner_amd import _native
+    return _native.GpuSession(nsub, nchan, nbin, device=0, delay=delay)
+
+
 def test_fft_pols_f64_and_local_shards(oracle_lib):
     """Device pscrunch, f64 data and in-process channel shards in FFT mode."""
     import threading
