@@ -220,7 +220,8 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  * cannot serve.
  *   IC_OPT_FIT_TAIL        profiles left when k_fit_tail takes over the exact
  *                          fit (one wave per profile), >= 0, 0 = never; 8192
- *                          (4096 for sessions of >= 2^20 profiles)
+ *                          (4096 for sessions of >= 2^20 profiles, else 12288
+ *                          for nbin >= 2048)
  *   IC_OPT_DIAG_FORK       fit round after which the diagnostics of the fitted
  *                          profiles run on a second stream, 0..64, 0 = no fork;
  *                          3 with integer dedispersion (4 for nbin >= 2048), 0

@@ -64,6 +64,7 @@ const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",
 
 constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
 constexpr long kTailProfilesLarge = 4096;   // the same for sessions of >= 2^20 profiles
+constexpr long kTailProfilesLong = 12288;   // smaller sessions of >= 2048-bin profiles
 
 struct Timed {
     int kid;
@@ -1064,6 +1065,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     // clean at 8192, 26.19-26.23 at 4096 (2048: 26.23-26.28, 6144: 26.30-26.34),
     // C3 flat; C4 and C5 lose at 4096 (2.90 -> 3.02-3.04, 46.5 -> 46.9)
     if (P >= ((size_t)1 << 20)) s->tail_threshold = kTailProfilesLarge;
+    // long profiles hand over earlier: C5 (4096 bins) 46.1-47.0 ms at 8192,
+    // 45.5-46.2 at 12288 (C4 at 512 bins flat from 6144 to 12288)
+    else if (nbin >= 2048) s->tail_threshold = kTailProfilesLong;
     // long profiles take more rounds before their late phase: C5 (4096 bins)
     // 49.7-49.9 ms per clean forked after round 3 / delay 1, 48.2 after
     // round 4 / delay 2 (round 5: 48.4-48.7, 6: 49.1)
