@@ -533,7 +533,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--skip-big", action="store_true")
-    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64,fft (round-2 fixtures only)")
+    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64,fft,edge (later rounds' fixtures only)")
     a = ap.parse_args()
     ic = import_reference()
     only = set(filter(None, a.only.split(",")))
@@ -550,6 +550,8 @@ def main():
             run_f64_cases(ic, a.out)
         if "fft" in only:
             run_fft_cases(ic, a.out)
+        if "edge" in only:
+            run_edge_cases(ic, a.out)
         return
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s12x48x128", 12, 48, 128, 3, 0.05, workdir=wd, out_dir=a.out)
@@ -575,6 +577,15 @@ def main():
     run_leastsq_nonfinite(ic, a.out)
     run_f64_cases(ic, a.out)
     run_fft_cases(ic, a.out)
+    run_edge_cases(ic, a.out)
+
+
+def run_edge_cases(ic, out_dir=HERE):
+    """Degenerate archive shapes (round 4): one subint, one channel, 2 x 3."""
+    with tempfile.TemporaryDirectory() as wd:
+        run_clean_case(ic, "s1x40x64_edge", 1, 40, 64, 5, 0.2, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s6x1x128_edge", 6, 1, 128, 5, 0.2, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s2x3x64_edge", 2, 3, 64, 5, 0.2, workdir=wd, out_dir=out_dir)
 
 
 def run_fft_cases(ic, out_dir=HERE):
