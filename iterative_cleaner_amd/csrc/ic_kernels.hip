@@ -2902,7 +2902,7 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
             nanf |= __shfl_xor(nanf, off);
         }
         if (lane == 0) {
-            a.std_o[k] = valid ? sd : 0.0;
+            a.std_o[k] = valid && isfinite(mean) ? sd : 0.0;   // numpy.ma: a non-finite mean is masked -> std 0
             a.mean_o[k] = valid ? mean : 0.0;
             a.ptp_o[k] = ptp;
             a.fft_o[k] = nanf ? NAN : best;
@@ -3489,7 +3489,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
             fftv = nanx ? NAN : 0.0;
         }
         if (t == 0) {
-            a.std_o[k] = valid ? sd : 0.0;
+            a.std_o[k] = valid && isfinite(mean) ? sd : 0.0;   // numpy.ma: a non-finite mean is masked -> std 0
             a.mean_o[k] = valid ? mean : 0.0;
             a.ptp_o[k] = ptp;
             a.fft_o[k] = fftv;
@@ -3864,7 +3864,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
             fftv = nanx ? NAN : 0.0;
         }
         if (t == 0) {
-            a.std_o[kc] = valid ? sd : 0.0;
+            a.std_o[kc] = valid && isfinite(mean) ? sd : 0.0;   // numpy.ma: a non-finite mean is masked -> std 0
             a.mean_o[kc] = valid ? mean : 0.0;
             a.ptp_o[kc] = ptp;
             a.fft_o[kc] = fftv;

@@ -832,7 +832,9 @@ void orc_diagnostics(int P, int n, const float *X, const uint8_t *valid,
             if (x[i] > mx) mx = x[i];
             if (x[i] < mn) mn = x[i];
         }
-        std_o[k] = sqrt(var);
+        /* numpy.ma masks a non-finite mean (the domained divide of ma.mean), so
+         * every anomaly of ma.var is masked and its sum is 0: std 0 */
+        std_o[k] = isfinite(mean) ? sqrt(var) : 0.0;
         mean_o[k] = mean;
         ptp_o[k] = nan ? NAN : (mx - mn);
         fft_o[k] = fftmax(d, n, work, tab);
@@ -878,7 +880,9 @@ void orc_diagnostics_f64(int P, int n, const double *X, const uint8_t *valid,
             if (x[i] > mx) mx = x[i];
             if (x[i] < mn) mn = x[i];
         }
-        std_o[k] = sqrt(var);
+        /* numpy.ma masks a non-finite mean (the domained divide of ma.mean), so
+         * every anomaly of ma.var is masked and its sum is 0: std 0 */
+        std_o[k] = isfinite(mean) ? sqrt(var) : 0.0;
         mean_o[k] = mean;
         ptp_o[k] = nan ? NAN : (mx - mn);
         fft_o[k] = fftmax(d, n, work, tab);

@@ -15,12 +15,19 @@ def clean_fixtures():
     return sorted(glob.glob(os.path.join(GOLDEN, "clean_*.npz")))
 
 
+def poke_cube(data, meta):
+    """The non-finite samples a fixture placed in its synthetic data (make_golden.py poke)."""
+    for s_, c_, b_, v_ in meta.get("poke", ()):
+        data[s_, :, c_, b_] = float(v_)
+
+
 def load_clean_case(path):
     """(fixture npz, meta, raw total-intensity cube, w0, shift, args dict)."""
     z = np.load(path)
     meta = json.loads(str(z["meta"]))
     data, w0, shift = synth.make_cube(meta["nsub"], meta["nchan"], meta["nbin"], meta["seed"],
                                       meta["rfi"], npol=meta["npol"])
+    poke_cube(data, meta)
     assert hashlib.sha256(data.tobytes()).hexdigest() == str(z["input_sha256"]), \
         "synthetic generator drifted from the golden fixture"
     if meta.get("frac_weights"):
@@ -44,6 +51,18 @@ def bits_equal(a, b):
     a = np.ascontiguousarray(a)
     b = np.ascontiguousarray(b)
     return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
+
+
+def bits_equal_nan(a, b):
+    """bits_equal, except that a NaN matches any NaN: the sign and payload of a
+    NaN that an invalid operation produces are the hardware's (x86's default
+    NaN is negative, the GPU's positive), not part of numpy's semantics."""
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    if a.shape != b.shape or a.dtype != b.dtype:
+        return False
+    na, nb = np.isnan(a), np.isnan(b)
+    return bool(np.array_equal(na, nb)) and a[~na].tobytes() == b[~nb].tobytes()
 
 
 def nan_equal(a, b):
