@@ -151,8 +151,10 @@ def _load_f64(path):
 
 def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
                    keep_cubes=True, npol=1, workdir=None, out_dir=HERE, residual_full=True, data_f64=False,
-                   frac_weights=False, frac_delay=False, poke=()):
+                   frac_weights=False, frac_delay=False, poke=(), weights_zero=False):
     data, weights, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi, npol=npol)
+    if weights_zero:                  # every profile zapped before the first loop
+        weights = np.zeros_like(weights)
     for (s_, c_, b_, v_) in poke:      # non-finite samples placed in the data
         data[s_, :, c_, b_] = v_
     if frac_weights:
@@ -195,7 +197,8 @@ def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
             "args": {k: v for k, v in vars(args).items() if k != "archive"},
             "numpy": np.__version__, "scipy": scipy.__version__,
             **({"poke": [[int(a_), int(b_), int(c_), repr(float(v_))] for (a_, b_, c_, v_) in poke]}
-               if poke else {})})),
+               if poke else {}),
+            **({"weights_zero": True} if weights_zero else {})})),
     }
     for k, it in enumerate(rec.iters, start=1):
         arrays["T_%d" % k] = it["T"]
@@ -585,13 +588,14 @@ def main():
 
 
 def run_edge_cases(ic, out_dir=HERE):
-    """Degenerate archive shapes (round 4): one subint, one channel, 2 x 3; NaN / +-Inf samples."""
+    """Degenerate archives (round 4): one subint, one channel, 2 x 3; NaN / +-Inf samples; every weight 0."""
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s1x40x64_edge", 1, 40, 64, 5, 0.2, workdir=wd, out_dir=out_dir)
         run_clean_case(ic, "s6x1x128_edge", 6, 1, 128, 5, 0.2, workdir=wd, out_dir=out_dir)
         run_clean_case(ic, "s2x3x64_edge", 2, 3, 64, 5, 0.2, workdir=wd, out_dir=out_dir)
         run_clean_case(ic, "s8x24x128_nonfinite_edge", 8, 24, 128, 6, 0.2, workdir=wd, out_dir=out_dir,
                        poke=((1, 3, 10, np.nan), (4, 7, 100, np.inf), (6, 11, 0, -np.inf)))
+        run_clean_case(ic, "s4x16x64_w0_edge", 4, 16, 64, 5, 0.2, workdir=wd, out_dir=out_dir, weights_zero=True)
 
 
 def run_fft_cases(ic, out_dir=HERE):

@@ -32,6 +32,8 @@ def load_clean_case(path):
         "synthetic generator drifted from the golden fixture"
     if meta.get("frac_weights"):
         w0 = synth.fractional_weights(w0)
+    if meta.get("weights_zero"):
+        w0 = np.zeros_like(w0)
     raw = data[:, 0] if meta["npol"] == 1 else (data[:, 0] + data[:, 1]).astype(np.float32)
     return z, meta, np.ascontiguousarray(raw), w0, shift, meta["args"]
 

@@ -123,6 +123,8 @@ def test_clean_stdout_matches_reference(path, tmp_path, monkeypatch, capsys):
                                         meta["rfi"], npol=meta["npol"])
     if meta.get("frac_weights"):
         w0_ = synth.fractional_weights(w0_)
+    if meta.get("weights_zero"):
+        w0_ = np.zeros_like(w0_)
     poke_cube(data, meta)
     monkeypatch.chdir(tmp_path)
     arpath = str(tmp_path / ("%s.ar" % meta["name"]))
