@@ -588,7 +588,7 @@ def main():
 
 
 def run_edge_cases(ic, out_dir=HERE):
-    """Degenerate archives (round 4): one subint, one channel, 2 x 3; NaN / +-Inf samples; every weight 0; thresholds that zap everything."""
+    """Degenerate archives (round 4): one subint, one channel, 2 x 3; NaN / +-Inf samples; every weight 0; thresholds that zap everything; FFT-mode one subint and NaN / Inf."""
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s1x40x64_edge", 1, 40, 64, 5, 0.2, workdir=wd, out_dir=out_dir)
         run_clean_case(ic, "s6x1x128_edge", 6, 1, 128, 5, 0.2, workdir=wd, out_dir=out_dir)
@@ -598,6 +598,9 @@ def run_edge_cases(ic, out_dir=HERE):
         run_clean_case(ic, "s4x16x64_w0_edge", 4, 16, 64, 5, 0.2, workdir=wd, out_dir=out_dir, weights_zero=True)
         run_clean_case(ic, "s6x24x128_allzap_edge", 6, 24, 128, 5, 0.2, extra_args=("-c", "0.001", "-s", "0.001"),
                        workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s1x40x64_fft_edge", 1, 40, 64, 5, 0.2, frac_delay=True, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s8x24x128_fft_nonfinite_edge", 8, 24, 128, 6, 0.2, frac_delay=True, workdir=wd,
+                       out_dir=out_dir, poke=((1, 3, 10, np.nan), (4, 7, 100, np.inf)))
 
 
 def run_fft_cases(ic, out_dir=HERE):
