@@ -588,7 +588,7 @@ def main():
 
 
 def run_edge_cases(ic, out_dir=HERE):
-    """Degenerate archives (round 4): one subint, one channel, 2 x 3; NaN / +-Inf samples; every weight 0; thresholds that zap everything; FFT-mode one subint and NaN / Inf."""
+    """Degenerate archives (round 4): one subint, one channel, 2 x 3; NaN / +-Inf samples; every weight 0; thresholds that zap everything; FFT-mode one subint and NaN / Inf; f64 data with NaN / -Inf and -u."""
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s1x40x64_edge", 1, 40, 64, 5, 0.2, workdir=wd, out_dir=out_dir)
         run_clean_case(ic, "s6x1x128_edge", 6, 1, 128, 5, 0.2, workdir=wd, out_dir=out_dir)
@@ -601,6 +601,8 @@ def run_edge_cases(ic, out_dir=HERE):
         run_clean_case(ic, "s1x40x64_fft_edge", 1, 40, 64, 5, 0.2, frac_delay=True, workdir=wd, out_dir=out_dir)
         run_clean_case(ic, "s8x24x128_fft_nonfinite_edge", 8, 24, 128, 6, 0.2, frac_delay=True, workdir=wd,
                        out_dir=out_dir, poke=((1, 3, 10, np.nan), (4, 7, 100, np.inf)))
+        run_clean_case(ic, "s8x24x128_f64_nonfinite_edge", 8, 24, 128, 6, 0.2, data_f64=True, extra_args=("-u",),
+                       workdir=wd, out_dir=out_dir, poke=((2, 5, 40, -np.inf), (5, 9, 3, np.nan)))
 
 
 def run_fft_cases(ic, out_dir=HERE):
