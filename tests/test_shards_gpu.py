@@ -7,7 +7,7 @@ and bit-identical to the unsharded GPU run (same kernels)."""
 import numpy as np
 import pytest
 
-from helpers import bits_equal
+from helpers import bits_equal, bits_equal_nan
 
 pytestmark = pytest.mark.gpu
 
@@ -81,6 +81,30 @@ def test_local_shards_under_schedule_options(opts):
     assert out["loops"] == one["loops"] and np.array_equal(out["changed"], one["changed"])
     for key in ("weights", "test", "amp", "info", "std", "mean", "ptp", "fft", "T"):
         assert bits_equal(out[key], one[key]), key
+
+
+def test_local_shards_with_non_finite_samples(oracle_lib):
+    """NaN / +-Inf samples (they poison the template: nothing is zapped, std is
+    0 where numpy.ma masks the non-finite mean; clean_s8x24x128_nonfinite_edge)
+    and a zero-weight channel, at world 2 and 4: the single session's values,
+    NaN for NaN (a NaN's sign is the hardware's), and the oracle's weights."""
+    from iterative_cleaner_amd import sharded, synth
+    data, w0, shift = synth.make_cube(6, 1100, 128, 38, 0.2)
+    raw = np.ascontiguousarray(data[:, 0])
+    raw[1, 700, 10] = np.nan
+    raw[4, 300, 100] = np.inf
+    raw[5, 1050, 0] = -np.inf
+    w0 = w0.copy()
+    w0[:, 17] = 0.0
+    one = _single(raw, w0, shift)
+    ref = oracle_lib.clean_loop(raw, w0, shift, want_details=True)
+    assert one["loops"] == ref["loops"] and bits_equal(one["weights"], ref["weights"])
+    assert bits_equal_nan(one["std"], ref["std"]) and not one["std"][w0 != 0].any()
+    for world in (2, 4):
+        out = sharded.clean_cube_local(raw, w0, shift, world, want_details=True)
+        assert out["loops"] == one["loops"] and np.array_equal(out["changed"], one["changed"])
+        for key in ("weights", "test", "amp", "info", "std", "mean", "ptp", "fft", "T"):
+            assert bits_equal_nan(out[key], one[key]), "world %d: %s differs" % (world, key)
 
 
 def test_shard_layout_rejects_bad_worlds():
