@@ -536,11 +536,40 @@ def run_cli_case(ic, out_dir=HERE):
         print("wrote cli_case.npz")
 
 
+def run_cli_memory_case(ic, out_dir=HERE):
+    """main() with --memory and -o on a 4-pol archive (round 4): clean() does not
+    pscrunch the archive in memory and does not reload it (:66-70, :147-149), so
+    the named output keeps its 4 polarisations with the new weights."""
+    with tempfile.TemporaryDirectory() as wd:
+        data, weights, shift = synth.make_cube(6, 32, 64, 23, 0.2, npol=4)
+        path = os.path.join(wd, "mem.ar")
+        ica.Archive(data, weights, shift, filename=path).unload(path)
+        buf = io.StringIO()
+        old = sys.argv
+        cwd = os.getcwd()
+        os.chdir(wd)
+        try:
+            sys.argv = ["iterative_cleaner.py", "-l", "--memory", "-o", "mem_out.ar", path]
+            with contextlib.redirect_stdout(buf):
+                ic.main(ic.parse_arguments())
+        finally:
+            sys.argv = old
+            os.chdir(cwd)
+        out_ar = ica.Archive_load(os.path.join(wd, "mem_out.ar"))
+        out = out_ar.get_data()
+        np.savez_compressed(os.path.join(out_dir, "cli_memory_case.npz"),
+                            weights=out_ar.get_weights(), data_shape=np.array(out.shape),
+                            data_sha256=np.array(sha(np.ascontiguousarray(out))),
+                            stdout=np.array(buf.getvalue().replace(wd, "<WD>")),
+                            input_sha256=np.array(sha(data)))
+        print("wrote cli_memory_case.npz")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--skip-big", action="store_true")
-    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64,fft,edge (later rounds' fixtures only)")
+    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64,fft,edge,cli_memory (later rounds' fixtures only)")
     a = ap.parse_args()
     ic = import_reference()
     only = set(filter(None, a.only.split(",")))
@@ -559,6 +588,8 @@ def main():
             run_fft_cases(ic, a.out)
         if "edge" in only:
             run_edge_cases(ic, a.out)
+        if "cli_memory" in only:
+            run_cli_memory_case(ic, a.out)
         return
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s12x48x128", 12, 48, 128, 3, 0.05, workdir=wd, out_dir=a.out)
@@ -585,6 +616,7 @@ def main():
     run_f64_cases(ic, a.out)
     run_fft_cases(ic, a.out)
     run_edge_cases(ic, a.out)
+    run_cli_memory_case(ic, a.out)
 
 
 def run_edge_cases(ic, out_dir=HERE):

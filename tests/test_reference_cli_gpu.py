@@ -4,6 +4,7 @@ its drop-in host (iterative_cleaner_amd/cleaner.py):
 * ``main()`` on the CLI fixture (iterative_cleaner.py:45-62, :148-157,
   :308-335): output naming, final weights after find_bad_parts, and stdout
   byte for byte (tests/golden/cli_case.npz, written by running the reference);
+* ``main()`` with ``--memory -o`` on a 4-pol archive (tests/golden/cli_memory_case.npz);
 * ``clean()`` with ``-z``: the zap PNG is pixel-identical to the reference's
   (iterative_cleaner.py:164-171; tests/golden/zap_plot_case.npz)."""
 import hashlib
@@ -33,6 +34,30 @@ def test_cli_main_matches_reference(tmp_path, monkeypatch, capsys):
     assert printed == str(z["stdout"])
     out_ar = ica.Archive_load(os.path.join(wd, "cli_cleaned.ar"))
     assert bits_equal(out_ar.get_weights(), z["weights"])
+
+
+def test_cli_memory_output_matches_reference(tmp_path, monkeypatch, capsys):
+    """main() with --memory and -o on a 4-pol archive (iterative_cleaner.py:66-70,
+    :147-149): the named output keeps its 4 polarisations (neither pscrunched in
+    memory nor reloaded) with the reference's weights, data bytes and stdout
+    (tests/golden/cli_memory_case.npz)."""
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import cleaner, synth
+    z = np.load(os.path.join(GOLDEN, "cli_memory_case.npz"))
+    data, weights, shift = synth.make_cube(6, 32, 64, 23, 0.2, npol=4)
+    assert hashlib.sha256(data.tobytes()).hexdigest() == str(z["input_sha256"])
+    wd = str(tmp_path)
+    path = os.path.join(wd, "mem.ar")
+    ica.Archive(data, weights, shift, filename=path).unload(path)
+    monkeypatch.chdir(tmp_path)
+    cleaner.main(cleaner.parse_arguments(["-l", "--memory", "-o", "mem_out.ar", path]))
+    printed = capsys.readouterr().out.replace(wd, "<WD>")
+    assert printed == str(z["stdout"])
+    out_ar = ica.Archive_load(os.path.join(wd, "mem_out.ar"))
+    out = np.ascontiguousarray(out_ar.get_data())
+    assert out.shape == tuple(z["data_shape"])
+    assert bits_equal(out_ar.get_weights(), z["weights"])
+    assert hashlib.sha256(out.tobytes()).hexdigest() == str(z["data_sha256"])
 
 
 def test_zap_png_matches_reference(tmp_path, monkeypatch):
