@@ -536,6 +536,30 @@ def run_cli_case(ic, out_dir=HERE):
         print("wrote cli_case.npz")
 
 
+def run_cli_std_name_case(ic, out_dir=HERE):
+    """main() with -o std -q (round 4): the NAME.FREQ.MJD.ar output name
+    (iterative_cleaner.py:52-56) and its weights."""
+    with tempfile.TemporaryDirectory() as wd:
+        data, weights, shift = synth.make_cube(5, 16, 64, 24, 0.2)
+        path = os.path.join(wd, "std.ar")
+        ica.Archive(data, weights, shift, filename=path).unload(path)
+        old = sys.argv
+        cwd = os.getcwd()
+        os.chdir(wd)
+        try:
+            sys.argv = ["iterative_cleaner.py", "-l", "-q", "-o", "std", path]
+            ic.main(ic.parse_arguments())
+        finally:
+            sys.argv = old
+            os.chdir(cwd)
+        names = sorted(f for f in os.listdir(wd) if f != "std.ar")
+        assert len(names) == 1, names
+        out_ar = ica.Archive_load(os.path.join(wd, names[0]))
+        np.savez_compressed(os.path.join(out_dir, "cli_std_name_case.npz"), name=np.array(names[0]),
+                            weights=out_ar.get_weights(), input_sha256=np.array(sha(data)))
+        print("wrote cli_std_name_case.npz (%s)" % names[0])
+
+
 def run_cli_memory_case(ic, out_dir=HERE):
     """main() with --memory and -o on a 4-pol archive (round 4): clean() does not
     pscrunch the archive in memory and does not reload it (:66-70, :147-149), so
@@ -590,6 +614,7 @@ def main():
             run_edge_cases(ic, a.out)
         if "cli_memory" in only:
             run_cli_memory_case(ic, a.out)
+            run_cli_std_name_case(ic, a.out)
         return
     with tempfile.TemporaryDirectory() as wd:
         run_clean_case(ic, "s12x48x128", 12, 48, 128, 3, 0.05, workdir=wd, out_dir=a.out)
@@ -617,6 +642,7 @@ def main():
     run_fft_cases(ic, a.out)
     run_edge_cases(ic, a.out)
     run_cli_memory_case(ic, a.out)
+    run_cli_std_name_case(ic, a.out)
 
 
 def run_edge_cases(ic, out_dir=HERE):

@@ -4,7 +4,8 @@ its drop-in host (iterative_cleaner_amd/cleaner.py):
 * ``main()`` on the CLI fixture (iterative_cleaner.py:45-62, :148-157,
   :308-335): output naming, final weights after find_bad_parts, and stdout
   byte for byte (tests/golden/cli_case.npz, written by running the reference);
-* ``main()`` with ``--memory -o`` on a 4-pol archive (tests/golden/cli_memory_case.npz);
+* ``main()`` with ``--memory -o`` on a 4-pol archive (tests/golden/cli_memory_case.npz)
+  and with ``-o std`` (the NAME.FREQ.MJD.ar name, tests/golden/cli_std_name_case.npz);
 * ``clean()`` with ``-z``: the zap PNG is pixel-identical to the reference's
   (iterative_cleaner.py:164-171; tests/golden/zap_plot_case.npz)."""
 import hashlib
@@ -58,6 +59,24 @@ def test_cli_memory_output_matches_reference(tmp_path, monkeypatch, capsys):
     assert out.shape == tuple(z["data_shape"])
     assert bits_equal(out_ar.get_weights(), z["weights"])
     assert hashlib.sha256(out.tobytes()).hexdigest() == str(z["data_sha256"])
+
+
+def test_cli_std_output_name_matches_reference(tmp_path, monkeypatch):
+    """main() with -o std -q: the reference's NAME.FREQ.MJD.ar name
+    (iterative_cleaner.py:52-56) and weights (tests/golden/cli_std_name_case.npz)."""
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import cleaner, synth
+    z = np.load(os.path.join(GOLDEN, "cli_std_name_case.npz"))
+    data, weights, shift = synth.make_cube(5, 16, 64, 24, 0.2)
+    assert hashlib.sha256(data.tobytes()).hexdigest() == str(z["input_sha256"])
+    wd = str(tmp_path)
+    path = os.path.join(wd, "std.ar")
+    ica.Archive(data, weights, shift, filename=path).unload(path)
+    monkeypatch.chdir(tmp_path)
+    cleaner.main(cleaner.parse_arguments(["-l", "-q", "-o", "std", path]))
+    names = sorted(f for f in os.listdir(wd) if f != "std.ar")
+    assert names == [str(z["name"])]
+    assert bits_equal(ica.Archive_load(os.path.join(wd, names[0])).get_weights(), z["weights"])
 
 
 def test_zap_png_matches_reference(tmp_path, monkeypatch):
