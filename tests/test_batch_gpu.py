@@ -5,7 +5,7 @@ archive, in order; misuse of the upload queue fails loudly."""
 import numpy as np
 import pytest
 
-from helpers import bits_equal
+from helpers import bits_equal, bits_equal_nan
 
 pytestmark = pytest.mark.gpu
 
@@ -51,6 +51,26 @@ def test_clean_batch_concurrent_lanes_match_single_sessions(lanes):
         ref = _one(cube, w0, shift)
         assert out["loops"] == ref["loops"] and np.array_equal(out["changed"], ref["changed"])
         assert bits_equal(out["weights"], ref["weights"]) and bits_equal(out["test"], ref["test"])
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_clean_batch_non_finite_archive_leaves_no_trace(lanes):
+    """An archive with NaN / Inf samples (every test value NaN, nothing zapped)
+    between ordinary ones: the sessions the batch reuses carry nothing of it
+    into the next archive, and it gives one session's results itself."""
+    from iterative_cleaner_amd import batch
+    arcs = _archives(5)
+    bad = arcs[2][0].copy()
+    bad[1, 7, 10] = np.nan
+    bad[3, 40, 100] = np.inf
+    arcs[2] = (bad, arcs[2][1], arcs[2][2])
+    got = list(batch.clean_batch(iter(arcs), SHAPE, device=0, lanes=lanes))
+    assert len(got) == len(arcs)
+    for k, ((cube, w0, shift), out) in enumerate(zip(arcs, got)):
+        ref = _one(cube, w0, shift)
+        assert out["loops"] == ref["loops"] and np.array_equal(out["changed"], ref["changed"]), k
+        assert bits_equal(out["weights"], ref["weights"]) and bits_equal_nan(out["test"], ref["test"]), k
+    assert np.isnan(got[2]["test"]).any()
 
 
 def test_pipeline_on_pinned_arrays_and_queue_rules():
