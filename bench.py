@@ -135,7 +135,7 @@ def s8d_bytes(name, nsub, nchan, nbin, launches, iterations, steps):
     chooses (lmdif's 5.5 sweeps per profile) are NOT algorithmic."""
     P = nsub * nchan
     N = P * nbin
-    per_iter = {"k_chan_partials": 4 * N, "k_fit_pass": 4 * N, "k_fit_lanes": 4 * N, "k_diag": 4 * N + 32 * P,
+    per_iter = {"k_chan_partials": 4 * N, "k_fit_pass": 4 * N, "k_diag": 4 * N + 32 * P,
                 "k_linestats": 16 * P, "k_combine": 16 * P}
     if name not in per_iter:
         return None
@@ -146,10 +146,10 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True,
     """Bytes a kernel's launches actually move, summed over the timed region
     (kernel table) - the implementation's own traffic model, not
     §8(d)'s.  `run`: one clean's counts, {"n_iter", "changed" (per iteration),
-    "fit_profile_sweeps", "fit_tail_sweeps", "fit_lane_sweeps", "window_moves"} (ic_run /
+    "fit_profile_sweeps", "fit_tail_sweeps", "window_moves"} (ic_run /
     ic_get_run_stats); every clean of the timed region is the same work.
       k_fit_pass       every profile-sweep reads its 4*nbin-byte profile once
-                       (k_fit_tail, k_fit_lanes: their own sweeps, the same);
+                       (k_fit_tail: its own sweeps, the same);
       k_fit_state      ~2 x 204 B of lmdif state per profile of a round (the
                        rounds' inputs are the sweeps of k_fit_pass);
       k_chan_partials  (every template-stage launch, k_chan_delta included)
@@ -174,8 +174,6 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True,
     n_iter = run["n_iter"]
     if name == "k_fit_pass":
         return 4 * nbin * run["fit_profile_sweeps"] * steps
-    if name == "k_fit_lanes":
-        return 4 * nbin * run.get("fit_lane_sweeps", 0) * steps
     if name == "k_fit_tail":
         return 4 * nbin * run["fit_tail_sweeps"] * steps
     if name == "k_fit_state":
@@ -458,13 +456,8 @@ def main():
     ap.add_argument("--no-flip-check", action="store_true",
                     help="closed mode: skip the (untimed) exact run that counts zap-mask flips "
                          "(profiling passes, whose kernel tallies it would mix in)")
-    ap.add_argument("--fit-schedule", choices=("rounds", "lanes"), default="rounds",
-                    help="exact fit: rounds of sweep / state kernels over compacted lists (default), or one "
-                         "persistent launch whose lanes each run lmdif for one profile after another")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="a session schedule option (_native.OPTIONS; same bits under every setting), repeatable")
-    ap.add_argument("--lane-waves", type=int, default=0,
-                    help="--fit-schedule lanes: waves of the persistent launch (0: every wave the device holds)")
     ap.add_argument("--dedisp", choices=("shift", "fft"), default="shift",
                     help="shift: integer dedispersion shifts (default); fft: fractional delays, dedispersed by "
                          "psrchive's FFT phase rotation (dedisp_mode IC_DEDISP_FFT)")
@@ -545,9 +538,6 @@ def main():
         else:
             cube, w0, shift = make_cube_device(nsub, nchan, nbin, seed + 7919 * rank, rfi, dev)
         sess = _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=local, fit_mode=fit_mode, delay=delay)
-        if a.fit_schedule == "lanes":
-            sess.set_option("fit_schedule", _native.FIT_LANES)
-            sess.set_option("fit_lane_waves", a.lane_waves)
         for opt in a.option:
             name, _, value = opt.partition("=")
             sess.set_option(name, int(value))
@@ -745,13 +735,10 @@ def main():
                        "fit_mode": a.fit_mode, "dedisp": a.dedisp,
                        "profiles_per_archive": nsub * nchan, "loops": loops[-1], "iterations": n_iter,
                        "fit_rounds": stats["fit_rounds"],
-                       "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"]
-                                                        + stats["fit_lane_sweeps"])
+                       "fit_sweeps_per_profile": round((stats["fit_profile_sweeps"] + stats["fit_tail_sweeps"])
                                                        / per_rank_P / max(1, n_iter), 2),
                        "fit_tail_sweeps": stats["fit_tail_sweeps"] // max(1, n_iter),
-                       "fit_schedule": a.fit_schedule,
-                       "fit_lane_use": (round(stats["fit_lane_sweeps"] / stats["fit_lane_slots"], 3)
-                                        if stats.get("fit_lane_slots") else None),
+                       "options": dict(opt.partition("=")[::2] for opt in a.option) or None,
                        "near_threshold_profiles": stats["near_threshold"],
                        "parallelism": parallelism,
                        "loop_hbm_gbs_per_gpu": round(loop_gbs, 1),

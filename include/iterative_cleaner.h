@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define IC_ABI_VERSION 6
+#define IC_ABI_VERSION 7
 
 #define IC_OK 0
 #define IC_EINVAL -1   /* bad argument / shape                         */
@@ -203,11 +203,9 @@ typedef struct {
     int32_t near_threshold;      /* last iteration: profiles whose test value lies within 1e-9 of
                                     the zap threshold 1.0, where fftmax's last bits (not
                                     bit-identical to numpy's pocketfft) could decide the zap */
-    int64_t fit_lane_slots;      /* k_fit_lanes: lane slots the waves swept (64 per wave sweep,
-                                    waiting lanes included); fit_lane_sweeps / this is the
-                                    share of lanes doing work */
-    int64_t fit_lane_sweeps;     /* profile sweeps done by k_fit_lanes (IC_FIT_LANES, or the
-                                    late profiles under IC_OPT_FIT_LATE_LANES) */
+    int64_t reserved0;           /* 0 (round 4's persistent-lanes counters; that schedule was
+                                    removed in round 5) */
+    int64_t reserved1;           /* 0 */
 } ic_run_stats;
 int ic_get_run_stats(void *session, ic_run_stats *out);
 
@@ -236,25 +234,15 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  *   IC_OPT_ROWSTAT_MINLEN  shortest row that takes them, 1..16384; 1024
  *   IC_OPT_DIAG_CHAIN      1 = chain-layout diagnostics kernel at nbin 1024,
  *                          2048, 4096; 0 = the row-layout kernel; 1
- *   IC_OPT_FIT_SCHEDULE    how the exact fit is scheduled (integer dedispersion):
- *                          IC_FIT_ROUNDS = rounds of a sweep kernel over every
- *                          profile with a pending data request and a state
- *                          kernel, compacted lists, k_fit_tail for the last
- *                          profiles; IC_FIT_LANES = one persistent launch whose
- *                          lanes each run lmdif for one profile after another
- *                          from a shared queue; IC_FIT_ROUNDS
- *   IC_OPT_FIT_LANE_WAVES  waves of the IC_FIT_LANES launch, 0 = every wave the
- *                          device holds at once (more are capped to that); 0
+ *   IC_OPT_FIT_SCHEDULE    how the exact fit is scheduled: IC_FIT_ROUNDS (the
+ *                          only value since round 5) = rounds of a sweep kernel
+ *                          over every profile with a pending data request and a
+ *                          state kernel, k_fit_tail for the last profiles
  *   IC_OPT_TAIL_SPLIT      with the fork: at the hand-over to k_fit_tail the
  *                          fork round's survivors already fitted are measured
  *                          on the second stream beside the tail, only the
  *                          tail's profiles after it: IC_TAIL_SPLIT_OFF, _ON, or
  *                          _AUTO (on for nbin >= 2048); IC_TAIL_SPLIT_AUTO
- *   IC_OPT_FIT_LATE_LANES  IC_FIT_ROUNDS: once at most this many profiles are
- *                          still fitting (after round 1 or later, and above
- *                          IC_OPT_FIT_TAIL), one k_fit_lanes launch resumes
- *                          them from the rounds' state and finishes the fit,
- *                          >= 0, 0 = never; 0
  *   IC_OPT_SYNC_TIMEOUT_MS longest host wait for the GPU, >= 1 ms; 600000.  A
  *                          wait that runs out fails its call with IC_EHIP and
  *                          marks the session failed: every later call on it
@@ -271,14 +259,13 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
 #define IC_OPT_DIAG_CHAIN 8
 #define IC_OPT_SYNC_TIMEOUT_MS 9
 #define IC_OPT_FIT_SCHEDULE 10
-#define IC_OPT_FIT_LANE_WAVES 11
-#define IC_OPT_FIT_LATE_LANES 12
+/* 11, 12: IC_OPT_FIT_LANE_WAVES, IC_OPT_FIT_LATE_LANES until round 4 (removed
+ * with the lanes schedule) */
 #define IC_OPT_TAIL_SPLIT 13
 #define IC_TAIL_SPLIT_OFF 0
 #define IC_TAIL_SPLIT_ON 1
 #define IC_TAIL_SPLIT_AUTO 2
 #define IC_FIT_ROUNDS 0
-#define IC_FIT_LANES 1
 int ic_set_option(void *session, int option, int64_t value);
 int ic_get_option(void *session, int option, int64_t *value);
 /* = ic_set_option(session, IC_OPT_FIT_TAIL, threshold) */
@@ -365,12 +352,26 @@ int ic_session_create_shard(const ic_params *params, int device, int rank, int w
  * (e.g. through the torch.distributed store); each rank then creates its shard
  * with them on its own device.  Every exchange is an RCCL collective (all-to-all
  * as grouped sends / receives) issued by the library on the session stream: no
- * host callback per exchange.  A failing shard aborts its communicator, so its
- * peers' collectives fail (IC_ECOMM) instead of waiting.  librccl is loaded on
- * first use (/opt/rocm/lib/librccl.so.1). */
+ * host callback per exchange.  A failing shard aborts its communicator and
+ * returns its error; a peer learns of it from RCCL (an error from its own
+ * collective, or RCCL's asynchronous error while the library waits on the
+ * GPU: IC_ECOMM), or at worst from IC_OPT_SYNC_TIMEOUT_MS (IC_EHIP).
+ * The communicator is created non-blocking and polled: a rank that never
+ * joins (it failed before ic_session_create_rccl) makes its peers' creation
+ * fail with IC_ECOMM after the init timeout instead of blocking them forever.
+ * librccl is loaded on first use (/opt/rocm/lib/librccl.so.1); IC_ECOMM if it
+ * is missing. */
 int ic_rccl_unique_id(void *id_out /* 128 bytes */);
 int ic_session_create_rccl(const ic_params *params, int device, int rank, int world, const void *unique_id,
                            void **session);
+/* The librccl file to load instead of the ROCm install's (another RCCL build,
+ * or a test stub exporting the same nccl* symbols); NULL restores the
+ * default.  Process-wide; must precede the first RCCL use of the process
+ * (IC_ESTATE after it, unless the path is the one already loaded). */
+int ic_rccl_set_library(const char *path);
+/* How long ic_session_create_rccl waits for every rank to join, in ms (>= 1;
+ * process-wide; default 600000). */
+int ic_rccl_set_init_timeout(int64_t ms);
 
 /* In-process shard group: `world` shards driven by `world` host threads of one
  * process (one or several devices), exchanging by device-to-device / peer

@@ -13,7 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # IC_LIBRARY: an alternative build of the same library (A/B measurements)
 LIB_PATH = os.environ.get("IC_LIBRARY") or os.path.join(HERE, "libicgpu.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # symbols exported by libicgpu.so, as declared in include/iterative_cleaner.h
 EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session_destroy",
@@ -25,16 +25,14 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_upload_pols", "ic_comprehensive_stats", "ic_get_bad_fits",
            "ic_fit_profiles", "ic_get_diagnostics_f64", "ic_set_delays", "ic_rotate_profiles",
            "ic_set_timing_kernel", "ic_set_option", "ic_get_option", "ic_comprehensive_stats_rowstat",
-           "ic_rccl_unique_id", "ic_session_create_rccl")
+           "ic_rccl_unique_id", "ic_session_create_rccl", "ic_rccl_set_library", "ic_rccl_set_init_timeout")
 
 # session schedule options (ic_set_option; include/iterative_cleaner.h): they
 # choose how the loop is scheduled, never its arithmetic
 OPTIONS = {"fit_tail": 1, "diag_fork": 2, "fork_delay": 3, "template_incr": 4, "fit_tiled": 5,
            "rowstat_waves": 6, "rowstat_minlen": 7, "diag_chain": 8, "sync_timeout_ms": 9,
-           "fit_schedule": 10, "fit_lane_waves": 11, "fit_late_lanes": 12,
-           "tail_split": 13}
-FIT_ROUNDS = 0   # IC_FIT_ROUNDS: sweep / state rounds over compacted lists (k_fit_pass, k_fit_state, k_fit_tail)
-FIT_LANES = 1    # IC_FIT_LANES: one persistent launch, a lane per profile at a time (k_fit_lanes)
+           "fit_schedule": 10, "tail_split": 13}
+FIT_ROUNDS = 0   # IC_FIT_ROUNDS: sweep / state rounds (k_fit_pass, k_fit_state, k_fit_tail); the only schedule
 
 FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)
 FIT_CLOSED = 1   # IC_FIT_CLOSED: closed-form amplitude fused with the diagnostics (fast mode)
@@ -57,8 +55,8 @@ class Params(C.Structure):
 class RunStats(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("fit_rounds", C.c_int32),
                 ("fit_profile_sweeps", C.c_int64), ("fit_tail_sweeps", C.c_int64),
-                ("window_moves", C.c_int32), ("near_threshold", C.c_int32), ("fit_lane_slots", C.c_int64),
-                ("fit_lane_sweeps", C.c_int64)]
+                ("window_moves", C.c_int32), ("near_threshold", C.c_int32), ("reserved0", C.c_int64),
+                ("reserved1", C.c_int64)]
 
 
 class KernelTime(C.Structure):
@@ -152,6 +150,8 @@ def load_library(path: str = LIB_PATH):
     lib.ic_session_create_grouped.argtypes = [C.POINTER(Params), C.c_int, vp, C.c_int, C.POINTER(vp)]
     lib.ic_rccl_unique_id.argtypes = [vp]
     lib.ic_session_create_rccl.argtypes = [C.POINTER(Params), C.c_int, C.c_int, C.c_int, vp, C.POINTER(vp)]
+    lib.ic_rccl_set_library.argtypes = [C.c_char_p]
+    lib.ic_rccl_set_init_timeout.argtypes = [C.c_int64]
     lib.ic_get_bad_fits.argtypes = [vp, vp, C.c_int]
     lib.ic_fit_profiles.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp]
     lib.ic_set_delays.argtypes = [vp, vp]
@@ -371,9 +371,7 @@ class GpuSession:
         return dict(iterations=st.iterations, fit_rounds=st.fit_rounds,
                     fit_profile_sweeps=int(st.fit_profile_sweeps),
                     fit_tail_sweeps=int(st.fit_tail_sweeps),
-                    window_moves=int(st.window_moves), near_threshold=int(st.near_threshold),
-                    fit_lane_slots=int(st.fit_lane_slots),
-                    fit_lane_sweeps=int(st.fit_lane_sweeps))
+                    window_moves=int(st.window_moves), near_threshold=int(st.near_threshold))
 
     def kernel_times(self):
         buf = (KernelTime * 32)()
@@ -494,6 +492,23 @@ def rccl_unique_id() -> bytes:
     if rc != 0:
         raise NativeError("ic_rccl_unique_id: %s (rc=%d)" % (_err(lib), rc))
     return bytes(buf.raw)
+
+
+def rccl_set_library(path):
+    """Load `path` instead of the ROCm install's librccl (ic_rccl_set_library;
+    None = the default).  Process-wide, before the first RCCL use."""
+    lib = load_library()
+    rc = lib.ic_rccl_set_library(None if path is None else os.fsencode(path))
+    if rc != 0:
+        raise NativeError("ic_rccl_set_library: %s (rc=%d)" % (_err(lib), rc))
+
+
+def rccl_set_init_timeout(ms):
+    """How long ic_session_create_rccl waits for every rank to join (ms)."""
+    lib = load_library()
+    rc = lib.ic_rccl_set_init_timeout(int(ms))
+    if rc != 0:
+        raise NativeError("ic_rccl_set_init_timeout: %s (rc=%d)" % (_err(lib), rc))
 
 
 class ShardGroup:

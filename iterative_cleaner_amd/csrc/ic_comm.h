@@ -21,6 +21,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/iterative_cleaner.h"
 
 namespace icgpu {
@@ -38,14 +40,20 @@ public:
     virtual int allreduce_sum_i32(int32_t *buf, size_t n, hipStream_t st) = 0;
     // a failing shard tells its peers (LocalComm: wakes their barriers)
     virtual void abort() {}
+    // the transport lost a peer after the fact (RCCL's asynchronous errors)
+    virtual bool remote_error() { return false; }
 };
 
 Comm *make_callback_comm(const ic_comm_ops &ops, int rank, int world);
 
 // RCCL: 128-byte unique id (rank 0's, handed to every rank); the communicator
 // is created on the current device.  nullptr + message in *err on failure.
-int rccl_unique_id(void *id, const char **err);
-Comm *make_rccl_comm(const void *unique_id, int rank, int world, const char **err);
+int rccl_unique_id(void *id, std::string *err);
+Comm *make_rccl_comm(const void *unique_id, int rank, int world, std::string *err);
+// the librccl file to dlopen (nullptr / "": the ROCm install's), before its first use
+int rccl_set_library(const char *path, const char **err);
+// how long a communicator's creation may wait for every rank to join
+int rccl_set_init_timeout(long long ms, const char **err);
 
 struct LocalGroup;
 LocalGroup *local_group_create(int world);

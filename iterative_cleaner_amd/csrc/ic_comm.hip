@@ -2,9 +2,13 @@
 #include <dlfcn.h>
 #include <string.h>
 
+#include <rccl/rccl.h>
+
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "ic_comm.h"
@@ -249,70 +253,104 @@ Comm *make_local_comm(LocalGroup *g, int rank, int device, const char **err)
 
 // ------------------------------------------------------------ native RCCL
 
-// librccl is opened on first use (dlopen, RTLD_LOCAL, the ROCm install's copy):
-// a process that never asks for the native transport never loads it, and
-// torch's own bundled RCCL, if loaded, stays a separate instance.
+// librccl is opened on first use (dlopen, RTLD_LOCAL): a process that never
+// asks for the native transport never loads it, and torch's own bundled RCCL,
+// if loaded, stays a separate instance.  The ROCm install's copy by default;
+// ic_rccl_set_library() names another file first (a test stub, another RCCL
+// build).  Types and the config layout come from ROCm's rccl.h; no symbol is
+// linked.
 namespace {
-typedef struct ncclComm *nccl_comm_t;
-typedef struct {
-    char internal[128];
-} nccl_id_t;
-enum { kNcclInt8 = 0, kNcclUint8 = 1, kNcclInt32 = 2, kNcclSum = 0 };
 struct RcclApi {
     void *h = nullptr;
-    const char *err = nullptr;
-    int (*GetUniqueId)(nccl_id_t *) = nullptr;
-    int (*CommInitRank)(nccl_comm_t *, int, nccl_id_t, int) = nullptr;
-    int (*CommDestroy)(nccl_comm_t) = nullptr;
-    int (*CommAbort)(nccl_comm_t) = nullptr;
-    int (*AllGather)(const void *, void *, size_t, int, nccl_comm_t, hipStream_t) = nullptr;
-    int (*AllReduce)(const void *, void *, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
-    int (*Send)(const void *, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
-    int (*Recv)(void *, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
-    int (*GroupStart)() = nullptr;
-    int (*GroupEnd)() = nullptr;
-    const char *(*GetErrorString)(int) = nullptr;
+    std::string err;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRankConfig)(ncclComm_t *, int, ncclUniqueId, int, ncclConfig_t *) = nullptr;
+    ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t *) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
 };
 
-RcclApi *rccl_api()
+std::mutex g_rccl_mu;
+RcclApi g_api;
+bool g_api_tried = false;
+std::string g_rccl_path;                 // ic_rccl_set_library ("" = the ROCm install's)
+long long g_init_timeout_ms = 600000;    // ic_rccl_set_init_timeout
+
+RcclApi *rccl_api(std::string *err)
 {
-    static RcclApi api;
-    static std::once_flag once;
-    std::call_once(once, [] {
-        const char *paths[] = {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"};
-        for (const char *p : paths)
-            if ((api.h = dlopen(p, RTLD_NOW | RTLD_LOCAL))) break;
-        if (!api.h) {
-            api.err = "librccl.so.1 not found (dlopen)";
-            return;
-        }
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (!g_api_tried) {
+        g_api_tried = true;
+        std::vector<std::string> paths;
+        if (!g_rccl_path.empty())
+            paths.push_back(g_rccl_path);
+        else
+            paths = {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"};
+        for (const auto &p : paths)
+            if ((g_api.h = dlopen(p.c_str(), RTLD_NOW | RTLD_LOCAL))) break;
+        if (!g_api.h) {
+            g_api.err = "dlopen of " + paths[0] + " failed: " + std::string(dlerror() ? dlerror() : "?");
+        } else {
 #define SYM(F)                                                   \
-    *(void **)(&api.F) = dlsym(api.h, "nccl" #F);                \
-    if (!api.F) {                                                \
-        api.err = "librccl lacks nccl" #F;                       \
-        return;                                                  \
+    if (g_api.err.empty()) {                                     \
+        *(void **)(&g_api.F) = dlsym(g_api.h, "nccl" #F);        \
+        if (!g_api.F) g_api.err = "librccl lacks nccl" #F;       \
     }
-        SYM(GetUniqueId) SYM(CommInitRank) SYM(CommDestroy) SYM(CommAbort) SYM(AllGather) SYM(AllReduce)
-        SYM(Send) SYM(Recv) SYM(GroupStart) SYM(GroupEnd) SYM(GetErrorString)
+            SYM(GetUniqueId) SYM(CommInitRankConfig) SYM(CommGetAsyncError) SYM(CommDestroy) SYM(CommAbort)
+            SYM(AllGather) SYM(AllReduce) SYM(Send) SYM(Recv) SYM(GroupStart) SYM(GroupEnd) SYM(GetErrorString)
 #undef SYM
-    });
-    return api.err ? nullptr : &api;
+        }
+    }
+    if (!g_api.err.empty()) {
+        *err = "librccl unavailable: " + g_api.err;
+        return nullptr;
+    }
+    return &g_api;
 }
 }  // namespace
 
-int rccl_unique_id(void *id, const char **err)
+int rccl_set_library(const char *path, const char **err)
 {
-    RcclApi *a = rccl_api();
-    if (!a) {
-        *err = "librccl unavailable (dlopen of /opt/rocm/lib/librccl.so.1 failed)";
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    const std::string p = path ? path : "";
+    if (g_api_tried && p != g_rccl_path) {
+        *err = "librccl was already loaded by this process (ic_rccl_set_library must come first)";
         return -1;
     }
-    nccl_id_t u;
-    const int rc = a->GetUniqueId(&u);
-    if (rc != 0) {
+    g_rccl_path = p;
+    return 0;
+}
+
+int rccl_set_init_timeout(long long ms, const char **err)
+{
+    if (ms < 1) {
+        *err = "the RCCL init timeout must be >= 1 ms";
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    g_init_timeout_ms = ms;
+    return 0;
+}
+
+int rccl_unique_id(void *id, std::string *err)
+{
+    RcclApi *a = rccl_api(err);
+    if (!a) return -1;
+    ncclUniqueId u;
+    const ncclResult_t rc = a->GetUniqueId(&u);
+    if (rc != ncclSuccess) {
         *err = a->GetErrorString(rc);
         return -1;
     }
+    static_assert(sizeof u == 128, "ncclUniqueId is 128 bytes");
     memcpy(id, &u, sizeof u);
     return 0;
 }
@@ -320,7 +358,11 @@ int rccl_unique_id(void *id, const char **err)
 // One RCCL communicator per shard session, on the session's device; every
 // exchange is issued from here on the session stream (no host callbacks):
 // all-gathers and the counter all-reduce as RCCL collectives, the all-to-alls
-// as one group of per-peer sends and receives.
+// as one group of per-peer sends and receives.  The communicator is
+// non-blocking (config.blocking = 0): its creation is polled under a timeout,
+// so a rank that never joins (it failed before creating its session) makes
+// its peers' creation fail instead of blocking them forever, and a call that
+// returns ncclInProgress is settled by polling ncclCommGetAsyncError.
 class RcclComm final : public Comm {
 public:
     ~RcclComm() override
@@ -339,25 +381,28 @@ public:
     }
     int allgather(const void *send, void *recv, size_t bytes, hipStream_t st) override
     {
-        return check(api->AllGather(send, recv, bytes, kNcclUint8, comm, st));
+        if (!comm) return -1;
+        return check(api->AllGather(send, recv, bytes, ncclUint8, comm, st));
     }
     int alltoallv(const void *send, const size_t *sb, void *recv, const size_t *rb, hipStream_t st) override
     {
-        if (api->GroupStart() != 0) return -1;
+        if (!comm) return -1;
+        if (settle(api->GroupStart()) != ncclSuccess) return check(ncclInternalError);
         size_t so = 0, ro = 0;
-        int rc = 0;
-        for (int p = 0; p < world && rc == 0; ++p) {
-            if (sb[p]) rc = api->Send((const char *)send + so, sb[p], kNcclUint8, p, comm, st);
-            if (rc == 0 && rb[p]) rc = api->Recv((char *)recv + ro, rb[p], kNcclUint8, p, comm, st);
+        ncclResult_t rc = ncclSuccess;
+        for (int p = 0; p < world && rc == ncclSuccess; ++p) {
+            if (sb[p]) rc = api->Send((const char *)send + so, sb[p], ncclUint8, p, comm, st);
+            if (rc == ncclSuccess && rb[p]) rc = api->Recv((char *)recv + ro, rb[p], ncclUint8, p, comm, st);
             so += sb[p];
             ro += rb[p];
         }
-        const int rc2 = api->GroupEnd();
-        return check(rc ? rc : rc2);
+        const ncclResult_t rc2 = api->GroupEnd();
+        return check(rc != ncclSuccess && rc != ncclInProgress ? rc : rc2);
     }
     int allreduce_sum_i32(int32_t *buf, size_t n, hipStream_t st) override
     {
-        return check(api->AllReduce(buf, buf, n, kNcclInt32, kNcclSum, comm, st));
+        if (!comm) return -1;
+        return check(api->AllReduce(buf, buf, n, ncclInt32, ncclSum, comm, st));
     }
     void abort() override
     {
@@ -367,38 +412,83 @@ public:
             comm = nullptr;
         }
     }
+    // a failure RCCL detected asynchronously (a peer's connection lost): the
+    // session's host waits poll this between their event queries
+    bool remote_error() override
+    {
+        if (!comm) return aborted;
+        ncclResult_t st = ncclSuccess;
+        if (api->CommGetAsyncError(comm, &st) != ncclSuccess) return true;
+        return st != ncclSuccess && st != ncclInProgress;
+    }
 
 private:
     RcclApi *api = nullptr;
-    nccl_comm_t comm = nullptr;
+    ncclComm_t comm = nullptr;
     bool aborted = false;
-    int check(int rc)
+    // a non-blocking communicator's call may return ncclInProgress: wait for
+    // its state to settle (enqueueing on the stream takes microseconds)
+    ncclResult_t settle(ncclResult_t rc)
     {
-        if (rc != 0) abort();
-        return rc == 0 ? 0 : -1;
+        if (rc != ncclInProgress) return rc;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            ncclResult_t st = ncclSuccess;
+            if (api->CommGetAsyncError(comm, &st) != ncclSuccess) return ncclInternalError;
+            if (st != ncclInProgress) return st;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return ncclInternalError;
+            std::this_thread::yield();
+        }
     }
-    friend Comm *make_rccl_comm(const void *, int, int, const char **);
+    int check(ncclResult_t rc)
+    {
+        rc = settle(rc);
+        if (rc != ncclSuccess) abort();
+        return rc == ncclSuccess ? 0 : -1;
+    }
+    friend Comm *make_rccl_comm(const void *, int, int, std::string *);
 };
 
-Comm *make_rccl_comm(const void *unique_id, int rank, int world, const char **err)
+Comm *make_rccl_comm(const void *unique_id, int rank, int world, std::string *err)
 {
-    RcclApi *a = rccl_api();
-    if (!a) {
-        *err = "librccl unavailable (dlopen of /opt/rocm/lib/librccl.so.1 failed)";
-        return nullptr;
+    RcclApi *a = rccl_api(err);
+    if (!a) return nullptr;
+    long long timeout_ms;
+    {
+        std::lock_guard<std::mutex> lk(g_rccl_mu);
+        timeout_ms = g_init_timeout_ms;
     }
-    nccl_id_t u;
+    ncclUniqueId u;
     memcpy(&u, unique_id, sizeof u);
     auto *c = new RcclComm();
     c->api = a;
     c->rank = rank;
     c->world = world;
-    const int rc = a->CommInitRank(&c->comm, world, u, rank);   // on the current (session) device
-    if (rc != 0) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t rc = a->CommInitRankConfig(&c->comm, world, u, rank, &cfg);   // on the current (session) device
+    if (rc != ncclSuccess && rc != ncclInProgress) {
+        *err = std::string("ncclCommInitRankConfig: ") + a->GetErrorString(rc);
+        if (c->comm) (void)a->CommAbort(c->comm);
         c->comm = nullptr;
-        *err = a->GetErrorString(rc);
         delete c;
         return nullptr;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        rc = a->CommGetAsyncError(c->comm, &st);
+        if (rc == ncclSuccess && st == ncclSuccess) break;
+        const bool timed_out = std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms);
+        if (rc != ncclSuccess || st != ncclInProgress || timed_out) {
+            *err = timed_out ? "RCCL communicator init timed out (a rank did not join; ic_rccl_set_init_timeout)"
+                             : std::string("RCCL communicator init: ") + a->GetErrorString(rc != ncclSuccess ? rc : st);
+            (void)a->CommAbort(c->comm);
+            c->comm = nullptr;
+            delete c;
+            return nullptr;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
     return c;
 }

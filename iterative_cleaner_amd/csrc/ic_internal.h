@@ -105,7 +105,6 @@ enum KernelId {
     K_EXCHANGE,       // the collectives themselves (host transport or peer copies)
     K_TNORM,          // fit_mode 1: sum(T*T)
     K_ROTATE,         // fractional dedispersion (FFT phase rotation)
-    K_FIT_LANES,      // the exact fit as one persistent launch (IC_FIT_LANES)
     K_COUNT
 };
 
@@ -215,34 +214,16 @@ hipError_t launch_mark_list(hipStream_t st, const int32_t *list, const unsigned 
                             uint8_t *m, uint8_t v);
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
-                           const FitStateArrays &S);
+                           const FitStateArrays &S, bool round0);
 // ctr: zeroed device word, packed [63:32] B survivors, [31:0] A survivors
 // (the next round's nctr); done: zeroed word counting the finished blocks;
-// host_n: host-mapped int the last block writes the survivor total to
+// host_n: host-mapped int the last block writes the survivor total to.
+// round0 (launch_fit_pass): the first round (list == nullptr: every profile
+// at x = 1, the fused first B sweep).
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,
                             const unsigned long long *nctr, long bound, double *amp, int32_t *info,
                             int32_t *next_list, unsigned long long *ctr, unsigned *done, int32_t *host_n,
                             uint8_t *late = nullptr);
-// The whole exact fit in one persistent launch (k_fit_lanes): `waves` waves of
-// 64 lanes, each lane taking profiles from *qhead (zeroed) until P are taken.
-// ls: lmdif state of the lane slots, kLaneFieldsMax f64 fields of `lst` >=
-// waves * 64 slots; U: k_fit_prep's shared qrfac; dummy_row: a zero row of D
-// (waiting lanes' DMA reads it); sweeps[0] += the profile sweeps made,
-// sweeps[1] += 64 x the wave sweeps (lane slots swept, waiting lanes included).
-// phase 0: to completion; 1: until the queue runs out, then every profile in
-// flight is saved in its slot, flagged in late[] and appended to flist (count
-// in *fctr, RoundList's packed form: nA = count); 2: resume those to completion;
-// 3: the queue runs over a round list (list, nctr; at most `bound` entries),
-// every profile resumed from the state k_fit_state left in *S.
-constexpr int kLaneFieldsMax = 25;
-hipError_t launch_fit_lanes(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                            int dtiled, int dummy_row, int waves, double *ls, long lst, const double *U,
-                            unsigned *qhead, double *amp, int32_t *info, unsigned long long *sweeps, int phase = 0,
-                            uint8_t *late = nullptr, int32_t *flist = nullptr, unsigned long long *fctr = nullptr,
-                            const FitStateArrays *S = nullptr, const int32_t *list = nullptr,
-                            const unsigned long long *nctr = nullptr, long bound = 0);
-// waves of k_fit_lanes resident at once on `device` (occupancy x CUs), 0 on error
-int fit_lanes_max_waves(int device);
 hipError_t launch_fit_tail(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
                            const FitStateArrays &S, double *amp, int32_t *info, unsigned long long *sweeps);

@@ -1474,115 +1474,6 @@ __device__ __forceinline__ void fast_sweep(const DmaTiles &d, int ldD, const Pas
     out.jt = FUSE && body.jt && !out.bad;
 }
 
-// Unified sweep body (k_fit_lanes): every lane evaluates f and J at ITS point
-// x, both norms (what an A request needs) and the dot sum_i RN(Jn_i f_i) with
-// Jn_i = RN(J_i / aj) (+1 at i = 0) at ITS aj (what a B request needs; an A
-// request at x = 1 takes k_fit_prep's shared aj: the fused first B sweep, with
-// jt = (J_i == T_i for every i)).  So one sweep answers every lane whatever it
-// requested.  Per lane the operations are exactly FastBody's for its request
-// (at x = 1: 1 t = t, (1 + 2^-26) t, and mdiv by 2^-26 = the exact scaling
-// FastBody<FUSE> writes as d 2^26).
-struct UniIn {
-    double x, h, xh, yh, yl;   // the lane's point (A: xa; B: x), h = eps |x| (eps if 0)
-    double aj, yaj, ylj;       // the dot's divisor (B: the lane's aj; A at x = 1: k_fit_prep's)
-};
-
-struct UniBody {
-    static constexpr bool kPeel = true;
-    const UniIn &in;
-    const double *__restrict__ T64;
-    FastAcc fF, fJ;
-    double fa0, Ja0, sum;
-    int lo_ok;
-    bool jt;
-
-    __device__ __forceinline__ UniBody(const UniIn &i, const double *T) : in(i), T64(T)
-    {
-        fa_zero(fF);
-        fa_zero(fJ);
-        fa0 = Ja0 = sum = 0.0;
-        lo_ok = 1;
-        jt = true;
-    }
-    __device__ __forceinline__ void checked()
-    {
-        const uint32_t hr1 = (uint32_t)((unsigned long long)__double_as_longlong(kRdwarf * kRdwarf) >> 32) + 1u;
-        lo_ok = (fa_lo_ok(fF, hr1) && fa_lo_ok(fJ, hr1)) ? 1 : 0;
-        asm volatile("" : "+v"(lo_ok));
-    }
-    __device__ __forceinline__ void fence()
-    {
-        asm volatile("" : "+v"(fF.s2), "+v"(fJ.s2), "+v"(sum), "+v"(fF.minhm1), "+v"(fJ.minhm1));
-    }
-    double tv[FIT_TB];
-    __device__ __forceinline__ void load_T(int b0)
-    {
-#pragma unroll
-        for (int i = 0; i < FIT_TB; ++i) tv[i] = T64[b0 + i];
-    }
-    template <bool CHK>
-    __device__ __forceinline__ void group4(const double (&t)[4], const fv4 &pv4, bool first)
-    {
-        const float pf[4] = {pv4.x, pv4.y, pv4.z, pv4.w};
-        double p[4], f[4], d[4], q[4], r[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) p[k] = (double)pf[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f[k] = in.x * t[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = in.xh * t[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f[k] = f[k] - p[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = d[k] - p[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = d[k] - f[k];
-        // J = mdiv(d, h, yh, yl)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = d[k] * in.yl;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = fma(d[k], in.yh, q[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) r[k] = fma(-in.h, q[k], d[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = fma(r[k], in.yh, q[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            fa_add<CHK>(fF, f[k]);
-            fa_add<CHK>(fJ, q[k]);
-        }
-        if (first) {
-            fa0 = f[0];
-            Ja0 = q[0];
-        }
-        // Jn = mdiv(J, aj, yaj, ylj) (+1 on sample 0), the dot in sample order
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = q[k] * in.ylj;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = fma(q[k], in.yaj, d[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) r[k] = fma(-in.aj, d[k], q[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = fma(r[k], in.yaj, d[k]);
-        if (first) d[0] = d[0] + 1.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            jt = jt && (q[k] == t[k]);
-            d[k] = d[k] * f[k];
-            sum = sum + d[k];
-        }
-    }
-    template <bool CHK>
-    __device__ __forceinline__ void run(int b0, const fv4 (&v)[4])
-    {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const double t4[4] = {tv[4 * c], tv[4 * c + 1], tv[4 * c + 2], tv[4 * c + 3]};
-            group4<CHK>(t4, v[c], CHK && c == 0 && b0 == 0);
-        }
-    }
-};
-
 // ---- split lmdif: state machine (k_fit_state) <-> data sweeps (k_fit_pass) ----
 // Per-profile state lives in HBM as structure-of-arrays (FitState below);
 // a round is one k_fit_pass (every profile with a pending request reads its
@@ -1795,6 +1686,84 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     if (reqB) S.o_sum[k] = o.sum;
 }
 
+// One profile's MINPACK transition after its sweep (k_fit_state): request
+// st, the sweep's results from o (OutS: k_fit_pass's o_* fields), the lmdif
+// state read from and written to S; returns the next request (ST_DONE: amp /
+// info written).
+struct OutS {
+    const FitStateArrays &S;
+    long k;
+    __device__ __forceinline__ double fnorm() const { return S.o_fnorm[k]; }
+    __device__ __forceinline__ double acnorm() const { return S.o_acnorm[k]; }
+    __device__ __forceinline__ double f0() const { return S.o_f0[k]; }
+    __device__ __forceinline__ double J0() const { return S.o_J0[k]; }
+    __device__ __forceinline__ double sum() const { return S.o_sum[k]; }
+    __device__ __forceinline__ int exact() const { return S.o_exact[k]; }
+};
+template <typename Out>
+__device__ __forceinline__ int fit_transition(const FitStateArrays &S, long k, int st, const Out &o,
+                                              double *__restrict__ amp_o, int32_t *__restrict__ info_o)
+{
+    LmState L;
+    if (st == ST_B) {
+        // after a B sweep only qtf and the inner-loop start change: read the
+        // fields lm_after_b / lm_after_qtf / lm_start_inner use, write the
+        // ones they set (half the state traffic of a full load/store)
+        L.Jn0 = S.Jn0[k]; L.f0 = S.f0[k]; L.fnorm = S.fnorm[k]; L.acnorm = S.acnorm[k]; L.r = S.r[k];
+        L.diag = S.diag[k]; L.delta = S.delta[k]; L.par = S.par[k]; L.x = S.x[k]; L.iter = S.iter[k];
+        L.info = 0;
+        st = lm_after_b(L, o.sum());
+        S.qtf[k] = L.qtf; S.gnorm[k] = L.gnorm; S.diag[k] = L.diag; S.par[k] = L.par;
+        S.delta[k] = L.delta; S.wa1[k] = L.wa1; S.x2[k] = L.x2; S.pnorm[k] = L.pnorm;
+    } else if (st == ST_A0) {
+        // the first transition: the state is k_fit_init's (x = 1, par = 0,
+        // iter = 1) and lm_outer reads nothing else; on the usual way out (a B
+        // request) only the fields it set are written
+        L.x = 1.0; L.par = 0.0; L.iter = 1; L.info = 0;
+        L.acn2 = 0.0; L.J02 = 0.0; L.f02 = 0.0;
+        L.fnorm = o.fnorm();
+        L.nfev = 1;
+        L.acnorm = o.acnorm();
+        L.f0 = o.f0();
+        L.J0 = o.J0();
+        const int oe = o.exact();
+        S.slow[k] = oe & 1;
+        st = lm_outer(L);
+        // J(1) == T and the same qrfac as k_fit_prep's: the round-0 sweep
+        // already summed qtf's dot, so the B request is answered here
+        if (st == ST_B && (oe & 2) && S.U[0] != 0.0 && L.acnorm == S.U[1] && L.aj == S.U[2] &&
+            L.Jn0 == S.U[3]) {
+            st = lm_after_b(L, o.sum());
+            lm_store(L, S, k);
+        } else if (st == ST_B) {
+            S.fnorm[k] = L.fnorm; S.nfev[k] = L.nfev; S.acnorm[k] = L.acnorm; S.f0[k] = L.f0;
+            S.J0[k] = L.J0; S.Jn0[k] = L.Jn0; S.aj[k] = L.aj; S.r[k] = L.r; S.diag[k] = L.diag;
+            S.xnorm[k] = L.xnorm; S.delta[k] = L.delta;
+        } else {
+            lm_store(L, S, k);
+        }
+    } else if (st != ST_DONE) {
+        lm_load(L, S, k);
+        if (st == ST_A2) {
+            L.acn2 = o.acnorm();
+            L.f02 = o.f0();
+            L.J02 = o.J0();
+            st = lm_after_a2(L, o.fnorm());
+            if (L.x == L.x2) S.slow[k] = o.exact() & 1;
+        }
+        lm_store(L, S, k);
+    } else {
+        return ST_DONE;
+    }
+    S.mode[k] = st;
+    if (st == ST_A2) S.xa[k] = L.x2;
+    if (st == ST_DONE) {
+        amp_o[k] = L.x;
+        info_o[k] = L.info;
+    }
+    return st;
+}
+
 // Consume the sweep result, run lmdif's scalar logic to the next request.
 // Survivors (profiles still needing a sweep) are appended to next_list;
 // *next_n counts them (order within the list is irrelevant: profiles are
@@ -1837,82 +1806,8 @@ __global__ __launch_bounds__(BS) void k_fit_state(FitStateArrays S, long P, cons
     long k = 0;
     if (slot < nact) {
         k = rl.at(slot);
-        int st = S.mode[k];
-        if (st == ST_B) {
-            // after a B sweep only qtf and the inner-loop start change: read the
-            // fields lm_after_b / lm_after_qtf / lm_start_inner use, write the
-            // ones they set (half the state traffic of a full load/store)
-            LmState L;
-            L.Jn0 = S.Jn0[k]; L.f0 = S.f0[k]; L.fnorm = S.fnorm[k]; L.acnorm = S.acnorm[k]; L.r = S.r[k];
-            L.diag = S.diag[k]; L.delta = S.delta[k]; L.par = S.par[k]; L.x = S.x[k]; L.iter = S.iter[k];
-            L.info = 0;
-            st = lm_after_b(L, S.o_sum[k]);
-            S.qtf[k] = L.qtf; S.gnorm[k] = L.gnorm; S.diag[k] = L.diag; S.par[k] = L.par;
-            S.delta[k] = L.delta; S.wa1[k] = L.wa1; S.x2[k] = L.x2; S.pnorm[k] = L.pnorm;
-            S.mode[k] = st;
-            if (st == ST_A2) S.xa[k] = L.x2;
-            if (st == ST_DONE) {
-                amp_o[k] = L.x;
-                info_o[k] = L.info;
-            } else {
-                still = st == ST_B ? 2 : 1;   // B requests go to the list's end
-            }
-        } else if (st == ST_A0) {
-            // the first transition: the state is k_fit_init's (x = 1, par = 0,
-            // iter = 1) and lm_outer reads nothing else; on the usual way out (a B
-            // request) only the fields it set are written
-            LmState L;
-            L.x = 1.0; L.par = 0.0; L.iter = 1; L.info = 0;
-            L.acn2 = 0.0; L.J02 = 0.0; L.f02 = 0.0;
-            L.fnorm = S.o_fnorm[k];
-            L.nfev = 1;
-            L.acnorm = S.o_acnorm[k];
-            L.f0 = S.o_f0[k];
-            L.J0 = S.o_J0[k];
-            const int oe = S.o_exact[k];
-            S.slow[k] = oe & 1;
-            st = lm_outer(L);
-            // J(1) == T and the same qrfac as k_fit_prep's: the round-0 sweep
-            // already summed qtf's dot, so the B request is answered here
-            if (st == ST_B && (oe & 2) && S.U[0] != 0.0 && L.acnorm == S.U[1] && L.aj == S.U[2] &&
-                L.Jn0 == S.U[3]) {
-                st = lm_after_b(L, S.o_sum[k]);
-                lm_store(L, S, k);
-            } else if (st == ST_B) {
-                S.fnorm[k] = L.fnorm; S.nfev[k] = L.nfev; S.acnorm[k] = L.acnorm; S.f0[k] = L.f0;
-                S.J0[k] = L.J0; S.Jn0[k] = L.Jn0; S.aj[k] = L.aj; S.r[k] = L.r; S.diag[k] = L.diag;
-                S.xnorm[k] = L.xnorm; S.delta[k] = L.delta;
-            } else {
-                lm_store(L, S, k);
-            }
-            S.mode[k] = st;
-            if (st == ST_A2) S.xa[k] = L.x2;
-            if (st == ST_DONE) {
-                amp_o[k] = L.x;
-                info_o[k] = L.info;
-            } else {
-                still = st == ST_B ? 2 : 1;   // B requests go to the list's end
-            }
-        } else if (st != ST_DONE) {
-            LmState L;
-            lm_load(L, S, k);
-            if (st == ST_A2) {
-                L.acn2 = S.o_acnorm[k];
-                L.f02 = S.o_f0[k];
-                L.J02 = S.o_J0[k];
-                st = lm_after_a2(L, S.o_fnorm[k]);
-                if (L.x == L.x2) S.slow[k] = S.o_exact[k] & 1;
-            }
-            lm_store(L, S, k);
-            S.mode[k] = st;
-            if (st == ST_A2) S.xa[k] = L.x2;
-            if (st == ST_DONE) {
-                amp_o[k] = L.x;
-                info_o[k] = L.info;
-            } else {
-                still = st == ST_B ? 2 : 1;   // B requests go to the list's end
-            }
-        }
+        const int st = fit_transition(S, k, S.mode[k], OutS{S, k}, amp_o, info_o);
+        if (st != ST_DONE) still = st == ST_B ? 2 : 1;   // B requests go to the list's end
     }
     if (late && still) late[k] = 1;   // the fork round: still fitting after it
     // block-aggregated append, partitioned by request (RoundList)
@@ -1950,6 +1845,9 @@ __global__ __launch_bounds__(BS) void k_fit_state(FitStateArrays S, long P, cons
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned fin = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (fin == (unsigned)nblk - 1) {
+            // (the last block only: an acquire orders its load of ctr after every
+            // block's offset atomic in the memory model too, not just on the hardware)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const unsigned long long v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(host_n, (int32_t)((v & 0xffffffffull) + (v >> 32)), __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2226,317 +2124,6 @@ __global__ __launch_bounds__(64 * TAIL_WAVES, IC_TAIL_MINW) void k_fit_tail(cons
         }
     }
     if (lane == 0 && nsw) atomicAdd(sweeps, nsw);
-}
-
-// ---- persistent lanes: the whole fit in one launch ---------------------------
-// Every lane is a worker that runs scipy's lmdif for one profile at a time to
-// completion (the same MINPACK transitions as k_fit_state, the same sweep
-// bodies as k_fit_pass), and takes the next profile from a shared queue the
-// moment it finishes: no rounds, no lists, no per-round launches, and a
-// profile's sweeps follow each other while its row is recent in the caches.
-// A wave runs one sweep body at a time (A at x = 1 with the fused dot, A, or
-// B), the one most of its lanes request; the others wait a sweep (their DMA
-// reads a zero row) and most of the time catch up in step, since every lane
-// alternates A and B requests.  The lmdif state of a lane lives in S indexed
-// by the lane (coalesced), read and written around each transition only.
-// Empty lanes refill at the top of each step: one queue atomic per wave and
-// step.  Bits are those of the round schedule (same operations per profile).
-enum { LN_EMPTY = 4 };
-
-__device__ __forceinline__ int lane_row_of(int row, int src)
-{
-    return __builtin_amdgcn_ds_bpermute(src << 2, row);
-}
-
-// lmdif state of a lane slot: kLaneFieldsMax f64 fields, field f of slot g at
-// ls[f * stride + g] (a wave's field is one coalesced 512-B access): 0-18 the
-// LmState (ln_load), then what phase 1 leaves for phase 2 (k < 0: none)
-enum { kLaneK = 19, kLaneSt, kLaneXa, kLaneXb, kLaneAjb, kLaneSlow };
-__device__ __forceinline__ void ln_load(LmState &L, const double *ls, long st, long g)
-{
-    L.x = ls[0 * st + g]; L.fnorm = ls[1 * st + g]; L.par = ls[2 * st + g]; L.delta = ls[3 * st + g];
-    L.diag = ls[4 * st + g]; L.xnorm = ls[5 * st + g]; L.acnorm = ls[6 * st + g]; L.J0 = ls[7 * st + g];
-    L.f0 = ls[8 * st + g]; L.aj = ls[9 * st + g]; L.r = ls[10 * st + g]; L.Jn0 = ls[11 * st + g];
-    L.qtf = ls[12 * st + g]; L.gnorm = ls[13 * st + g]; L.x2 = ls[14 * st + g]; L.pnorm = ls[15 * st + g];
-    L.wa1 = ls[16 * st + g];
-    L.iter = (int)ls[17 * st + g]; L.nfev = (int)ls[18 * st + g];
-    L.info = 0;
-    L.acn2 = 0.0; L.J02 = 0.0; L.f02 = 0.0;
-}
-
-__device__ __forceinline__ void ln_store(const LmState &L, double *ls, long st, long g)
-{
-    ls[0 * st + g] = L.x; ls[1 * st + g] = L.fnorm; ls[2 * st + g] = L.par; ls[3 * st + g] = L.delta;
-    ls[4 * st + g] = L.diag; ls[5 * st + g] = L.xnorm; ls[6 * st + g] = L.acnorm; ls[7 * st + g] = L.J0;
-    ls[8 * st + g] = L.f0; ls[9 * st + g] = L.aj; ls[10 * st + g] = L.r; ls[11 * st + g] = L.Jn0;
-    ls[12 * st + g] = L.qtf; ls[13 * st + g] = L.gnorm; ls[14 * st + g] = L.x2; ls[15 * st + g] = L.pnorm;
-    ls[16 * st + g] = L.wa1;
-    ls[17 * st + g] = (double)L.iter; ls[18 * st + g] = (double)L.nfev;
-}
-
-struct LaneNext {
-    double xa, xb, ajb;
-    int st, slow;
-};
-
-// One lane's MINPACK transition after a sweep of kind `body` (k_fit_state's,
-// per request kind), its state read from / written to its slot.  Not inlined:
-// MINPACK's scalar logic would otherwise share the sweep's register budget.
-__device__ __attribute__((noinline)) LaneNext lane_transition(double *ls, long lst, long g, int k, int body,
-                                                             double fnorm, double acnorm, double f0, double J0,
-                                                             double sum, int jt, int exA, int slow,
-                                                             const double *U, double *amp_o, int32_t *info_o)
-{
-    LmState L;
-    int st;
-    if (body == ST_A0) {
-        L.x = 1.0; L.par = 0.0; L.iter = 1; L.info = 0;
-        L.acn2 = 0.0; L.J02 = 0.0; L.f02 = 0.0;
-        L.fnorm = fnorm;
-        L.nfev = 1;
-        L.acnorm = acnorm;
-        L.f0 = f0;
-        L.J0 = J0;
-        slow = exA;
-        st = lm_outer(L);
-        if (st == ST_B && jt && U[0] != 0.0 && L.acnorm == U[1] && L.aj == U[2] && L.Jn0 == U[3])
-            st = lm_after_b(L, sum);
-    } else if (body == ST_B) {
-        ln_load(L, ls, lst, g);
-        st = lm_after_b(L, sum);
-    } else {
-        ln_load(L, ls, lst, g);
-        L.acn2 = acnorm;
-        L.f02 = f0;
-        L.J02 = J0;
-        st = lm_after_a2(L, fnorm);
-        if (L.x == L.x2) slow = exA;
-    }
-    LaneNext nx;
-    nx.st = st;
-    nx.slow = slow;
-    nx.xa = L.x2;
-    nx.xb = L.x;
-    nx.ajb = L.aj;
-    if (st == ST_DONE) {
-        amp_o[k] = L.x;
-        info_o[k] = L.info;
-        nx.st = LN_EMPTY;
-    } else {
-        ln_store(L, ls, lst, g);
-    }
-    return nx;
-}
-
-#ifndef IC_LANE_MINW
-#define IC_LANE_MINW 3   // waves per SIMD the register allocation must allow
-#endif
-__global__ __launch_bounds__(64, IC_LANE_MINW) void k_fit_lanes(const float *__restrict__ D, const double *__restrict__ T64,
-                                                  long P, int nbin, int ldD, int nsw, int dtiled, int dummy_row,
-                                                  double *__restrict__ ls, long lst, const double *__restrict__ U,
-                                                  unsigned *__restrict__ qhead, double *__restrict__ amp_o,
-                                                  int32_t *__restrict__ info_o,
-                                                  unsigned long long *__restrict__ sweeps, int phase,
-                                                  uint8_t *__restrict__ late, int32_t *__restrict__ flist,
-                                                  unsigned long long *__restrict__ fctr, FitStateArrays S,
-                                                  const int32_t *__restrict__ list,
-                                                  const unsigned long long *__restrict__ nctr)
-{
-    __shared__ __attribute__((aligned(16))) char lbuf[2 * FIT_BUF];
-    const int lane = threadIdx.x;
-    const long g = (long)blockIdx.x * 64 + lane;   // this lane's slot in S
-    const double agiant = kRgiant / (double)nbin;
-    const double eps = sqrt(DBL_EPSILON);
-    const double U2 = U[2];
-    int k = 0;              // the lane's profile
-    int st = LN_EMPTY;      // its request (ST_A0, ST_A2, ST_B) or LN_EMPTY
-    double xa = 1.0;        // A request: the trial point
-    double xb = 1.0, ajb = 1.0;   // B request: x and the signed Jacobian norm
-    int slow = 0;           // J at x came from an exact sweep: the B sweep is exact too
-    bool qdone = false;     // the queue is exhausted (wave-uniform)
-    unsigned long long nsweeps = 0, nslots = 0;
-    // phase 3: the queue runs over a round list (the profiles still fitting
-    // after the rounds), each taken with the state k_fit_state left in S
-    const RoundList rl(phase == 3 ? list : nullptr, nctr, P);
-    const long nq = rl.n();
-    if (phase == 2) {   // resume the profiles phase 1 left in flight in these slots
-        const double sk = ls[kLaneK * lst + g];
-        if (sk >= 0.0) {
-            k = (int)sk;
-            st = (int)ls[kLaneSt * lst + g];
-            xa = ls[kLaneXa * lst + g];
-            xb = ls[kLaneXb * lst + g];
-            ajb = ls[kLaneAjb * lst + g];
-            slow = (int)ls[kLaneSlow * lst + g];
-        }
-        qdone = true;
-    }
-    DmaTiles dt;
-    dt.lds = lbuf;
-    dt.tiled = dtiled;
-    {
-        const uint32_t base = lds_u32(lbuf) + 16u * (uint32_t)(64 * (lane >> 4) + 4 * (lane & 15));
-        const int gq = (lane >> 2) & 3;
-#pragma unroll
-        for (int c2 = 0; c2 < 4; ++c2) dt.rd[c2] = base + 16u * (uint32_t)(c2 ^ gq);
-    }
-    const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
-    for (;;) {
-        if (!qdone) {   // refill the empty lanes from the queue (one atomic per wave)
-            const bool emp = st == LN_EMPTY;
-            const unsigned long long m = __ballot(emp);
-            if (m) {
-                const unsigned nfree = (unsigned)__popcll(m);
-                unsigned base = 0;
-                if (lane == 0) base = atomicAdd(qhead, nfree);
-                base = __builtin_amdgcn_readfirstlane(base);
-                if ((long)base + nfree >= nq) qdone = true;
-                if (phase == 1 && qdone) {
-                    // the queue ran out: leave every profile in flight to phase 2
-                    // (saved in the slot), flagged for the second diagnostics pass
-                    // and listed for it
-                    const long kk = (long)base + __popcll(m & ((1ull << lane) - 1ull));
-                    if (emp && kk < P) {
-                        k = (int)kk;
-                        st = ST_A0;
-                        xa = 1.0;
-                        slow = 0;
-                    }
-                    const bool fly = st != LN_EMPTY;
-                    ls[kLaneK * lst + g] = fly ? (double)k : -1.0;
-                    if (fly) {
-                        ls[kLaneSt * lst + g] = (double)st;
-                        ls[kLaneXa * lst + g] = xa;
-                        ls[kLaneXb * lst + g] = xb;
-                        ls[kLaneAjb * lst + g] = ajb;
-                        ls[kLaneSlow * lst + g] = (double)slow;
-                        late[k] = 1;
-                    }
-                    const unsigned long long mf = __ballot(fly);
-                    unsigned fb = 0;
-                    if (lane == 0 && mf) fb = (unsigned)atomicAdd(fctr, (unsigned long long)__popcll(mf));
-                    fb = __builtin_amdgcn_readfirstlane(fb);
-                    if (fly) flist[fb + __popcll(mf & ((1ull << lane) - 1ull))] = k;
-                    break;
-                }
-                if (emp) {
-                    const long kk = (long)base + __popcll(m & ((1ull << lane) - 1ull));
-                    if (kk < nq && phase == 3) {   // resume a profile the rounds left
-                        k = (int)rl.at(kk);
-                        st = S.mode[k];
-                        xa = S.xa[k];
-                        xb = S.x[k];
-                        ajb = S.aj[k];
-                        slow = S.slow[k];
-                        const double *f17[17] = {S.x, S.fnorm, S.par, S.delta, S.diag, S.xnorm, S.acnorm, S.J0, S.f0,
-                                                 S.aj, S.r, S.Jn0, S.qtf, S.gnorm, S.x2, S.pnorm, S.wa1};
-#pragma unroll
-                        for (int f = 0; f < 17; ++f) ls[f * lst + g] = f17[f][k];
-                        ls[17 * lst + g] = (double)S.iter[k];
-                        ls[18 * lst + g] = (double)S.nfev[k];
-                    } else if (kk < nq) {
-                        k = (int)kk;
-                        st = ST_A0;
-                        xa = 1.0;
-                        slow = 0;
-                    }
-                }
-            }
-        }
-        const bool part = st != LN_EMPTY;
-        const int cnt = __popcll(__ballot(part));
-        if (cnt == 0) {
-            if (qdone) break;
-            continue;
-        }
-        nsweeps += (unsigned long long)cnt;
-        nslots += 64;
-        // DMA sources: instruction m, lane l fetches chunk `chunk` of slot 16m + l/4's
-        // row (k_fit_pass's source-side transpose); empty lanes read a zero row
-        const int myrow = part ? k : dummy_row;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int kr = lane_row_of(myrow, m * 16 + (lane >> 2));
-            dt.src[m] = D + d_ofs((size_t)kr, 4 * chunk, ldD, dtiled);
-        }
-        const bool isA = st == ST_A0 || st == ST_A2;
-        const bool isB = st == ST_B;
-        UniIn ui;
-        ui.x = isA ? xa : (isB ? xb : 1.0);
-        ui.h = eps * fabs(ui.x);
-        if (ui.h == 0.0) ui.h = eps;
-        ui.xh = ui.x + ui.h;
-        ui.yh = 1.0 / ui.h;
-        ui.yl = recip_lo(ui.h, ui.yh);
-        ui.aj = isB ? ajb : (st == ST_A0 ? U2 : 1.0);
-        ui.yaj = 1.0 / ui.aj;
-        ui.ylj = recip_lo(ui.aj, ui.yaj);
-        const bool fastA = isA && x_in_sq_range(ui.x);
-        const bool fastB = isB && !slow && x_in_fast_range(ui.x) && x_in_fast_range(ui.aj);
-        PassOut o;
-        o.jt = false;
-        o.fnorm = o.acnorm = o.f0 = o.J0 = o.sum = 0.0;
-        bool bad = false;
-        if (__any(fastA || fastB)) {
-            UniBody ub(ui, T64);
-            sweep_dma(dt, nsw, ub);
-            const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant * agiant) >> 32);
-            o.f0 = ub.fa0;
-            o.J0 = ub.Ja0;
-            o.sum = ub.sum;
-            o.fnorm = fa_fin(ub.fF);
-            o.acnorm = fa_fin(ub.fJ);
-            bad = isA && !(ub.lo_ok && fa_hi_ok(ub.fF, hg) && fa_hi_ok(ub.fJ, hg));
-            // the fused dot counts only where J stayed in the verified range
-            o.jt = st == ST_A0 && ub.jt && !bad;
-        }
-        // the exact path for the lanes outside the fast path's verified ranges
-        const bool exA = isA && (!fastA || bad);
-        const bool exB = isB && !fastB;
-        if (__any(exA || exB)) {
-            PassIn ie;
-            ie.A = exA;
-            ie.B = exB;
-            ie.xa = exA ? ui.x : 1.0;
-            ie.ha = exA ? ui.h : eps;
-            ie.xha = ie.xa + ie.ha;
-            ie.yha = 1.0 / ie.ha;
-            ie.yla = recip_lo(ie.ha, ie.yha);
-            ie.xb = exB ? ui.x : 1.0;
-            ie.hb = exB ? ui.h : eps;
-            ie.xhb = ie.xb + ie.hb;
-            ie.yhb = 1.0 / ie.hb;
-            ie.ylb = recip_lo(ie.hb, ie.yhb);
-            ie.ajb = exB ? ui.aj : 1.0;
-            ie.yaj = 1.0 / ie.ajb;
-            ie.ylj = recip_lo(ie.ajb, ie.yaj);
-            ExactBody eb(ie, T64, agiant);
-            sweep_dma(dt, nsw, eb);
-            if (exA || exB) {
-                o.f0 = eb.fa0;
-                o.J0 = eb.Ja0;
-                o.sum = eb.sum;
-                o.fnorm = en_fin(eb.eF);
-                o.acnorm = en_fin(eb.eJ);
-            }
-        }
-        const int body = st;
-        if (part) {   // the lane's MINPACK transition
-            const LaneNext nx = lane_transition(ls, lst, g, k, body, o.fnorm, o.acnorm, o.f0, o.J0, o.sum,
-                                                o.jt ? 1 : 0, exA ? 1 : 0, slow, U, amp_o, info_o);
-            st = nx.st;
-            slow = nx.slow;
-            if (st == ST_A2) xa = nx.xa;
-            if (st == ST_B) {
-                xb = nx.xb;
-                ajb = nx.ajb;
-            }
-        }
-    }
-    if (lane == 0 && nsweeps) {
-        atomicAdd(sweeps, nsweeps);
-        atomicAdd(sweeps + 1, nslots);
-    }
 }
 
 // ============================================================ diagnostics
@@ -5128,7 +4715,7 @@ hipError_t launch_fit_prep(hipStream_t st, const FitStateArrays &S, const double
 
 hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
                            int dtiled, const int32_t *list, const unsigned long long *nctr, long bound,
-                           const FitStateArrays &S)
+                           const FitStateArrays &S, bool round0)
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
@@ -5136,7 +4723,8 @@ hipError_t launch_fit_pass(hipStream_t st, const float *D, const double *T64, lo
     // stride ldD may be longer (padding off the power-of-two stride)
     const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
     if (ldD % 4 != 0 || ldD < nsw || (dtiled && ldD % 32 != 0)) return hipErrorInvalidValue;
-    if (!list)
+    if (round0 && list) return hipErrorInvalidValue;
+    if (round0)
         IC_GGL(k_fit_pass<true>, dim3(cdiv(n, 64)), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled,
                            list, nctr, S, (const double *)S.U);
     else
@@ -5152,35 +4740,6 @@ hipError_t launch_mark_list(hipStream_t st, const int32_t *list, const unsigned 
     if (bound <= 0) return hipSuccess;
     IC_GGL(k_mark_list, dim3(cdiv(std::min(bound, P), 256)), dim3(256), 0, st, list, nctr, P, m, v);
     return hipGetLastError();
-}
-
-hipError_t launch_fit_lanes(hipStream_t st, const float *D, const double *T64, long P, int nbin, int ldD,
-                            int dtiled, int dummy_row, int waves, double *ls, long lst, const double *U,
-                            unsigned *qhead, double *amp, int32_t *info, unsigned long long *sweeps, int phase,
-                            uint8_t *late, int32_t *flist, unsigned long long *fctr, const FitStateArrays *S,
-                            const int32_t *list, const unsigned long long *nctr, long bound)
-{
-    if (phase < 0 || phase > 3 || (phase == 1 && (!late || !flist || !fctr)) ||
-        (phase == 3 && (!S || !list || !nctr)))
-        return hipErrorInvalidValue;
-    const FitStateArrays S0{};
-    const long nprof = phase == 3 ? std::min(bound, P) : P;
-    if ((long)waves * 64 > lst) return hipErrorInvalidValue;
-    if (P <= 0) return hipSuccess;
-    const int nsw = ((nbin + 2 * FIT_TB - 1) / (2 * FIT_TB)) * (2 * FIT_TB);
-    if (ldD % 4 != 0 || ldD < nsw || (dtiled && ldD % 32 != 0) || waves < 1) return hipErrorInvalidValue;
-    const long g = std::min<long>(cdiv(nprof, 64), waves);
-    IC_GGL(k_fit_lanes, dim3((unsigned)g), dim3(64), 0, st, D, T64, P, nbin, ldD, nsw, dtiled, dummy_row, ls,
-           lst, (const double *)U, qhead, amp, info, sweeps, phase, late, flist, fctr, S ? *S : S0, list, nctr);
-    return hipGetLastError();
-}
-
-int fit_lanes_max_waves(int device)
-{
-    int nblk = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nblk, k_fit_lanes, 64, 0) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-    return nblk * ncu;
 }
 
 hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, const int32_t *list,

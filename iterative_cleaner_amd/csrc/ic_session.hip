@@ -60,7 +60,7 @@ const char *kKernelNames[K_COUNT] = {"k_chan_partials", "k_window",    "k_base",
                                      "k_fscrunch",      "k_tscrunch",  "k_fit_pass", "k_fit_state",
                                      "k_diag",          "k_linestats", "k_combine",  "k_residual",
                                      "k_fit_tail",      "k_sb_tree",   "k_shard_pack", "exchange",
-                                     "k_tnorm",         "k_rotate",    "k_fit_lanes"};
+                                     "k_tnorm",         "k_rotate"};
 
 constexpr long kTailProfiles = 8192;  // default: hand the remaining profiles to k_fit_tail below this
 constexpr long kTailProfilesLarge = 4096;   // the same for sessions of >= 2^20 profiles
@@ -134,17 +134,13 @@ struct Session {
     int plan_ub = 0;            // max(leaves, ops) of the pairwise plan (k_tnorm scratch)
     LineStatsArgs ls_knobs;     // row-median form (IC_OPT_ROWSTAT_*)
     long tail_threshold = kTailProfiles;   // IC_OPT_FIT_TAIL
-    long late_lanes = 0;                   // IC_OPT_FIT_LATE_LANES
     bool diag_chain = true;     // IC_OPT_DIAG_CHAIN: k_diag_cl at nbin 1024/2048/4096
-    int fit_schedule = IC_FIT_ROUNDS;   // IC_OPT_FIT_SCHEDULE
-    int lane_waves = 0;         // IC_OPT_FIT_LANE_WAVES (0: every wave the device holds at once)
-    int lane_waves_max = 0;     // lane slots / 64 of `lanes` (k_fit_lanes' state)
-    double *lanes = nullptr;    // k_fit_lanes' lmdif state, kLaneFieldsMax x lane_slots
     double sync_timeout_s = 600.0;   // IC_OPT_SYNC_TIMEOUT_MS
     // a host wait timed out with kernels of this session possibly still in
     // flight: every later call but ic_session_destroy fails (IC_ESTATE), and
     // destroy leaks the device buffers instead of freeing memory in use
     bool failed = false;
+    bool comm_lost = false;   // ... because the transport reported a lost peer
     // diagnostics forked onto a second stream (exact fit): the state kernel
     // of round diag_fork (0 = off) flags the profiles still fitting; from
     // round diag_fork + fork_delay on the others are measured on dstream while
@@ -270,13 +266,23 @@ static hipError_t poll_event(Session *s, hipEvent_t ev)
     const auto spin = std::chrono::microseconds(200);
     const auto limit = std::chrono::duration<double>(s->sync_timeout_s);
     hipError_t e;
+    unsigned n = 0;
     while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
         const auto dt = clk::now() - t0;
         if (dt > limit) {
             s->failed = true;
             return hipErrorLaunchTimeOut;
         }
-        if (dt > spin) sched_yield();
+        if (dt > spin) {
+            sched_yield();
+            // a peer lost by the transport (RCCL's asynchronous error): the
+            // kernels queued behind its collective may never run
+            if (s->comm && (++n & 255) == 0 && s->comm->remote_error()) {
+                s->failed = true;
+                s->comm_lost = true;
+                return hipErrorLaunchTimeOut;
+            }
+        }
     }
     return e;
 }
@@ -378,8 +384,7 @@ void free_all(Session *s)
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
-                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph, s->T2, s->fs.U,
-                    s->lanes};
+                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph, s->T2, s->fs.U, s->tmark};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     void *rbufs[] = {s->std_r, s->mean_r, s->fft_r, s->ptp_r, s->valid_r};
@@ -741,12 +746,9 @@ int shard_rowstats(Session *s, const LineStatsArgs &la)
 // already fitted run on s->dstream (fork_diag); the survivors of that round
 // are kept in the third list buffer for the main stream's second pass.
 int fork_diag(Session *s, const DiagArgs &da, int r);
-// after the round counters: k_fit_lanes' queue head (u32, zeroed with them by
-// k_fit_init), then the tail's and k_fit_lanes' sweep counters (u64 each,
-// accumulating over a run)
-unsigned *lane_queue(Session *s) { return (unsigned *)(s->rcount + kRoundWords); }
+// after the round counters (and two spare words): the tail's sweep counter
+// (u64, accumulating over a run: zeroed and read once per run by ic_run)
 unsigned long long *tail_counter(Session *s) { return (unsigned long long *)(s->rcount + kRoundWords + 2); }
-unsigned long long *lane_counter(Session *s) { return (unsigned long long *)(s->rcount + kRoundWords + 4); }
 
 int run_fit(Session *s, const DiagArgs *fork)
 {
@@ -771,21 +773,6 @@ int run_fit(Session *s, const DiagArgs *fork)
     int flagged = -1;   // the fork round, once its survivors are flagged and pass A not yet queued
     for (int r = 0;; ++r) {
         if (r >= kMaxRounds) return fail(IC_EHIP, "lmdif did not terminate after %d rounds", r);
-        if (r >= 1 && s->late_lanes > 0 && s->lanes && bound <= s->late_lanes && bound > s->tail_threshold) {
-            // the late rounds as one persistent launch: k_fit_lanes takes the
-            // round list with the state k_fit_state left (phase 3)
-            if (flagged >= 0) {
-                if (int rc = fork_diag(s, *fork, flagged)) return rc;
-                flagged = -1;
-            }
-            const int waves = s->lane_waves > 0 ? std::min(s->lane_waves, s->lane_waves_max) : s->lane_waves_max;
-            LAUNCH(s, K_FIT_LANES, launch_fit_lanes(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, (int)s->Ppad,
-                                                    waves, s->lanes, (long)s->lane_waves_max * 64, s->fs.U,
-                                                    lane_queue(s), s->amp, s->info, lane_counter(s), 3, nullptr,
-                                                    nullptr, nullptr, &s->fs, cur, cin, bound));
-            tail = true;
-            break;
-        }
         if (bound <= s->tail_threshold) {
             if (flagged >= 0) {
                 if (int rc = fork_diag(s, *fork, flagged)) return rc;
@@ -823,7 +810,7 @@ int run_fit(Session *s, const DiagArgs *fork)
         const bool fork_here = fork && r == s->diag_fork;
         int32_t *next = fork_here ? bufs[2] : bufs[r & 1];
         LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
-                                                s->fs));
+                                                s->fs, r == 0));
         s->h_rcount[r] = -1;
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
                                                 ctr + r, done + r, s->d_h_rcount + r, fork_here ? s->late : nullptr));
@@ -861,41 +848,6 @@ int run_fit(Session *s, const DiagArgs *fork)
     s->fit_rounds = effective;
     s->stats.fit_rounds += effective;
     s->stats.fit_profile_sweeps += swept;
-    return 0;
-}
-
-// The exact fit as one persistent launch (IC_FIT_LANES, k_fit_lanes): every
-// lane runs lmdif for one profile after another from a shared queue.
-// fork != nullptr: the launch stops once the queue has run out (phase 1),
-// leaving the profiles in flight flagged in s->late and listed in the third
-// list buffer (count in round word 0); the diagnostics of all the others run
-// on dstream (fork_diag) while phase 2 finishes the ones in flight, and the
-// main stream's pass B measures those after it (run_impl).
-int run_fit_lanes(Session *s, const DiagArgs *fork)
-{
-    s->fork_round = -1;
-    const long P = (long)s->P;
-    if (fork) CK(hipMemsetAsync(s->late, 0, P, s->stream));
-    CK(launch_fit_init(s->stream, s->fs, 0, s->rcount, kRoundWords + 2, nullptr));   // round words, queue head
-    CK(launch_fit_prep(s->stream, s->fs, s->T64, s->p.nbin));
-    const int waves = s->lane_waves > 0 ? std::min(s->lane_waves, s->lane_waves_max) : s->lane_waves_max;
-    const long lst = (long)s->lane_waves_max * 64;
-    if (!fork) {
-        LAUNCH(s, K_FIT_LANES, launch_fit_lanes(s->stream, s->D, s->T64, P, s->p.nbin, s->ldD, s->dtiled,
-                                                (int)s->Ppad, waves, s->lanes, lst, s->fs.U, lane_queue(s), s->amp,
-                                                s->info, lane_counter(s)));
-    } else {
-        LAUNCH(s, K_FIT_LANES, launch_fit_lanes(s->stream, s->D, s->T64, P, s->p.nbin, s->ldD, s->dtiled,
-                                                (int)s->Ppad, waves, s->lanes, lst, s->fs.U, lane_queue(s), s->amp,
-                                                s->info, lane_counter(s), 1, s->late, s->lists + 2 * s->P,
-                                                (unsigned long long *)s->rcount));
-        if (int rc = fork_diag(s, *fork, 0)) return rc;
-        LAUNCH(s, K_FIT_LANES, launch_fit_lanes(s->stream, s->D, s->T64, P, s->p.nbin, s->ldD, s->dtiled,
-                                                (int)s->Ppad, waves, s->lanes, lst, s->fs.U, lane_queue(s), s->amp,
-                                                s->info, lane_counter(s), 2));
-    }
-    s->fit_rounds = 1;
-    s->stats.fit_rounds += 1;
     return 0;
 }
 
@@ -1049,10 +1001,9 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     s->raw = s->slot_raw[0];
     // the closed-form fit reads the raw cube (no fit cube, no lmdif state), unless
     // the dedispersion is the FFT rotation: then the rotated fit cube is kept
-    // + one group of 64 zero rows (row Ppad on: the rows k_fit_lanes' waiting lanes read)
     if (exact || p.dedisp_mode == IC_DEDISP_FFT) {
-        AL(s->D, (s->Ppad + 64) * (size_t)s->ldD);
-        if (hipMemset(s->D, 0, sizeof(float) * (s->Ppad + 64) * (size_t)s->ldD) != hipSuccess)
+        AL(s->D, s->Ppad * (size_t)s->ldD);
+        if (hipMemset(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD) != hipSuccess)
             return bail(fail(IC_EHIP, "hipMemset(D) failed"));
     }
     AL(s->TT, 1);
@@ -1126,16 +1077,17 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     AL(s->tw_p2, (size_t)nbin);
     AL(s->plan, 1);
     if (exact) AL(s->lists, 3 * P);   // two ping-pong round lists + the fork round's survivors
-    AL(s->rcount, (size_t)kRoundWords + 8);   // + the lanes' queue, the tail's and the lanes' sweep counters
+    AL(s->rcount, (size_t)kRoundWords + 4);   // + two spare words and the tail's sweep counter
     if (exact) AL(s->late, P);
     if (exact) {
         AL(s->tmark, P);
         if (hipMemset(s->tmark, 0, P) != hipSuccess) return bail(fail(IC_EHIP, "hipMemset(tail marks) failed"));
     }
     if (sharded) {
-        const char *cerr = nullptr;
-        s->comm = make_comm(&cerr);
-        if (!s->comm) return bail(fail(IC_EINVAL, "shard transport: %s", cerr ? cerr : "failed"));
+        std::string cerr;
+        int ccode = IC_EINVAL;
+        s->comm = make_comm(&cerr, &ccode);
+        if (!s->comm) return bail(fail(ccode, "shard transport: %s", cerr.empty() ? "failed" : cerr.c_str()));
         const size_t nchan_g = (size_t)p.nchan;
         AL(s->std_r, (size_t)s->rows_own * nchan_g);
         AL(s->mean_r, (size_t)s->rows_own * nchan_g);
@@ -1213,13 +1165,6 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         for (auto *q : ip) { *q = (int32_t *)b; b += istride; }
         // k_fit_prep's 4 scalars
         if (dalloc(&s->fs.U, 8) != hipSuccess) return bail(fail(IC_ENOMEM, "hipMalloc(fit prep) failed"));
-        // k_fit_lanes' lane slots: every wave the device holds at once, at most one per 64 profiles
-        if (!s->fftded) {
-            const int mw = fit_lanes_max_waves(device);
-            s->lane_waves_max = (int)std::min<size_t>(mw > 0 ? (size_t)mw : 1024, s->Ppad / 64);
-            if (dalloc(&s->lanes, (size_t)kLaneFieldsMax * 64 * s->lane_waves_max) != hipSuccess)
-                return bail(fail(IC_ENOMEM, "hipMalloc(lane state) failed"));
-        }
     }
     // twiddles exp(-2 pi i q / n) and the pairwise plan
     std::vector<double2> tw(nbin);
@@ -1246,7 +1191,7 @@ extern "C" {
 
 int ic_session_create(const ic_params *params, int device, void **out)
 {
-    return create_session(params, device, 0, 1, false, [](const char **) -> Comm * { return nullptr; }, out);
+    return create_session(params, device, 0, 1, false, [](std::string *, int *) -> Comm * { return nullptr; }, out);
 }
 
 int ic_shard_layout(int nsub, int nchan, int world, int32_t *chan_ranges, int32_t *row_ranges)
@@ -1264,14 +1209,28 @@ int ic_session_create_shard(const ic_params *params, int device, int rank, int w
         return fail(IC_EINVAL, "incomplete ic_comm_ops");
     const ic_comm_ops o = *ops;
     return create_session(params, device, rank, world, true,
-                          [&](const char **) -> Comm * { return make_callback_comm(o, rank, world); }, out);
+                          [&](std::string *, int *) -> Comm * { return make_callback_comm(o, rank, world); }, out);
 }
 
 int ic_rccl_unique_id(void *id_out)
 {
     if (!id_out) return fail(IC_EINVAL, "null argument");
+    std::string err;
+    if (rccl_unique_id(id_out, &err)) return fail(IC_ECOMM, "ncclGetUniqueId: %s", err.c_str());
+    return IC_OK;
+}
+
+int ic_rccl_set_library(const char *path)
+{
     const char *err = nullptr;
-    if (rccl_unique_id(id_out, &err)) return fail(IC_ECOMM, "ncclGetUniqueId: %s", err ? err : "failed");
+    if (rccl_set_library(path, &err)) return fail(IC_ESTATE, "%s", err);
+    return IC_OK;
+}
+
+int ic_rccl_set_init_timeout(int64_t ms)
+{
+    const char *err = nullptr;
+    if (rccl_set_init_timeout((long long)ms, &err)) return fail(IC_EINVAL, "%s", err);
     return IC_OK;
 }
 
@@ -1280,7 +1239,10 @@ int ic_session_create_rccl(const ic_params *params, int device, int rank, int wo
 {
     if (!unique_id) return fail(IC_EINVAL, "null unique id");
     return create_session(params, device, rank, world, true,
-                          [&](const char **err) -> Comm * { return make_rccl_comm(unique_id, rank, world, err); },
+                          [&](std::string *err, int *code) -> Comm * {
+                              *code = IC_ECOMM;   // librccl missing, a rank that never joined, RCCL's own errors
+                              return make_rccl_comm(unique_id, rank, world, err);
+                          },
                           out);
 }
 
@@ -1299,7 +1261,12 @@ int ic_session_create_grouped(const ic_params *params, int device, void *group, 
     LocalGroup *g = (LocalGroup *)group;
     if (!g) return fail(IC_EINVAL, "null group");
     return create_session(params, device, rank, local_group_world(g), true,
-                          [&](const char **err) -> Comm * { return make_local_comm(g, rank, device, err); }, out);
+                          [&](std::string *err, int *) -> Comm * {
+                              const char *e = nullptr;
+                              Comm *c = make_local_comm(g, rank, device, &e);
+                              if (e) *err = e;
+                              return c;
+                          }, out);
 }
 
 void ic_session_destroy(void *session)
@@ -1360,7 +1327,7 @@ int ic_upload_pols(void *session, const float *data, int npol, const float *w0, 
                                         hipMemcpyHostToDevice, s->stream);
         if (e == hipSuccess) e = launch_pscrunch(s->stream, s->raw, pol1, s->N);
         if (e == hipSuccess && s->D)
-            e = hipMemsetAsync(s->D, 0, sizeof(float) * (s->Ppad + 64) * (size_t)s->ldD, s->stream);
+            e = hipMemsetAsync(s->D, 0, sizeof(float) * s->Ppad * (size_t)s->ldD, s->stream);
         if (!s->D) {
             if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
             (void)hipFree(pol1);
@@ -1539,6 +1506,9 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     if (s->events.size() > 4096)
         if (int rc = collect_timing(s)) return rc;
     if (s->fftded && !s->delays_set) return fail(IC_ESTATE, "ic_run before ic_set_delays (dedisp_mode FFT)");
+    // the second fork's tail marks are cleared at the end of each iteration; a
+    // run that failed in between may have left some set
+    if (s->tmark) CK(hipMemsetAsync(s->tmark, 0, s->P, s->stream));
     const ic_params &p = s->p;
     const int nsub = p.nsub, nchan = s->nchan, nbin = p.nbin;
     int pr_start = p.pr_start < 0 ? 0 : (p.pr_start > nbin ? nbin : p.pr_start);
@@ -1565,7 +1535,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     s->bad_fits.clear();
     int x = 0, loops = -1, n_iter = 0, converged = 0;
     // k_fit_tail's sweep counter (after the per-round counters): one run's total
-    CK(hipMemsetAsync(tail_counter(s), 0, 3 * sizeof(unsigned long long), s->stream));   // + lane sweeps, slots
+    CK(hipMemsetAsync(tail_counter(s), 0, sizeof(unsigned long long), s->stream));
     while (x < p.max_iter) {
         x += 1;
         ++n_iter;
@@ -1584,11 +1554,7 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         s->pr_hi = pr_end;
         if (p.fit_mode == IC_FIT_EXACT) {
             const bool fork = s->diag_fork > 0 && s->dstream && s->late && diag_list_supported(ds);
-            if (s->fit_schedule == IC_FIT_LANES) {
-                if (int rc = run_fit_lanes(s, fork ? &ds : nullptr)) return rc;
-            } else {
-                if (int rc = run_fit(s, fork ? &ds : nullptr)) return rc;
-            }
+            if (int rc = run_fit(s, fork ? &ds : nullptr)) return rc;
         } else {
             LAUNCH(s, K_TNORM, launch_tnorm(s->stream, s->T64, s->plan, s->plan_ub, s->TT));
         }
@@ -1665,12 +1631,10 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
         int32_t *moves = s->h_small + p.max_iter + 6;                               // pinned
         unsigned long long *tsw = (unsigned long long *)(s->h_small + ((p.max_iter + 9) & ~1));   // 8-B aligned
         CK(hipMemcpyAsync(moves, s->wflag + nsub, sizeof *moves, hipMemcpyDeviceToHost, s->stream));
-        CK(hipMemcpyAsync(tsw, tail_counter(s), 3 * sizeof *tsw, hipMemcpyDeviceToHost, s->stream));
+        CK(hipMemcpyAsync(tsw, tail_counter(s), sizeof *tsw, hipMemcpyDeviceToHost, s->stream));
         CK(spin_sync(s));
         s->stats.window_moves = *moves;
         s->stats.fit_tail_sweeps += (int64_t)tsw[0];
-        s->stats.fit_lane_sweeps += (int64_t)tsw[1];
-        s->stats.fit_lane_slots += (int64_t)tsw[2];
     }
     // timing events are read when asked for (ic_get_kernel_times), not here
     if (loops_out) *loops_out = loops;
@@ -1691,7 +1655,8 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null session");
     if (s->failed) return failed_session();
-    const int rc = run_impl(s, test_out, weights_out, loops_out, changed_out, nzero_out, n_iter_out, converged_out);
+    int rc = run_impl(s, test_out, weights_out, loops_out, changed_out, nzero_out, n_iter_out, converged_out);
+    if (rc && s->comm_lost) rc = fail(IC_ECOMM, "the shard transport lost a peer (RCCL asynchronous error)");
     if (rc && s->comm) s->comm->abort();   // peers must not wait for this shard
     return rc;
 }
@@ -1813,7 +1778,6 @@ int ic_set_option(void *session, int option, int64_t v)
     Session *s = (Session *)session;
     if (!s) return fail(IC_EINVAL, "null session");
     if (s->failed) return fail(IC_ESTATE, "session failed (a host wait timed out); destroy it");
-    const bool exact_shift = s->p.fit_mode == IC_FIT_EXACT && !s->fftded;
     switch (option) {
     case IC_OPT_FIT_TAIL:
         if (v < 0) return fail(IC_EINVAL, "IC_OPT_FIT_TAIL=%lld < 0", (long long)v);
@@ -1836,6 +1800,9 @@ int ic_set_option(void *session, int option, int64_t v)
         if (v != 0 && v != 1) return fail(IC_EINVAL, "IC_OPT_FIT_TILED=%lld (0 or 1)", (long long)v);
         if (v && s->fftded && s->p.fit_mode != IC_FIT_EXACT)
             return fail(IC_EINVAL, "IC_OPT_FIT_TILED: the closed-form fit of the FFT mode reads a row-major cube");
+        // the fit cube of the last run is in the old layout: its residual
+        // (ic_get_residual, the FFT mode's rotation) waits for the next run
+        if ((int)v != s->dtiled) s->ran = false;
         s->dtiled = (int)v;
         return IC_OK;
     case IC_OPT_ROWSTAT_WAVES:
@@ -1855,25 +1822,13 @@ int ic_set_option(void *session, int option, int64_t v)
         s->sync_timeout_s = (double)v / 1000.0;
         return IC_OK;
     case IC_OPT_FIT_SCHEDULE:
-        if (v != IC_FIT_ROUNDS && v != IC_FIT_LANES)
-            return fail(IC_EINVAL, "IC_OPT_FIT_SCHEDULE=%lld (IC_FIT_ROUNDS or IC_FIT_LANES)", (long long)v);
-        if (v == IC_FIT_LANES && !(exact_shift && s->lanes))
-            return fail(IC_EINVAL, "IC_OPT_FIT_SCHEDULE=IC_FIT_LANES needs the exact fit with integer dedispersion");
-        s->fit_schedule = (int)v;
-        return IC_OK;
-    case IC_OPT_FIT_LANE_WAVES:
-        if (v < 0 || v > 1 << 20) return fail(IC_EINVAL, "IC_OPT_FIT_LANE_WAVES=%lld outside 0..2^20", (long long)v);
-        s->lane_waves = (int)v;
+        // the persistent lanes schedule (round 4, measured slower than the
+        // rounds) was removed in round 5: only the rounds remain
+        if (v != IC_FIT_ROUNDS) return fail(IC_EINVAL, "IC_OPT_FIT_SCHEDULE=%lld (only IC_FIT_ROUNDS)", (long long)v);
         return IC_OK;
     case IC_OPT_TAIL_SPLIT:
         if (v < 0 || v > 2) return fail(IC_EINVAL, "IC_OPT_TAIL_SPLIT=%lld (0, 1 or 2)", (long long)v);
         s->tail_split_mode = (int)v;
-        return IC_OK;
-    case IC_OPT_FIT_LATE_LANES:
-        if (v < 0) return fail(IC_EINVAL, "IC_OPT_FIT_LATE_LANES=%lld < 0", (long long)v);
-        if (v > 0 && !(exact_shift && s->lanes))
-            return fail(IC_EINVAL, "IC_OPT_FIT_LATE_LANES needs the exact fit with integer dedispersion");
-        s->late_lanes = (long)v;
         return IC_OK;
     default:
         return fail(IC_EINVAL, "unknown option %d", option);
@@ -1894,9 +1849,7 @@ int ic_get_option(void *session, int option, int64_t *out)
     case IC_OPT_ROWSTAT_MINLEN: *out = s->ls_knobs.grp_minlen; return IC_OK;
     case IC_OPT_DIAG_CHAIN: *out = s->diag_chain ? 1 : 0; return IC_OK;
     case IC_OPT_SYNC_TIMEOUT_MS: *out = (int64_t)(s->sync_timeout_s * 1000.0 + 0.5); return IC_OK;
-    case IC_OPT_FIT_SCHEDULE: *out = s->fit_schedule; return IC_OK;
-    case IC_OPT_FIT_LANE_WAVES: *out = s->lane_waves; return IC_OK;
-    case IC_OPT_FIT_LATE_LANES: *out = s->late_lanes; return IC_OK;
+    case IC_OPT_FIT_SCHEDULE: *out = IC_FIT_ROUNDS; return IC_OK;
     case IC_OPT_TAIL_SPLIT: *out = s->tail_split_mode; return IC_OK;
     default: return fail(IC_EINVAL, "unknown option %d", option);
     }
@@ -2090,7 +2043,7 @@ int ic_fit_profiles(int device, int nprof, int nbin, const float *T, const float
     p.baseline_duty = 0.15;
     p.fit_mode = fit_mode;
     void *h = nullptr;
-    int rc = create_session(&p, device, 0, 1, false, [](const char **) -> Comm * { return nullptr; }, &h);
+    int rc = create_session(&p, device, 0, 1, false, [](std::string *, int *) -> Comm * { return nullptr; }, &h);
     if (rc) return rc;
     Session *s = (Session *)h;
     struct Guard {

@@ -40,10 +40,6 @@ def test_algorithmic_bytes_of_the_fit_sweep():
     run = _run()
     assert bench.algorithmic_bytes("k_fit_pass", 2, 3, 1024, 30, run, 1) == 4 * 1024 * 1000
     assert bench.algorithmic_bytes("k_fit_tail", 2, 3, 1024, 3, run, 2) == 4 * 1024 * 10 * 2
-    # the persistent lanes kernel is charged its own sweeps, k_fit_pass / k_fit_state only the rounds'
-    run = _run(fit_lane_sweeps=700)
-    assert bench.algorithmic_bytes("k_fit_lanes", 2, 3, 1024, 3, run, 1) == 4 * 1024 * 700
-    assert bench.algorithmic_bytes("k_fit_pass", 2, 3, 1024, 30, run, 1) == 4 * 1024 * 1000
     assert bench.algorithmic_bytes("k_fit_state", 2, 3, 1024, 30, run, 1) == 2 * 204 * 1000
 
 

@@ -13,15 +13,13 @@ from helpers import bits_equal, nan_equal
 pytestmark = pytest.mark.gpu
 
 
-def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1, schedule=0, lane_waves=0, late_lanes=0, split=2):
+def _run(monkeypatch, shape, fork, tail, seed=5, rfi=0.1, split=2):
     from iterative_cleaner_amd import _native, synth
     nsub, nchan, nbin = shape
     data, w0, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi)
     raw = np.ascontiguousarray(data[:, 0])
     with _native.GpuSession(nsub, nchan, nbin, max_iter=5, device=0,
-                            options={"diag_fork": fork, "fit_schedule": schedule,
-                                     "fit_lane_waves": lane_waves,
-                                     "fit_late_lanes": late_lanes, "tail_split": split}) as s:
+                            options={"diag_fork": fork, "tail_split": split}) as s:
         if tail is not None:
             s.set_fit_tail(tail)
         s.upload(raw, w0, shift)
@@ -61,45 +59,6 @@ def test_fork_matches_c_oracle_whole_subints(monkeypatch, oracle_lib):
         assert nan_equal(x, ref[name]) and x.dtype == ref[name].dtype, name
     ff = ref["fft"]
     assert np.all(np.abs(diag[3] - ff) <= 1e-9 * np.abs(ff)), "fftmax"
-
-
-@pytest.mark.parametrize("shape", [(16, 256, 1024), (40, 512, 1024), (6, 256, 2048), (4, 192, 4096),
-                                   (24, 256, 256), (16, 300, 512)])
-@pytest.mark.parametrize("lane_waves", [0, 3])
-def test_lanes_fork_is_bit_identical(monkeypatch, shape, lane_waves):
-    """The persistent-lanes fit (IC_FIT_LANES) with the fork: phase 1 stops when
-    the queue runs out, the diagnostics of the finished profiles run beside
-    phase 2, the profiles it finishes are measured after it.  The same bits as
-    the unforked rounds schedule, with every wave the device holds and with 3
-    waves (most profiles then pass through lanes that were refilled)."""
-    from iterative_cleaner_amd import _native
-    ref = _run(monkeypatch, shape, 0, None)
-    for fork in (0, 3):
-        got = _run(monkeypatch, shape, fork, None, schedule=_native.FIT_LANES, lane_waves=lane_waves)
-        assert got[3]["loops"] == ref[3]["loops"]
-        assert bits_equal(got[3]["weights"], ref[3]["weights"]) and bits_equal(got[3]["test"], ref[3]["test"])
-        assert bits_equal(got[4], ref[4]) and bits_equal(got[5], ref[5])
-        for name, x0, x1 in zip(("std", "mean", "ptp", "fftmax"), ref[6], got[6]):
-            assert bits_equal(x1, x0), (fork, name)
-
-
-@pytest.mark.parametrize("shape", [(16, 256, 1024), (40, 512, 1024), (6, 256, 2048), (24, 256, 256)])
-@pytest.mark.parametrize("late", [1 << 40, 3000])
-def test_late_lanes_are_bit_identical(monkeypatch, shape, late):
-    """Option fit_late_lanes: the rounds hand the profiles still fitting to one
-    k_fit_lanes launch (phase 3, each resumed from the state k_fit_state left).
-    The same bits as the rounds to the end, with and without the fork, with
-    the tail threshold above and below the hand-over bound."""
-    ref = _run(monkeypatch, shape, 0, None)
-    for fork, tail in ((0, 0), (3, 0), (3, None), (1, 512)):
-        got = _run(monkeypatch, shape, fork, tail, late_lanes=late)
-        assert got[3]["loops"] == ref[3]["loops"]
-        assert bits_equal(got[3]["weights"], ref[3]["weights"]) and bits_equal(got[3]["test"], ref[3]["test"])
-        assert bits_equal(got[4], ref[4]) and bits_equal(got[5], ref[5])
-        for name, x0, x1 in zip(("std", "mean", "ptp", "fftmax"), ref[6], got[6]):
-            assert bits_equal(x1, x0), (fork, tail, name)
-        if late > 1 << 30 and tail == 0:
-            assert got[7]["fit_lane_slots"] > 0
 
 
 @pytest.mark.parametrize("shape", [(40, 512, 1024), (30, 512, 512), (12, 512, 2048), (24, 300, 256)])

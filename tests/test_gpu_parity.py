@@ -16,9 +16,8 @@ FFT_RTOL = 1e-9
 TEST_ATOL = 1e-9
 
 
-# exact-fit schedules: sweep/state rounds only, k_fit_tail only, the default
-# mix, and the persistent lanes launch (k_fit_lanes; integer dedispersion)
-FIT_MODES = {"rounds": 0, "tail": 1 << 40, "default": None, "lanes": "lanes"}
+# exact-fit schedules: sweep/state rounds only, k_fit_tail only, the default mix
+FIT_MODES = {"rounds": 0, "tail": 1 << 40, "default": None}
 
 
 def _session(shape, args, duty=0.15, fit_mode="default", data_f64=False, delay=None):
@@ -27,10 +26,7 @@ def _session(shape, args, duty=0.15, fit_mode="default", data_f64=False, delay=N
     s = _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"],
                            args["subintthresh"], args["pulse_region"], duty, device=0, data_f64=data_f64,
                            delay=delay)
-    if FIT_MODES[fit_mode] == "lanes":
-        if delay is None:
-            s.set_option("fit_schedule", _native.FIT_LANES)
-    elif FIT_MODES[fit_mode] is not None:
+    if FIT_MODES[fit_mode] is not None:
         s.set_fit_tail(FIT_MODES[fit_mode])
     return s
 
@@ -176,7 +172,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("fit_mode", ["rounds", "tail", "lanes"])
+@pytest.mark.parametrize("fit_mode", ["rounds", "tail"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "%dx%dx%d" % c[:3])
 def test_loop_matches_c_oracle(case, fit_mode, oracle_lib):
     from iterative_cleaner_amd import synth
@@ -196,10 +192,7 @@ def test_loop_matches_c_oracle(case, fit_mode, oracle_lib):
         R = s.residual()
         st = s.run_stats()
     if fit_mode == "rounds":
-        assert st["fit_tail_sweeps"] == 0
-    elif fit_mode == "lanes":
-        assert st["fit_rounds"] == out["n_iter"] and st["fit_tail_sweeps"] == 0
-        assert st["fit_profile_sweeps"] == 0 and st["fit_lane_sweeps"] > 0 and st["fit_lane_slots"] > 0
+        assert st["fit_tail_sweeps"] == 0 and st["fit_profile_sweeps"] > 0
     else:
         assert st["fit_profile_sweeps"] == 0 and st["fit_tail_sweeps"] > 0
     assert out["loops"] == ref["loops"]
@@ -212,7 +205,7 @@ def test_loop_matches_c_oracle(case, fit_mode, oracle_lib):
     assert bits_equal(R, ref["residual"])
 
 
-@pytest.mark.parametrize("fit_mode", ["rounds", "tail", "lanes"])
+@pytest.mark.parametrize("fit_mode", ["rounds", "tail"])
 def test_edge_profiles_match_c_oracle(fit_mode, oracle_lib):
     """Dead (all-zero) channels with weight 1, zero profiles, a NaN-free
     constant channel, fractional weights (K2, K7, K10)."""
@@ -261,7 +254,7 @@ def test_moving_baseline_window_matches_c_oracle(oracle_lib):
     assert _close_test(out["test"], ref["test"])
 
 
-@pytest.mark.parametrize("fit_mode", ["rounds", "default", "lanes"])
+@pytest.mark.parametrize("fit_mode", ["rounds", "default"])
 def test_extreme_amplitudes_match_c_oracle(fit_mode, oracle_lib):
     """Profiles whose fitted amplitudes fall outside the fast sweep's ranges
     (|x| < 2^-100 or > 2^100 for the A sweep, 2^+-500 for B) or whose samples

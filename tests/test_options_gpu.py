@@ -16,12 +16,11 @@ def test_option_ranges_and_modes():
         defaults = {name: s.get_option(name) for name in _native.OPTIONS}
         assert defaults == {"fit_tail": 8192, "diag_fork": 3, "fork_delay": 1, "template_incr": 1,
                             "fit_tiled": 1, "rowstat_waves": 8, "rowstat_minlen": 1024, "diag_chain": 1,
-                            "sync_timeout_ms": 600000, "fit_schedule": 0, "fit_lane_waves": 0,
-                            "fit_late_lanes": 0, "tail_split": 2}
+                            "sync_timeout_ms": 600000, "fit_schedule": 0, "tail_split": 2}
         for name, bad in (("fit_tail", -1), ("diag_fork", 65), ("diag_fork", -1), ("fork_delay", 9),
                           ("template_incr", 2), ("fit_tiled", -1), ("rowstat_waves", 2),
                           ("rowstat_minlen", 0), ("diag_chain", 3), ("sync_timeout_ms", 0),
-                          ("fit_schedule", 2), ("fit_lane_waves", -1), ("fit_late_lanes", -1), ("tail_split", 3)):
+                          ("fit_schedule", 1), ("fit_schedule", 2), ("tail_split", 3)):
             with pytest.raises(_native.NativeError, match="IC_OPT"):
                 s.set_option(name, bad)
             assert s.get_option(name) == defaults[name]
@@ -29,22 +28,19 @@ def test_option_ranges_and_modes():
         assert s.get_option("diag_fork") == 5
         with pytest.raises(ValueError):
             s.set_option("no_such_option", 1)
-    # the fork serves the exact fit only (either dedispersion), the lanes the
-    # exact fit with integer dedispersion; the tiled cube every exact fit and
-    # the closed form with integer dedispersion
+        # options 11 and 12 were the lanes schedule's until round 4: unknown now
+        for opt in (11, 12):
+            with pytest.raises(_native.NativeError, match="unknown option %d" % opt):
+                s._check(s.lib.ic_set_option(s.h, opt, 1), "ic_set_option")
+    # the fork serves the exact fit only (either dedispersion); the tiled cube
+    # every exact fit and the closed form with integer dedispersion
     with _native.GpuSession(4, 64, 256, device=0, fit_mode=_native.FIT_CLOSED) as s:
         with pytest.raises(_native.NativeError, match="DIAG_FORK"):
             s.set_option("diag_fork", 3)
-        with pytest.raises(_native.NativeError, match="FIT_SCHEDULE"):
-            s.set_option("fit_schedule", _native.FIT_LANES)
-        with pytest.raises(_native.NativeError, match="FIT_LATE_LANES"):
-            s.set_option("fit_late_lanes", 1000)
         s.set_option("diag_fork", 0)
     with _native.GpuSession(4, 64, 256, device=0, delay=np.zeros(64)) as s:
         assert s.get_option("diag_fork") == 0 and s.get_option("template_incr") == 1
         assert s.get_option("fit_tiled") == 1
-        with pytest.raises(_native.NativeError, match="FIT_SCHEDULE"):
-            s.set_option("fit_schedule", _native.FIT_LANES)
         for name in ("template_incr", "fit_tiled", "diag_fork"):
             s.set_option(name, 0)
             s.set_option(name, 1)

@@ -68,11 +68,12 @@ def test_local_shards_moving_window_and_pulse_region():
         assert out["loops"] == one["loops"]
 
 
-@pytest.mark.parametrize("opts", [{"tail_split": 1, "diag_fork": 2}, {"fit_late_lanes": 1 << 40},
-                                  {"fit_schedule": 1, "diag_fork": 3}])
+@pytest.mark.parametrize("opts", [{"tail_split": 1, "diag_fork": 2}, {"diag_fork": 0},
+                                  {"fork_delay": 0, "template_incr": 0}])
 def test_local_shards_under_schedule_options(opts):
-    """Schedule options on every shard (the second fork at the tail, the late
-    lanes, the lanes schedule): the same bits as one default session."""
+    """Schedule options on every shard (the second fork at the tail, no fork,
+    the forked pass at once with the full template passes): the same bits as
+    one default session."""
     from iterative_cleaner_amd import sharded, synth
     data, w0, shift = synth.make_cube(12, 2048, 256, 34, 0.2)
     raw = np.ascontiguousarray(data[:, 0])
@@ -167,11 +168,11 @@ def test_native_rccl_one_rank_shard_session():
     dev = torch.device("cuda", 0)
     dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
     try:
-        for schedule in (_native.FIT_ROUNDS, _native.FIT_LANES):
+        for _ in range(1):
             rid = share_rccl_id()          # one unique id per communicator
             assert len(rid) == 128
             with _native.ShardSession(8, 600, 256, 0, 1, rccl_id=rid, device=0,
-                                      options={"fit_schedule": schedule}) as s:
+                                      options={"diag_fork": 3}) as s:
                 s.upload(raw, w0, shift)
                 out = s.run()
                 amp, _ = s.fit()
