@@ -132,11 +132,15 @@ def s8d_bytes(name, nsub, nchan, nbin, launches, iterations, steps):
     once by the fit + diagnostics stage (k_fit_pass + k_diag together in the
     exact mode, k_diag alone in the closed-form mode); the 4 f64 diagnostics
     are written and read once (64 B per profile).  Re-reads an implementation
-    chooses (lmdif's 5.5 sweeps per profile) are NOT algorithmic."""
+    chooses (lmdif's 5.5 sweeps per profile) are NOT algorithmic.
+    Fractional dedispersion (k_rotate): the residual's dededispersion
+    (iterative_cleaner.py:104) reads and writes the cube once per iteration,
+    8N; the template's and the fit cube's rotations (:91, :100) are carried
+    between iterations here, so they are not counted."""
     P = nsub * nchan
     N = P * nbin
     per_iter = {"k_chan_partials": 4 * N, "k_fit_pass": 4 * N, "k_diag": 4 * N + 32 * P,
-                "k_linestats": 16 * P, "k_combine": 16 * P}
+                "k_linestats": 16 * P, "k_combine": 16 * P, "k_rotate": 8 * N}
     if name not in per_iter:
         return None
     return per_iter[name] * iterations * steps
@@ -187,6 +191,11 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True,
         return 4 * width * (P + nchan * run["window_moves"]) * steps
     if name == "k_diag":
         return (4 * N + 44 * P) * n_iter * steps
+    if name == "k_rotate":
+        # 8 B per sample rotated (f32 in, f32 out): preparation's rot(raw) and
+        # fit cube, every iteration's residual, and the carried template rows
+        # of the subints whose baseline window moved
+        return (8 * N * (2 + n_iter) + 8 * nchan * nbin * run["window_moves"]) * steps
     per_launch = {"k_linestats": 2 * 4 * 8 * P, "k_combine": 4 * 8 * P + 2 * 4 * P}
     if name in per_launch:
         return per_launch[name] * launches

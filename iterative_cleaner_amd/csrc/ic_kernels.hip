@@ -127,18 +127,12 @@ struct OpOr {
 //           (iteration 1: base = base0, W = w0: the fit cube of ic.py:96-100 comes
 //           out of the same read of the cube)
 // flags != nullptr: only subints with flags[s] != 0 (a moved window) run.
-#ifndef IC_NT_FITCUBE
-#define IC_NT_FITCUBE 1
-#endif
-#ifndef IC_NT_RAW
-#define IC_NT_RAW 0
-#endif
 // the fit cube is written once and read by the next kernels' sweeps, not by
-// this one: non-temporal stores keep the write stream out of the way (A/B knob)
+// this one: non-temporal stores keep the write stream out of the way (C2
+// -0.14 ms per clean; non-temporal raw loads here cost +0.5 ms)
 __device__ __forceinline__ void st_fitcube(float *p, float v)
 {
-    if (IC_NT_FITCUBE) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    __builtin_nontemporal_store(v, p);
 }
 
 // Exactness of a super-block column (the incremental template stage,
@@ -201,8 +195,7 @@ __global__ __launch_bounds__(256) void k_chan_partials(
             for (int q = 0; q < B; ++q) {
                 int j = i + shift[c + q];
                 if (j >= nbin) j -= nbin;
-                xv[q] = IC_NT_RAW ? __builtin_nontemporal_load(&raw[(krow + c + q) * nbin + j])
-                                  : raw[(krow + c + q) * nbin + j];
+                xv[q] = raw[(krow + c + q) * nbin + j];
                 wv[q] = W[krow + c + q];
                 bv[q] = F ? base[krow + c + q] : 0.0f;
             }
@@ -1109,12 +1102,6 @@ __device__ __forceinline__ bool x_in_sq_range(double x)
 // all 64 lanes hits 16 distinct 16-B slots in each 16-lane bank group.
 // D is padded to [roundup(P,64)][ldD], ldD a multiple of 32: no guards.
 #define FIT_TB 16
-#ifndef IC_NT_SWEEP
-#define IC_NT_SWEEP 0
-#endif
-#ifndef IC_FIT_ROWPROBE
-#define IC_FIT_ROWPROBE 0
-#endif
 #define FIT_BUF 4096
 
 typedef float fv4 __attribute__((ext_vector_type(4)));
@@ -1138,7 +1125,7 @@ __device__ __forceinline__ void dma_tile(const DmaTiles &d, char *buf, int b0)
     for (int m = 0; m < 4; ++m)
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(d.src[m] + off),
                                          (__attribute__((address_space(3))) void *)(buf + m * 1024), 16, 0,
-                                         IC_NT_SWEEP ? 2 : 0);   // cache policy: 2 = nt (A/B knob)
+                                         0);   // default cache policy (nt: 15.7 -> 18.8 ms per C2 clean)
 }
 
 // ds_read in asm: the compiler would otherwise order every LDS read behind a
@@ -1603,9 +1590,6 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
             const long sl = (long)blockIdx.x * 64 + m * 16 + (lane >> 2);
             long kr = 0;   // empty slots read row 0 (valid: D is padded)
             if (sl < nact) kr = rl.at(sl);
-#if IC_FIT_ROWPROBE   // A/B probe only: every wave sweeps rows 0..63 (L2-resident data, VALU-only time)
-            kr = m * 16 + (lane >> 2);
-#endif
             dt.src[m] = D + d_ofs(kr, 4 * c, ldD, dtiled);
         }
         const uint32_t base = lds_u32(lbuf) + 16u * (uint32_t)(64 * (lane >> 4) + 4 * (lane & 15));
@@ -1770,13 +1754,11 @@ __device__ __forceinline__ int fit_transition(const FitStateArrays &S, long k, i
 // independent).  The append is aggregated per block (one atomic per 512
 // profiles), and the last block to finish publishes the final count to
 // host-mapped memory (host_n), so the host needs no copy dispatch to learn it.
-// BS threads per block: 512 for rounds of IC_STATE_SMALL_P profiles or more,
+// BS threads per block: 512 for rounds of kStateSmallP profiles or more,
 // 256 below (twice the blocks: C5 47.8 -> 45.6-46.3 ms per clean; C2's late
 // rounds 25.41-25.43 -> 25.29-25.31; 256 for C2's full rounds too: 26.55
 // against 26.44-26.49)
-#ifndef IC_STATE_SMALL_P
-#define IC_STATE_SMALL_P 524288
-#endif
+constexpr long kStateSmallP = 524288;
 template <int BS>
 __global__ __launch_bounds__(BS) void k_fit_state(FitStateArrays S, long P, const int32_t *__restrict__ list,
                                                             const unsigned long long *__restrict__ nctr,
@@ -2065,10 +2047,8 @@ __device__ __forceinline__ double tail_sweep_b(const RowRef &p, const double *__
     return sum;
 }
 
-#ifndef IC_TAIL_MINW
-#define IC_TAIL_MINW 3   // waves per SIMD the register allocation must allow (A/B: 1 = 2 waves, 0.1 ms/clean slower)
-#endif
-__global__ __launch_bounds__(64 * TAIL_WAVES, IC_TAIL_MINW) void k_fit_tail(const float *__restrict__ D,
+// 3 waves per SIMD for the register allocation (2 waves: 0.1 ms per C2 clean slower)
+__global__ __launch_bounds__(64 * TAIL_WAVES, 3) void k_fit_tail(const float *__restrict__ D,
                                                               const double *__restrict__ T64, long P, int nbin,
                                                               int ldD, int dtiled, const int32_t *__restrict__ list,
                                                               const unsigned long long *__restrict__ nctr,
@@ -2730,15 +2710,8 @@ __device__ __forceinline__ void p2_fft(double2 *C, const XT *X, double mu, const
 // instead of being held in 32 VGPRs.  Measured on C2 (k_diag ms per clean):
 // 3 waves + template in registers 8.63, 4 waves + registers 8.10 (spills),
 // 4 waves + L1 template 7.95 (profiles/r02_c2_diag_ab.txt).
-// IC_P2_MINW_1024 / IC_P2_TREG_1024: A/B build knobs for the N = 1024 kernel.
-#ifndef IC_P2_MINW_1024
-#define IC_P2_MINW_1024 4
-#endif
-#ifndef IC_P2_TREG_1024
-#define IC_P2_TREG_1024 0
-#endif
 template <int N>
-constexpr int p2_min_waves() { return N >= 2048 ? 4 : (N == 1024 ? IC_P2_MINW_1024 : 1); }
+constexpr int p2_min_waves() { return N >= 2048 ? 4 : (N == 1024 ? 4 : 1); }
 
 // D64 (data_f64): psrchive's get_data returns f64, so apply_weights and the
 // masked statistics run in f64 (iterative_cleaner.py:111-112, :206-209): X =
@@ -2751,7 +2724,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
     constexpr int WPP = C::WPP, TPP = C::TPP, NPT = C::NPT;
     // one-wave groups keep the template and the next row in registers; the
     // multi-wave groups (N >= 2048) read both when needed and rely on occupancy
-    constexpr bool TREG = WPP == 1 && (N != 1024 || IC_P2_TREG_1024), PREFETCH = WPP == 1;
+    constexpr bool TREG = WPP == 1 && N != 1024, PREFETCH = WPP == 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // [M] post-processing twiddles, then the stage tables (LDS copy unless TWG)
     const double2 *tw = C::TWG ? a.tw_p2 : (const double2 *)smem;
@@ -3120,51 +3093,26 @@ constexpr int p2_tw_entries(int N)
     return n;
 }
 
-// A/B build knobs of the one-wave (N = 1024) form: IC_CL_TWG = twiddles read
-// through L1/L2 instead of an LDS copy, IC_CL_MINW = waves per SIMD the
-// register allocation must allow, IC_CL_GPB = waves (profile groups) per block
-#ifndef IC_CL_OPAQUE_T
-#define IC_CL_OPAQUE_T 0
-#endif
-#ifndef IC_CL_TWG
-#define IC_CL_TWG 0
-#endif
-#ifndef IC_CL_MINW
-#define IC_CL_MINW 4
-#endif
-#ifndef IC_CL_GPB
-#define IC_CL_GPB 8
-#endif
-// timing probes (wrong results; A/B builds only): 1 = no template gather,
-// 2 = no raw row loads, 3 = FFT stages 2.. skipped
-#ifndef IC_CL_PROBE
-#define IC_CL_PROBE 0
-#endif
-// closed mode: the dedispersed-order samples of the row from an LDS copy of
-// the registers' dispersed-order ones (1) or a second global read (0).  The
-// second read misses L2 often enough to add 15 % to the pass's HBM traffic,
+// The one-wave (N = 1024) form: twiddles from an LDS copy (through L1/L2:
+// 2.59 ms per pass against 2.00), 4 waves per SIMD, 8 profile groups per
+// block.  Closed mode takes the dedispersed-order samples of the row by a
+// second global read, not from an LDS copy of the registers' dispersed-order
+// ones: the read misses L2 often enough to add 15 % to the pass's HBM traffic,
 // but the copy costs LDS bandwidth, which binds at N = 1024 (C2 fast mode
-// 2.48 -> 2.62 ms per pass with the copy; C5 3.09 -> 3.03): off (A/B knob)
-#ifndef IC_CL_PSTAGE
-#define IC_CL_PSTAGE 0
-#endif
-// Stage and spectrum twiddles derived from one base twiddle per butterfly /
-// lane (p2_stage DER; tw[t + L j] = tw[t] exp(-2 pi i j / 16)) instead of one
-// read each: for the multi-wave groups (N >= 2048), whose table is read
-// through L1/L2 (C5 k_diag 2.81 -> 2.68 ms per launch); at N = 1024, whose
-// table is in LDS, it measured no faster (2.005 -> 2.03).  IC_CL_TWDER: -1 =
-// that rule, 0 / 1 = off / on for every N (A/B knob)
-#ifndef IC_CL_TWDER
-#define IC_CL_TWDER -1
-#endif
+// 2.48 -> 2.62 ms per pass with the copy).  Stage and spectrum twiddles are
+// derived from one base twiddle per butterfly / lane (p2_stage DER; tw[t + L j]
+// = tw[t] exp(-2 pi i j / 16)) instead of read one each for the multi-wave
+// groups (N >= 2048), whose table is read through L1/L2 (C5 k_diag 2.81 ->
+// 2.68 ms per launch); at N = 1024, whose table is in LDS, that measured no
+// faster (2.005 -> 2.03).
 template <int N>
 struct CLay {
     static constexpr int L = N / 16;     // threads per profile = chains of 16 samples
     static constexpr int WPP = L / 64;   // waves per profile
     static constexpr int M = N / 2;
     static constexpr int LG = __builtin_ctz(M);
-    static constexpr int GPB = WPP > 1 ? 1 : IC_CL_GPB;   // profile groups per block
-    static constexpr bool TWG = WPP > 1 || IC_CL_TWG;   // multi-wave groups read the table through L1/L2
+    static constexpr int GPB = WPP > 1 ? 1 : 8;   // profile groups per block
+    static constexpr bool TWG = WPP > 1;   // multi-wave groups read the table through L1/L2
     static constexpr int TW_LDS = TWG ? 0 : p2_tw_entries(N);
     static constexpr int CBYTES = M * 16;
     static constexpr int RED_BYTES = WPP > 1 ? 512 : 0;
@@ -3181,12 +3129,12 @@ __device__ __forceinline__ double ufirst(double v)
 }
 
 template <int N, int MODE>
-__global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MINW) void k_diag_cl(DiagArgs a)
+__global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagArgs a)
 {
     using C = CLay<N>;
     constexpr int L = C::L, WPP = C::WPP, M = C::M;
     constexpr bool closed = MODE == DIAG_CLOSED;
-    constexpr bool twder = IC_CL_TWDER < 0 ? WPP > 1 : IC_CL_TWDER != 0;
+    constexpr bool twder = WPP > 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double2 *tw = C::TWG ? a.tw_p2 : (const double2 *)smem;
     const int lane = threadIdx.x & 63;
@@ -3228,7 +3176,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
     auto loadrow = [&](unsigned kk) {
         const float *pn = a.raw + (size_t)kk * N + jb;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) pv[q] = IC_CL_PROBE == 2 ? (float)(q + kk) : pn[8 * q];
+        for (int q = 0; q < 16; ++q) pv[q] = pn[8 * q];
     };
     unsigned slot = next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
     unsigned k = slot < nslot ? (unsigned)rl.at(slot) : 0u;
@@ -3248,7 +3196,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
     for (unsigned snext; slot < nslot; slot = snext) {
         // multi-wave groups: keep the FFT's LDS addresses inside the loop (hoisted,
         // they spill at N >= 2048; k_diag_p2); one wave: hoisted, 118 VGPRs
-        if (WPP > 1 || IC_CL_OPAQUE_T) asm volatile("" : "+v"(t));
+        if (WPP > 1) asm volatile("" : "+v"(t));
         double x = ufirst(nx);
         int st = ufirst(nst);
         const float w = ufirst(nw);
@@ -3259,31 +3207,14 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
         {
             const double *tb = a.T2 + ((unsigned)(jb - sh) & (unsigned)(N - 1));
 #pragma unroll
-            for (int q = 0; q < 16; ++q) tg[q] = IC_CL_PROBE == 1 ? 1.0 + q : tb[8 * q];
+            for (int q = 0; q < 16; ++q) tg[q] = tb[8 * q];
         }
         if constexpr (closed) {
             // a = sum(T*p)/sum(T*T) over the dedispersed-frame chains i = jb + 8q,
             // p_i = f32(raw[(i + sh) mod N] - base)
             const unsigned j0 = (unsigned)(jb + sh);
             float pi[16];
-            if (IC_CL_PSTAGE) {
-                // the row, in registers in dispersed order, through the group's work
-                // area: element j at j ^ (((j >> 7) & 7) << 3), conflict-free for the
-                // chain stores and the rotated loads
-                float *pst = (float *)gb;
-                gsync<WPP>();   // the previous profile's spectrum reads are done
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int j = jb + 8 * q;
-                    pst[j ^ (((j >> 7) & 7) << 3)] = pv[q];
-                }
-                gsync<WPP>();
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int j = (int)((j0 + 8u * q) & (unsigned)(N - 1));
-                    pi[q] = pst[j ^ (((j >> 7) & 7) << 3)];
-                }
-            } else {
+            {
                 const float *row = a.raw + (size_t)k * N;
 #pragma unroll
                 for (int q = 0; q < 16; ++q) pi[q] = row[(j0 + 8u * q) & (unsigned)(N - 1)];
@@ -3391,8 +3322,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, N >= 2048 ? 4 : IC_CL_MI
                 for (int r8 = 0; r8 < 8; ++r8) Cb[A ^ r8] = v[r8];
             }
             gsync<WPP>();
-            if (IC_CL_PROBE != 3)
-                p2_fft<M, L, C::LG, 3, 8, M, float, twder>(Cb, (const float *)nullptr, 0.0, tw, t);
+            p2_fft<M, L, C::LG, 3, 8, M, float, twder>(Cb, (const float *)nullptr, 0.0, tw, t);
             // spectrum in conjugate bin pairs (k_diag_p2).  No NaN bookkeeping:
             // a finite f32 sum s32 means every X is finite, and then every d,
             // Z and |X_k|^2 is finite (|X_k|^2 < 1e85); a non-finite s32 (a NaN or
@@ -3520,11 +3450,8 @@ struct RotCfg {
 // contiguous ds_read_b128 reads are 2-way, and the addresses keep their
 // per-q immediate offsets (an XOR swizzle, conflict-free on both, needs an
 // address register per q and spills at N = 1024).
-#ifndef IC_ROT_PAD
-#define IC_ROT_PAD 1
-#endif
-__device__ __forceinline__ constexpr int rsw(int i) { return IC_ROT_PAD ? i + (i >> 3) : i; }
-template <int M> constexpr int rot_lds_slots() { return IC_ROT_PAD ? M + M / 8 : M; }
+__device__ __forceinline__ constexpr int rsw(int i) { return i + (i >> 3); }
+template <int M> constexpr int rot_lds_slots() { return M + M / 8; }
 
 // R consecutive radix-2 Stockham stages (ns = 2^lg .. 2^(lg+R-1)) through
 // registers: group ja < G = M/2^R holds the 2^R points v[ja + q G]; the stages
@@ -3649,19 +3576,9 @@ __device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
     return make_double2(er - oi, ei + orr);
 }
 
-// A/B knobs: waves per SIMD at N <= 1024; prefetch of the post step's
-// twiddles/phasors one pair ahead; prefetch of the next profile's rows
-#ifndef IC_ROT_OCC
-#define IC_ROT_OCC 3   // round 4: 4 spilled 21 VGPRs; 3 (154 VGPRs, none spilled): C2 fft 57.0 -> 56.4 ms
-#endif
-#ifndef IC_ROT_POSTPF
-#define IC_ROT_POSTPF 0
-#endif
-#ifndef IC_ROT_NEXTPF
-#define IC_ROT_NEXTPF 0
-#endif
 template <int N>
-__global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_rotate(RotateArgs a)
+// 3 waves per SIMD at N <= 1024 (4 spilled 21 VGPRs; 3, 154 VGPRs: C2 fft 57.0 -> 56.4 ms)
+__global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 3 : 2) void k_rotate(RotateArgs a)
 {
     using C = RotCfg<N>;
     constexpr int M = C::M, H = C::H, TB = C::TB;
@@ -3691,21 +3608,12 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_r
     auto skip = [&](size_t p, unsigned s) {
         return (a.flags && a.flags[s] == 0) || (a.late && ((a.late[p] != 0) != (a.late_sel != 0)));
     };
-    float4 xnext[NJ];
-    if (IC_ROT_NEXTPF && blockIdx.x < P) load_rows(blockIdx.x, xnext);
     for (size_t item = blockIdx.x; item < P; item += gridDim.x) {
         const unsigned c = (unsigned)(item / nsub), s = (unsigned)(item % nsub);
         const size_t p = (size_t)s * nchan + c;
+        if (skip(p, s)) continue;
         float4 xin[NJ];
-        if constexpr (IC_ROT_NEXTPF) {
-#pragma unroll
-            for (int u = 0; u < NJ; ++u) xin[u] = xnext[u];
-            if (item + gridDim.x < P) load_rows(item + gridDim.x, xnext);   // lands during this profile
-            if (skip(p, s)) continue;
-        } else {
-            if (skip(p, s)) continue;
-            load_rows(item, xin);
-        }
+        load_rows(item, xin);
         if (a.amp) {
             // the residual of the exact fit (k_residual's arithmetic), formed on the fly
             const int st = a.info[p];
@@ -3748,8 +3656,8 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_r
         gsync<TB / 64>();
         rot_fft<N>(v, twr, t);
         const __amdgpu_buffer_rsrc_t phr = rot_rsrc(a.ph + (size_t)c * (M + 1), M + 1);
-        // the post step's twiddles and phasors: pair u + 1's loads in flight
-        // while pair u computes (IC_ROT_POSTPF; else loaded at their use)
+        // the post step's twiddles and phasors, loaded at their use (a pair ahead:
+        // no faster at 3 or 4 waves per SIMD)
         auto ld = [&](int u, double2 (&w4)[4]) {
             const int k = t + u * TB;
             if (k <= H) {
@@ -3759,12 +3667,10 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_r
                 w4[3] = rot_ld(phr, 16u * (unsigned)(M - k), 0);
             }
         };
-        double2 cw[4], nw[4];
-        if (IC_ROT_POSTPF) ld(0, cw);
+        double2 cw[4];
 #pragma unroll
         for (int u = 0; u < NK; ++u) {
-            if (!IC_ROT_POSTPF) ld(u, cw);
-            else if (u + 1 < NK) ld(u + 1, nw);
+            ld(u, cw);
             const int k = t + u * TB;
             if (k <= H) {
                 const double2 wk = cw[0], wq = cw[1], pk = cw[2], pq = cw[3];
@@ -3784,10 +3690,6 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? IC_ROT_OCC : 2) void k_r
                     v[rsw(q)] = make_double2(Zq.x, -Zq.y);
                     v[rsw(k)] = make_double2(Zk.x, -Zk.y);
                 }
-            }
-            if (IC_ROT_POSTPF) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) cw[e] = nw[e];
             }
         }
         gsync<TB / 64>();
@@ -3831,9 +3733,6 @@ __device__ __forceinline__ double unkey64(unsigned long long k)
 }
 
 // ---- per-line median / MAD: one wave per line, radix select ------------------
-#ifndef IC_LS_EARLY
-#define IC_LS_EARLY 1   // finish a select by one scan once a single key holds the prefix
-#endif
 // Lines: columns (length nsub) of each diagnostic, or rows (length nchan);
 // diag 0 std, 1 mean, 2 ptp (f32 arithmetic), 3 fft (plain: every entry valid).
 // The valid values of the line go to wave-private LDS as order-preserving
@@ -3928,7 +3827,7 @@ __device__ unsigned long long wave_select(const unsigned long long *keys, int n,
         }
         r -= below;
         prefix |= (unsigned long long)bin << shift;
-        if (IC_LS_EARLY && cb == 1u && shift > 0) {
+        if (cb == 1u && shift > 0) {   // a single key holds the prefix: one compare-only scan
             // one key left under the prefix: it is the answer, found in one
             // compare-only scan instead of the remaining digit passes
             const unsigned long long m = ~0ull << shift;
@@ -4148,7 +4047,7 @@ __device__ unsigned long long grp_select(GrpRed<W> &g, const unsigned long long 
         }
         r -= below;
         prefix |= (unsigned long long)bin << shift;
-        if (IC_LS_EARLY && cb == 1u && shift > 0) {   // uniform: every wave read the same bins
+        if (cb == 1u && shift > 0) {   // uniform: every wave read the same bins
             const unsigned long long m = ~0ull << shift;
             unsigned long long f = 0ull;
             for (int j = lane; j < n; j += 64) {
@@ -4571,10 +4470,8 @@ hipError_t launch_chan_delta(hipStream_t st, const float *raw, const int32_t *sh
     const int nsb = (nchan + kSuperBlock - 1) / kSuperBlock;
     if (!exA || !exF) return hipErrorInvalidValue;
     // 256 threads: one per channel of the super-block (the change list), then one per bin
-#ifndef IC_CD_BPT
-#define IC_CD_BPT 0   // bins per thread of k_chan_delta; 0: by nbin
-#endif
-    const int bpt = IC_CD_BPT > 0 ? IC_CD_BPT : (nbin >= 1024 ? 4 : (nbin >= 512 ? 2 : 1));
+    // bins per thread by nbin (C5 template stage 4.55 -> 4.32 ms per clean against 1)
+    const int bpt = nbin >= 1024 ? 4 : (nbin >= 512 ? 2 : 1);
 #define IC_CD(BP, SP)                                                                                   \
     IC_GGL((k_chan_delta<BP, SP>), dim3(cdiv(nbin, 256 * BP), nsb, nsub), dim3(256), 0, st, raw, rawF, shift, \
            base, Wn, Wo, nchan, nbin, nsb, part, part2, wpart, exA, exF)
@@ -4606,10 +4503,7 @@ hipError_t launch_base(hipStream_t st, const float *raw, const int32_t *shift, c
 {
     const size_t P = (size_t)nsub * nchan;
     const unsigned grid = (unsigned)std::min<size_t>(cdiv(P, 16), 16384);
-#ifndef IC_BASE_V4
-#define IC_BASE_V4 1
-#endif
-    if (IC_BASE_V4 && nbin % 4 == 0 && ((uintptr_t)raw & 15) == 0 && width <= nbin)
+    if (nbin % 4 == 0 && ((uintptr_t)raw & 15) == 0 && width <= nbin)
         IC_GGL(k_base<true>, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
     else
         IC_GGL(k_base<false>, dim3(grid), dim3(256), 0, st, raw, shift, win, flags, nsub, nchan, nbin, width, base);
@@ -4749,7 +4643,7 @@ hipError_t launch_fit_state(hipStream_t st, const FitStateArrays &S, long P, con
 {
     const long n = list ? bound : P;
     if (n <= 0) return hipSuccess;
-    if (n < (long)IC_STATE_SMALL_P)
+    if (n < kStateSmallP)
         IC_GGL(k_fit_state<256>, dim3(cdiv(n, 256)), dim3(256), 0, st, S, P, list, nctr, amp, info, next_list, ctr,
                done, host_n, late);
     else

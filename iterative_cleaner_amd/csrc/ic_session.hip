@@ -294,9 +294,6 @@ static hipError_t spin_sync(Session *s)
     return poll_event(s, s->sev);
 }
 
-#ifndef IC_TIMING_MARKERS
-#define IC_TIMING_MARKERS 0   // A/B knob: 1 = hipEventRecord markers around every timed launch
-#endif
 // Timed launches go through the dispatch packet (g_timing, ic_internal.h):
 // no marker packets around them.  A wrapper that launched nothing drops its
 // events; one that launched several kernels ends the interval with a marker.
@@ -308,15 +305,14 @@ static hipError_t spin_sync(Session *s)
         if (tm_) {                                                             \
             CK(take_event((S), &t_.a));                                        \
             CK(take_event((S), &t_.b));                                        \
-            if (IC_TIMING_MARKERS) CK(hipEventRecord(t_.a, (ST)));             \
-            else g_timing = PendingTiming{t_.a, t_.b, 0, 0};                   \
+            g_timing = PendingTiming{t_.a, t_.b, 0, 0};                        \
         }                                                                      \
         const hipError_t lc_ = (CALL);                                         \
         const PendingTiming pt_ = g_timing;                                    \
         g_timing = PendingTiming{};                                            \
         CK(lc_);                                                               \
-        if (tm_ && (pt_.used || IC_TIMING_MARKERS)) {                          \
-            if (pt_.extra || IC_TIMING_MARKERS) CK(hipEventRecord(t_.b, (ST))); \
+        if (tm_ && pt_.used) {                                                 \
+            if (pt_.extra) CK(hipEventRecord(t_.b, (ST)));                     \
             (S)->events.push_back(t_);                                         \
         } else if (tm_) {                                                      \
             (S)->enext -= 2;   /* nothing launched: the pair goes back */      \

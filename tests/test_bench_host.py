@@ -69,3 +69,16 @@ def test_rates_above_peak_refuse_the_line():
     # a cube the Infinity Cache holds may be re-read on-die faster than HBM: reported, not refused
     over, resident = bench.check_kernel_rates(pk, 4 * 64 * 256 * 256)
     assert over == {} and resident == {"k_chan_partials": 8936.1}
+
+
+def test_rotation_bytes():
+    """k_rotate (fractional dedispersion): 8 B per rotated sample; preparation
+    rotates the raw cube and the fit cube, every iteration the residual, and
+    the carried template rows of the subints whose window moved.  Its SURVEY
+    §8(d) share is the residual's dededispersion alone (8N per iteration)."""
+    nsub, nchan, nbin = 4, 6, 128
+    N = nsub * nchan * nbin
+    run = _run(window_moves=5)
+    assert bench.algorithmic_bytes("k_rotate", nsub, nchan, nbin, 7, run, 2) == \
+        2 * (8 * N * (2 + 3) + 8 * nchan * nbin * 5)
+    assert bench.s8d_bytes("k_rotate", nsub, nchan, nbin, 7, 3, 2) == 8 * N * 3 * 2

@@ -24,7 +24,7 @@ CATS = [
     ("cvt", re.compile(r"^v_cvt_")),
     ("f64 add", re.compile(r"^v_add_f64")),
     ("f64 mul", re.compile(r"^v_mul_f64")),
-    ("f64 fma", re.compile(r"^v_fma_f64")),
+    ("f64 fma", re.compile(r"^v_fmac?_f64")),
     ("f64 other", re.compile(r"^v_\w+_f64")),
     ("f32 packed", re.compile(r"^v_pk_\w+_f32")),
     ("f32", re.compile(r"^v_\w+_f32")),
