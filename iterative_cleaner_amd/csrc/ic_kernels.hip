@@ -1168,13 +1168,16 @@ __device__ __forceinline__ void sweep_pair(const DmaTiles &d, int t, int nt, Bod
 }
 
 // Body::kPeel: the first pair (32 samples) is peeled with the checks on, then
-// body.checked()
+// body.checked().  issued: the first tile pair's DMA is already in flight
+// (k_fit_pass issues it before it loads the lanes' lmdif state)
 template <typename Body>
-__device__ __forceinline__ void sweep_dma(const DmaTiles &d, int ldD, Body &body)
+__device__ __forceinline__ void sweep_dma(const DmaTiles &d, int ldD, Body &body, bool issued = false)
 {
     const int nt = ldD / FIT_TB;   // even, >= 2
-    dma_tile(d, d.lds, 0);
-    dma_tile(d, d.lds + FIT_BUF, FIT_TB);
+    if (!issued) {
+        dma_tile(d, d.lds, 0);
+        dma_tile(d, d.lds + FIT_BUF, FIT_TB);
+    }
     int t = 0;
     if constexpr (Body::kPeel) {
         sweep_pair<true>(d, 0, nt, body);
@@ -1446,10 +1449,11 @@ struct ExactBody {
 
 template <bool DA, bool DB, bool FUSE = false>
 __device__ __forceinline__ void fast_sweep(const DmaTiles &d, int ldD, const PassIn &in,
-                                           const double *__restrict__ T64, double agiant, PassOut &out)
+                                           const double *__restrict__ T64, double agiant, PassOut &out,
+                                           bool issued = false)
 {
     FastBody<DA, DB, FUSE> body(in, T64);
-    sweep_dma(d, ldD, body);
+    sweep_dma(d, ldD, body, issued);
     const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant * agiant) >> 32);
     out.f0 = body.fa0;
     out.J0 = body.Ja0;
@@ -1574,12 +1578,6 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     const RoundList rl(list, nctr, P);
     const long nact = rl.n();   // the grid is only an upper bound
     if ((long)blockIdx.x * 64 >= nact) return;
-    const bool in_range = slot < nact;
-    const long k = in_range ? rl.at(slot) : 0;
-    const int st = in_range ? S.mode[k] : ST_DONE;
-    const bool reqA = (st == ST_A0) || (st == ST_A2);
-    const bool reqB = (st == ST_B);
-    if (!__any(reqA || reqB)) return;
     DmaTiles dt;
     dt.lds = lbuf;
     dt.tiled = dtiled;
@@ -1596,6 +1594,20 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
         const int g = (lane >> 2) & 3;
 #pragma unroll
         for (int c2 = 0; c2 < 4; ++c2) dt.rd[c2] = base + 16u * (uint32_t)(c2 ^ g);
+    }
+    // the first tile pair is requested from the list alone, before the lanes'
+    // lmdif state is read: the state's dependent loads (list -> mode -> x, aj)
+    // then overlap the pair's memory latency instead of preceding it
+    dma_tile(dt, dt.lds, 0);
+    dma_tile(dt, dt.lds + FIT_BUF, FIT_TB);
+    const bool in_range = slot < nact;
+    const long k = in_range ? rl.at(slot) : 0;
+    const int st = in_range ? S.mode[k] : ST_DONE;
+    const bool reqA = (st == ST_A0) || (st == ST_A2);
+    const bool reqB = (st == ST_B);
+    if (!__any(reqA || reqB)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the block's LDS
+        return;
     }
     const double agiant = kRgiant / (double)nbin;
     const double eps = sqrt(DBL_EPSILON);
@@ -1634,14 +1646,14 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
         // uniform, but held in VGPRs: the sweep's scalars (a tile of template
         // values) already fill the SGPR file
         asm volatile("" : "+v"(in.ajb), "+v"(in.yaj), "+v"(in.ylj));
-        if (anyA) fast_sweep<true, false, true>(dt, nsw, in, T64, agiant, o);
+        if (anyA) fast_sweep<true, false, true>(dt, nsw, in, T64, agiant, o, true);
     } else {
         if (anyA && anyB)
-            fast_sweep<true, true>(dt, nsw, in, T64, agiant, o);
+            fast_sweep<true, true>(dt, nsw, in, T64, agiant, o, true);
         else if (anyA)
-            fast_sweep<true, false>(dt, nsw, in, T64, agiant, o);
+            fast_sweep<true, false>(dt, nsw, in, T64, agiant, o, true);
         else if (anyB)
-            fast_sweep<false, true>(dt, nsw, in, T64, agiant, o);
+            fast_sweep<false, true>(dt, nsw, in, T64, agiant, o, true);
     }
     const bool exA = reqA && (!fastA || o.bad);
     const bool exB = reqB && !fastB;
