@@ -113,8 +113,12 @@ struct FitStateArrays {
     double *x, *fnorm, *par, *delta, *diag, *xnorm, *acnorm, *J0, *f0, *aj, *r, *Jn0, *qtf, *gnorm,
         *x2, *pnorm, *wa1, *xa;
     int32_t *iter, *nfev, *mode, *slow;
-    double *o_fnorm, *o_acnorm, *o_f0, *o_J0, *o_sum;
-    int32_t *o_exact;   // bit 0: the A sweep took the exact path; bit 1: J(1) == T (round 0)
+    // sweep outputs (k_fit_pass -> k_fit_state): the norms carry the flags in
+    // their sign bits (fnorm: the A sweep took the exact path; acnorm: J(1) ==
+    // T in round 0), o_sum the dot of a B sweep (or round 0's fused one)
+    double *o_fnorm, *o_acnorm, *o_sum;
+    float *p0;            // first sample of every profile's fit-cube row (round 0)
+    const double *T64;    // the iteration's template (k_fit_state recomputes f0 / J0 from it)
     // the first outer iteration's profile-independent qrfac (k_fit_prep): U = {valid, acnorm, aj, Jn0}
     double *U;
 };

@@ -952,7 +952,7 @@ __device__ int lm_after_b(LmState &L, double sum)
     return lm_after_qtf(L);
 }
 
-__device__ int lm_after_a2(LmState &L, double fnorm1)
+__device__ int lm_after_a2(LmState &L, double fnorm1, bool *accepted = nullptr)
 {
     const double ftol = 1.49012e-8, xtol = 1.49012e-8, epsmch = DBL_EPSILON;
     L.nfev += 1;
@@ -980,6 +980,7 @@ __device__ int lm_after_a2(LmState &L, double fnorm1)
         L.delta = L.pnorm / 0.5;
         L.par = 0.5 * L.par;
     }
+    if (accepted) *accepted = ratio >= 1e-4;
     if (ratio >= 1e-4) {
         L.x = L.x2;
         L.xnorm = enorm1(L.diag * L.x);
@@ -1194,7 +1195,8 @@ struct PassIn {
 };
 
 struct PassOut {
-    double fnorm, acnorm, f0, J0, sum;
+    double fnorm, acnorm, sum;
+    float p0;                    // the profile's first sample (round 0: k_fit_state's f0 / J0)
     bool bad;                    // fast path left its verified range
     bool jt;                     // FUSE: J(1) == T, sum is qtf's dot
 };
@@ -1215,7 +1217,8 @@ struct FastBody {
     const PassIn &in;
     const double *__restrict__ T64;
     FastAcc fF, fJ;
-    double fa0, Ja0, sum, fsum;
+    double sum, fsum;
+    float p00;   // FUSE: the first sample
     int lo_ok;
     bool jt;
 
@@ -1223,7 +1226,8 @@ struct FastBody {
     {
         fa_zero(fF);
         fa_zero(fJ);
-        fa0 = Ja0 = sum = fsum = 0.0;
+        sum = fsum = 0.0;
+        p00 = 0.0f;
         lo_ok = 1;
         jt = true;
     }
@@ -1286,10 +1290,7 @@ struct FastBody {
                 fa_add<CHK>(fF, f[k]);
                 fa_add<CHK>(fJ, q[k]);
             }
-            if (first) {
-                fa0 = f[0];
-                Ja0 = q[0];
-            }
+            if (first) p00 = pf[0];
             // Jn = mdiv(J, aj, yaj, ylj) (the B sweep's), dot in sample order
 #pragma unroll
             for (int k = 0; k < 4; ++k) d[k] = q[k] * in.ylj;
@@ -1331,10 +1332,6 @@ struct FastBody {
             for (int k = 0; k < 4; ++k) {
                 fa_add<CHK>(fF, f[k]);
                 fa_add<CHK>(fJ, q[k]);
-            }
-            if (first) {
-                fa0 = f[0];
-                Ja0 = q[0];
             }
         }
         if (DB) {
@@ -1393,13 +1390,15 @@ struct ExactBody {
     const double *__restrict__ T64;
     double agiant;
     Enorm eF, eJ;
-    double fa0, Ja0, sum;
+    double sum;
+    float p00;   // the first sample
 
     __device__ __forceinline__ ExactBody(const PassIn &i, const double *T, double ag) : in(i), T64(T), agiant(ag)
     {
         en_zero(eF);
         en_zero(eJ);
-        fa0 = Ja0 = sum = 0.0;
+        sum = 0.0;
+        p00 = 0.0f;
     }
 
     __device__ void sample(double t, double pv, bool first)
@@ -1413,10 +1412,7 @@ struct ExactBody {
             en_add(eF, f, agiant);
             const double J = d / in.ha;
             en_add(eJ, J, agiant);
-            if (first) {
-                fa0 = f;
-                Ja0 = J;
-            }
+            if (first) p00 = (float)pv;
         }
         if (in.B) {
             const double u = in.xb * t;
@@ -1455,8 +1451,7 @@ __device__ __forceinline__ void fast_sweep(const DmaTiles &d, int ldD, const Pas
     FastBody<DA, DB, FUSE> body(in, T64);
     sweep_dma(d, ldD, body, issued);
     const uint32_t hg = (uint32_t)((unsigned long long)__double_as_longlong(agiant * agiant) >> 32);
-    out.f0 = body.fa0;
-    out.J0 = body.Ja0;
+    out.p0 = body.p00;
     out.sum = FUSE ? body.fsum : body.sum;
     out.fnorm = fa_fin(body.fF);
     out.acnorm = fa_fin(body.fJ);
@@ -1634,7 +1629,8 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
     in.B = fastB;
     PassOut o;
     o.bad = o.jt = false;
-    o.fnorm = o.acnorm = o.f0 = o.J0 = o.sum = 0.0;
+    o.fnorm = o.acnorm = o.sum = 0.0;
+    o.p0 = 0.0f;
     const bool anyA = __any(fastA), anyB = __any(fastB);
     if constexpr (R0) {
         // every profile at x = 1: the first B sweep's dot rides along (k_fit_prep)
@@ -1664,20 +1660,24 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
         ExactBody body(ie, T64, agiant);
         sweep_dma(dt, nsw, body);
         if (exA || exB) {
-            o.f0 = body.fa0;
-            o.J0 = body.Ja0;
+            if (exA) o.p0 = body.p00;
             o.sum = body.sum;
             o.fnorm = en_fin(body.eF);
             o.acnorm = en_fin(body.eJ);
         }
     }
+    // The outputs, as few bytes as possible: written into the sweep's read
+    // stream, a DRAM write costs ~10x its size (tools/ubench_sweep: five 8-B
+    // fields per profile +90 us per 4.7-GB round, one +20 us).  The two norms
+    // carry the flags in their sign bits (both are >= 0 or NaN, whose sign
+    // nothing reads): exA on fnorm, jt on acnorm.  f0 and J0, the residual and
+    // the Jacobian at sample 0, are recomputed by k_fit_state from the first
+    // sample, which round 0 stores once (OutS::f0J0).
     if (reqA) {
-        S.o_fnorm[k] = o.fnorm;
-        S.o_acnorm[k] = o.acnorm;
-        S.o_f0[k] = o.f0;
-        S.o_J0[k] = o.J0;
-        S.o_exact[k] = (exA ? 1 : 0) | (o.jt ? 2 : 0);
+        S.o_fnorm[k] = exA ? -fabs(o.fnorm) : fabs(o.fnorm);
+        S.o_acnorm[k] = o.jt ? -fabs(o.acnorm) : fabs(o.acnorm);
         if (o.jt) S.o_sum[k] = o.sum;
+        if (R0) S.p0[k] = o.p0;
     }
     if (reqB) S.o_sum[k] = o.sum;
 }
@@ -1689,12 +1689,33 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
 struct OutS {
     const FitStateArrays &S;
     long k;
-    __device__ __forceinline__ double fnorm() const { return S.o_fnorm[k]; }
-    __device__ __forceinline__ double acnorm() const { return S.o_acnorm[k]; }
-    __device__ __forceinline__ double f0() const { return S.o_f0[k]; }
-    __device__ __forceinline__ double J0() const { return S.o_J0[k]; }
+    __device__ __forceinline__ double fnorm() const { return fabs(S.o_fnorm[k]); }
+    __device__ __forceinline__ double acnorm() const { return fabs(S.o_acnorm[k]); }
     __device__ __forceinline__ double sum() const { return S.o_sum[k]; }
-    __device__ __forceinline__ int exact() const { return S.o_exact[k]; }
+    // bit 0: the A sweep took the exact path; bit 1: J(1) == T (round 0)
+    __device__ __forceinline__ int exact() const
+    {
+        return (signbit(S.o_fnorm[k]) ? 1 : 0) | (signbit(S.o_acnorm[k]) ? 2 : 0);
+    }
+    // the residual f0 and the Jacobian J0 at sample 0 of the A sweep at x: the
+    // sweep's own operations on its first sample (ExactBody::sample; the fast
+    // bodies' four-op division is RN(d / h) wherever their result is used, and
+    // at x = 1 d 2^26 = d / 2^-26), from the first sample round 0 stored
+    __device__ __forceinline__ void f0J0(double x, double &f0, double &J0) const
+    {
+        const double eps = sqrt(DBL_EPSILON);
+        double h = eps * fabs(x);
+        if (h == 0.0) h = eps;
+        const double xh = x + h;
+        const double t = S.T64[0], pv = (double)S.p0[k];
+        const double u = x * t;
+        const double f = u - pv;
+        const double uh = xh * t;
+        const double wa = uh - pv;
+        const double d = wa - f;
+        f0 = f;
+        J0 = d / h;
+    }
 };
 template <typename Out>
 __device__ __forceinline__ int fit_transition(const FitStateArrays &S, long k, int st, const Out &o,
@@ -1720,8 +1741,7 @@ __device__ __forceinline__ int fit_transition(const FitStateArrays &S, long k, i
         L.fnorm = o.fnorm();
         L.nfev = 1;
         L.acnorm = o.acnorm();
-        L.f0 = o.f0();
-        L.J0 = o.J0();
+        o.f0J0(1.0, L.f0, L.J0);
         const int oe = o.exact();
         S.slow[k] = oe & 1;
         st = lm_outer(L);
@@ -1738,16 +1758,32 @@ __device__ __forceinline__ int fit_transition(const FitStateArrays &S, long k, i
         } else {
             lm_store(L, S, k);
         }
-    } else if (st != ST_DONE) {
-        lm_load(L, S, k);
-        if (st == ST_A2) {
-            L.acn2 = o.acnorm();
-            L.f02 = o.f0();
-            L.J02 = o.J0();
-            st = lm_after_a2(L, o.fnorm());
-            if (L.x == L.x2) S.slow[k] = o.exact() & 1;
+    } else if (st == ST_A2) {
+        // lm_after_a2 and what follows it read 14 of the 19 fields (acnorm, J0,
+        // f0, aj and Jn0 are set anew on the way that uses them), and write: on
+        // a rejected step, the inner loop's 6 (nfev, par, delta, wa1, x2,
+        // pnorm); on an accepted one those and the outer iteration's 13; on
+        // ST_DONE, nothing but amp / info (most profiles end here)
+        L.x = S.x[k]; L.fnorm = S.fnorm[k]; L.par = S.par[k]; L.delta = S.delta[k]; L.diag = S.diag[k];
+        L.xnorm = S.xnorm[k]; L.r = S.r[k]; L.qtf = S.qtf[k]; L.gnorm = S.gnorm[k]; L.x2 = S.x2[k];
+        L.pnorm = S.pnorm[k]; L.wa1 = S.wa1[k]; L.iter = S.iter[k]; L.nfev = S.nfev[k]; L.info = 0;
+        L.acnorm = L.J0 = L.f0 = L.aj = L.Jn0 = 0.0;   // not read before they are set
+        L.acn2 = o.acnorm();
+        o.f0J0(L.x2, L.f02, L.J02);   // the A request was at the trial point x2
+        bool accepted = false;
+        st = lm_after_a2(L, o.fnorm(), &accepted);
+        if (st != ST_DONE) {
+            S.nfev[k] = L.nfev; S.par[k] = L.par; S.delta[k] = L.delta; S.wa1[k] = L.wa1; S.x2[k] = L.x2;
+            S.pnorm[k] = L.pnorm;
+            if (accepted) {
+                S.x[k] = L.x; S.xnorm[k] = L.xnorm; S.fnorm[k] = L.fnorm; S.iter[k] = L.iter;
+                S.acnorm[k] = L.acnorm; S.J0[k] = L.J0; S.f0[k] = L.f0; S.aj[k] = L.aj; S.r[k] = L.r;
+                S.Jn0[k] = L.Jn0; S.qtf[k] = L.qtf; S.gnorm[k] = L.gnorm; S.diag[k] = L.diag;
+                S.slow[k] = o.exact() & 1;   // J at the new x came from this sweep
+            }
         }
-        lm_store(L, S, k);
+    } else if (st != ST_DONE) {
+        return st;   // (no other request exists)
     } else {
         return ST_DONE;
     }

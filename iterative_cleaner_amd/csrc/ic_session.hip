@@ -1147,18 +1147,19 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (hipHostMalloc((void **)&s->h_small, sizeof(int32_t) * ((size_t)p.max_iter + 20)) != hipSuccess)
         return bail(fail(IC_ENOMEM, "hipHostMalloc(readback) failed"));
     if (exact) {
-        // fit state: 23 double arrays + 5 int arrays, each padded to 256 B
+        // fit state: 21 double arrays + 5 four-byte arrays, each padded to 256 B
         const size_t dstride = ((P * 8 + 255) / 256) * 256, istride = ((P * 4 + 255) / 256) * 256;
-        if (hipMalloc(&s->fs_block, 23 * dstride + 5 * istride) != hipSuccess)
+        if (hipMalloc(&s->fs_block, 21 * dstride + 5 * istride) != hipSuccess)
             return bail(fail(IC_ENOMEM, "hipMalloc(fit state) failed"));
         char *b = (char *)s->fs_block;
         double **dp[] = {&s->fs.x,     &s->fs.fnorm, &s->fs.par,   &s->fs.delta,   &s->fs.diag, &s->fs.xnorm,
                          &s->fs.acnorm, &s->fs.J0,   &s->fs.f0,    &s->fs.aj,      &s->fs.r,    &s->fs.Jn0,
                          &s->fs.qtf,   &s->fs.gnorm, &s->fs.x2,    &s->fs.pnorm,   &s->fs.wa1,  &s->fs.xa,
-                         &s->fs.o_fnorm, &s->fs.o_acnorm, &s->fs.o_f0, &s->fs.o_J0, &s->fs.o_sum};
+                         &s->fs.o_fnorm, &s->fs.o_acnorm, &s->fs.o_sum};
         for (auto *q : dp) { *q = (double *)b; b += dstride; }
-        int32_t **ip[] = {&s->fs.iter, &s->fs.nfev, &s->fs.mode, &s->fs.slow, &s->fs.o_exact};
+        int32_t **ip[] = {&s->fs.iter, &s->fs.nfev, &s->fs.mode, &s->fs.slow, (int32_t **)&s->fs.p0};
         for (auto *q : ip) { *q = (int32_t *)b; b += istride; }
+        s->fs.T64 = s->T64;
         // k_fit_prep's 4 scalars
         if (dalloc(&s->fs.U, 8) != hipSuccess) return bail(fail(IC_ENOMEM, "hipMalloc(fit prep) failed"));
     }
