@@ -3472,9 +3472,11 @@ __global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, c
 
 // ---------------------------------------------------------------------------
 // Fractional dedispersion: psrchive's FFT phase rotation in the stand-in's
-// written order (phase_rotation.py; oracle orc_rotate).  One block per
-// profile (persistent grid, channel-major so that the blocks in flight share a
-// channel's phasor row in L2); the N/2 complex points live in LDS.
+// written order (phase_rotation.py; oracle orc_rotate).  A profile per wave
+// (N <= 1024: four to a block, sharing the twiddle tables staged in LDS) or per
+// block (N >= 2048); grid-stride over channel-major items so that the profiles
+// in flight share a channel's phasor row in L2; the N/2 complex points live in
+// LDS between the passes.
 //   1. z[j] = (f64(f32(x[2j] - b)), f64(f32(x[2j+1] - b)))
 //   2. Z = FFT_{N/2}(z), radix-2 Stockham, register-staged in place
 //   3. pairs (k, N/2 - k): real spectrum, x phasor, inverse half-spectrum (conj)
@@ -3488,6 +3490,11 @@ struct RotCfg {
     static constexpr int LG = N == 64 ? 5 : N == 128 ? 6 : N == 256 ? 7 : N == 512 ? 8 : N == 1024 ? 9
                                                                               : N == 2048 ? 10 : 11;   // log2 M
     static constexpr int TB = M / 8 < 64 ? 64 : (M / 8 > 256 ? 256 : M / 8);
+    // one-wave profiles run four to a block, which stages the twiddle table in
+    // LDS once for all four (M entries: every index the passes and the post
+    // step use is below M)
+    static constexpr int WPB = TB == 64 ? 4 : 1;
+    static constexpr bool TW_LDS = WPB > 1;
 };
 
 // LDS slot of complex point i: one pad slot after every 8 points.
@@ -3520,13 +3527,47 @@ __device__ __forceinline__ double2 rot_ld(__amdgpu_buffer_rsrc_t r, unsigned vof
     return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-template <int N, int R, int LGS>
-__device__ __forceinline__ void rot_pass(double2 *v, __amdgpu_buffer_rsrc_t twr, int t)
+// Twiddle sources: the table in global memory (through L1/L2) or staged in LDS.
+// TW(voff, soff) = tw entry at byte offset voff + soff.
+// pass(k, kl): twiddle of global stage s = LGS + l for butterfly k + kl 2^LGS,
+// tw[(k + kl 2^LGS) N / 2^(s+1)];  post(i): tw[i].
+template <int N>
+struct TwGlobal {
+    __amdgpu_buffer_rsrc_t r;
+    template <int LGS>
+    __device__ __forceinline__ double2 pass(unsigned k, unsigned kl, int l) const
+    {
+        constexpr unsigned S0 = 16u * (N >> (LGS + 1));
+        return rot_ld(r, (k * S0) >> l, (kl << LGS) * (S0 >> l));
+    }
+    __device__ __forceinline__ double2 post(unsigned i) const { return rot_ld(r, 16u * i, 0); }
+};
+// LDS: stage s's 2^s twiddles contiguous at 2^s - 1 (a stage's lanes read
+// consecutive slots: no bank conflicts, where the strided plain table was up to
+// 8-way), and the plain table for the post step
+template <int N>
+struct TwLds {
+    const double2 *stage, *plain;
+    template <int LGS>
+    __device__ __forceinline__ double2 pass(unsigned k, unsigned kl, int l) const
+    {
+        return stage[(1u << (LGS + l)) - 1u + k + (kl << LGS)];
+    }
+    __device__ __forceinline__ double2 post(unsigned i) const { return plain[i]; }
+};
+
+// IN_REG: the pass's input is z (one group per thread, G == TB) instead of
+// LDS; OUT_REG: its output stays in z.  The last pass's group ja holds points
+// ja + q G, the distribution the first pass reads, so a profile can enter and
+// leave the FFT in registers (k_rotate's direct layout).
+template <int N, int R, int LGS, bool IN_REG = false, bool OUT_REG = false, typename TW>
+__device__ __forceinline__ void rot_pass(double2 *v, const TW &tw, int t, double2 *z = nullptr)
 {
     using C = RotCfg<N>;
     constexpr int M = C::M, TB = C::TB, G = M >> R, Q = 1 << R, HALF = Q / 2;
     constexpr int GPT = (G + TB - 1) / TB;
     constexpr int ns = 1 << LGS;
+    static_assert(!(IN_REG || OUT_REG) || G == TB, "register passes hold one group per thread");
     double2 u[GPT][Q];
     // the pass's twiddles first (global/L1 latency overlaps the LDS reads and
     // the barrier): local stage l uses 2^l distinct ones, w[2^l - 1 + kl]
@@ -3539,13 +3580,14 @@ __device__ __forceinline__ void rot_pass(double2 *v, __amdgpu_buffer_rsrc_t twr,
 #pragma unroll
             for (int l = 0; l < R; ++l) {
                 // tw[(kl ns + k) S], S = N / 2^(l + LGS + 1)
-                constexpr unsigned S0 = 16u * (N >> (LGS + 1));
-                const unsigned kb = ((unsigned)k * S0) >> l;
 #pragma unroll
                 for (int kl = 0; kl < (1 << l); ++kl)
-                    w[gi][(1 << l) - 1 + kl] = rot_ld(twr, kb, (unsigned)(kl * ns) * (S0 >> l));
+                    w[gi][(1 << l) - 1 + kl] = tw.template pass<LGS>((unsigned)k, (unsigned)kl, l);
             }
-            if constexpr (G % 8 == 0) {
+            if constexpr (IN_REG) {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) u[gi][q] = z[q];
+            } else if constexpr (G % 8 == 0) {
                 const double2 *vj = v + rsw(ja);    // rsw(ja + q G) = rsw(ja) + rsw(q G)
 #pragma unroll
                 for (int q = 0; q < Q; ++q) u[gi][q] = vj[rsw(q * G)];
@@ -3580,7 +3622,11 @@ __device__ __forceinline__ void rot_pass(double2 *v, __amdgpu_buffer_rsrc_t twr,
                 for (int q = 0; q < Q; ++q) u[gi][q] = w2[q];
             }
             const int base = ((ja >> LGS) << (LGS + R)) + k;
-            if constexpr (ns == 1 || ns % 8 == 0) {
+            if constexpr (OUT_REG) {
+                static_assert(ns * Q == M, "only the last pass keeps its output");
+#pragma unroll
+                for (int q = 0; q < Q; ++q) z[q] = u[gi][q];
+            } else if constexpr (ns == 1 || ns % 8 == 0) {
                 // ns = 1: base is a multiple of Q <= 8, so base + q stays in base's 8-block
                 double2 *vb = v + rsw(base);
 #pragma unroll
@@ -3594,15 +3640,17 @@ __device__ __forceinline__ void rot_pass(double2 *v, __amdgpu_buffer_rsrc_t twr,
     gsync<C::TB / 64>();
 }
 
-// the full N/2-point FFT: passes of 3 stages (the last one shorter)
-template <int N, int LG0 = 0>
-__device__ __forceinline__ void rot_fft(double2 *v, __amdgpu_buffer_rsrc_t twr, int t)
+// the full N/2-point FFT: passes of 3 stages (the last one shorter); IN_REG /
+// OUT_REG: the first pass reads z / the last pass leaves its output in z
+template <int N, int LG0 = 0, bool IN_REG = false, bool OUT_REG = false, typename TW>
+__device__ __forceinline__ void rot_fft(double2 *v, const TW &tw, int t, double2 *z = nullptr)
 {
     constexpr int LG = RotCfg<N>::LG;
     if constexpr (LG0 < LG) {
         constexpr int R = LG - LG0 >= 3 ? 3 : LG - LG0;
-        rot_pass<N, R, LG0>(v, twr, t);
-        rot_fft<N, LG0 + R>(v, twr, t);
+        constexpr bool LAST = LG0 + R >= LG;
+        rot_pass<N, R, LG0, IN_REG && LG0 == 0, OUT_REG && LAST>(v, tw, t, z);
+        rot_fft<N, LG0 + R, false, OUT_REG>(v, tw, t, z);
     }
 }
 
@@ -3626,19 +3674,40 @@ __device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
 
 template <int N>
 // 3 waves per SIMD at N <= 1024 (4 spilled 21 VGPRs; 3, 154 VGPRs: C2 fft 57.0 -> 56.4 ms)
-__global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 3 : 2) void k_rotate(RotateArgs a)
+__global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) void k_rotate(RotateArgs a)
 {
     using C = RotCfg<N>;
-    constexpr int M = C::M, H = C::H, TB = C::TB;
+    constexpr int M = C::M, H = C::H, TB = C::TB, WPB = C::WPB;
     constexpr int NJ = (M / 2 + TB - 1) / TB;    // float4 rows per lane (4 samples = 2 points)
     constexpr int NK = H / TB + 1;               // spectrum pairs (k, M - k) per lane, k <= H
-    __shared__ double2 v[rot_lds_slots<M>()];
-    const int t = threadIdx.x;
+    // direct layout (every pass radix 8, one group per lane: N = 1024): lane t
+    // loads points t + TB q (q < 8) straight into the first pass's registers and
+    // stores the last pass's registers, which are the same points; two LDS round
+    // trips per profile fewer
+    constexpr bool DIRECT = C::LG % 3 == 0 && (M >> 3) == TB;
+    __shared__ double2 vv[WPB][rot_lds_slots<M>()];
+    __shared__ double2 tws[C::TW_LDS ? 2 * M : 1];
+    const int t = threadIdx.x % TB, wv = threadIdx.x / TB;
+    double2 *v = vv[wv];
     const unsigned nsub = (unsigned)a.nsub, nchan = (unsigned)a.nchan;
     const size_t P = (size_t)nsub * nchan;
     const double sg = a.sign > 0 ? 1.0 : -1.0;
     const double inv = 1.0 / (double)M;
     const __amdgpu_buffer_rsrc_t twr = rot_rsrc(a.tw, N);
+    const auto tw = [&]() {
+        if constexpr (C::TW_LDS) return TwLds<N>{tws + M, tws};
+        else return TwGlobal<N>{twr};
+    }();
+    if constexpr (C::TW_LDS) {
+        for (int i = threadIdx.x; i < M; i += TB * WPB) {
+            tws[i] = a.tw[i];
+            // compact slot i: stage s = floor(log2(i + 1)), j = i + 1 - 2^s
+            // (slot M - 1 is unused: s = LG)
+            const int s = 31 - __clz(i + 1), j = i + 1 - (1 << s);
+            tws[M + i] = a.tw[(size_t)j * (N >> (s + 1))];
+        }
+        __syncthreads();
+    }
     // every global load of a profile in flight at once: one memory latency
     // per profile, not one per row (or per flag / fit lookup)
     auto load_rows = [&](size_t it, float4 (&xr)[NJ]) {
@@ -3656,18 +3725,69 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 3 : 2) void k_rotate(Rot
     auto skip = [&](size_t p, unsigned s) {
         return (a.flags && a.flags[s] == 0) || (a.late && ((a.late[p] != 0) != (a.late_sel != 0)));
     };
-    for (size_t item = blockIdx.x; item < P; item += gridDim.x) {
+    // a block's profiles are consecutive items (channel-major): they share a
+    // channel's phasor row
+    for (size_t item = (size_t)blockIdx.x * WPB + wv; item < P; item += (size_t)gridDim.x * WPB) {
         const unsigned c = (unsigned)(item / nsub), s = (unsigned)(item % nsub);
         const size_t p = (size_t)s * nchan + c;
         if (skip(p, s)) continue;
+        double2 z[8];
+        if constexpr (DIRECT) {
+            const size_t k = p;
+            float2 x2[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                x2[q] = *(const float2 *)(a.in + d_ofs(k, 2 * (t + TB * q), (int)a.ld_in, a.in_tiled));
+            if (a.amp) {
+                const __amdgpu_buffer_rsrc_t t64r = rot_rsrc((const double2 *)a.T64, M);
+                double2 tt[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) tt[q] = rot_ld(t64r, 16u * (unsigned)t, 16u * (unsigned)(TB * q));
+                const int st = a.info[p];
+                const bool ok = st >= 1 && st <= 4;
+                const double am = a.amp[p];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    float r[2] = {0.0f, 0.0f};
+                    if (ok) {
+                        const float pv[2] = {x2[q].x, x2[q].y};
+                        const double tv[2] = {tt[q].x, tt[q].y};
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const int i = 2 * (t + TB * q) + e;
+                            const double uu = am * tv[e];
+                            double d = uu - (double)pv[e];
+                            if (a.pr_on && i >= a.pr_start && i < a.pr_end) d = d * a.pr_factor;
+                            r[e] = (float)d;
+                        }
+                    }
+                    z[q] = make_double2((double)r[0], (double)r[1]);
+                }
+            } else {
+                const float b = a.base ? a.base[p] : 0.0f;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) z[q] = make_double2((double)(x2[q].x - b), (double)(x2[q].y - b));
+            }
+            rot_fft<N, 0, true, false>(v, tw, t, z);
+        } else {
         float4 xin[NJ];
         load_rows(item, xin);
         if (a.amp) {
-            // the residual of the exact fit (k_residual's arithmetic), formed on the fly
+            // the residual of the exact fit (k_residual's arithmetic), formed on the fly;
+            // the template is requested with the rows, before the status is known
+            // (behind the scattered amp / info loads it was a second latency)
+            const __amdgpu_buffer_rsrc_t t64r = rot_rsrc((const double2 *)a.T64, M);
+            double2 tt[NJ][2];
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) {
+                const int j2 = t + u * TB;
+                if ((M / 2) % TB != 0 && j2 >= M / 2) break;
+                tt[u][0] = rot_ld(t64r, 32u * (unsigned)t, 32u * (unsigned)(u * TB));
+                tt[u][1] = rot_ld(t64r, 32u * (unsigned)t, 32u * (unsigned)(u * TB) + 16u);
+            }
             const int st = a.info[p];
             const bool ok = st >= 1 && st <= 4;
             const double am = a.amp[p];
-            const __amdgpu_buffer_rsrc_t t64r = rot_rsrc((const double2 *)a.T64, M);
 #pragma unroll
             for (int u = 0; u < NJ; ++u) {
                 const int j2 = t + u * TB;
@@ -3675,9 +3795,7 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 3 : 2) void k_rotate(Rot
                 float r[4] = {0.0f, 0.0f, 0.0f, 0.0f};
                 if (ok) {
                     const float pv[4] = {xin[u].x, xin[u].y, xin[u].z, xin[u].w};
-                    const double2 ta = rot_ld(t64r, 32u * (unsigned)t, 32u * (unsigned)(u * TB));
-                    const double2 tb = rot_ld(t64r, 32u * (unsigned)t, 32u * (unsigned)(u * TB) + 16u);
-                    const double tv[4] = {ta.x, ta.y, tb.x, tb.y};
+                    const double tv[4] = {tt[u][0].x, tt[u][0].y, tt[u][1].x, tt[u][1].y};
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const int i = 4 * j2 + e;
@@ -3702,15 +3820,16 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 3 : 2) void k_rotate(Rot
             }
         }
         gsync<TB / 64>();
-        rot_fft<N>(v, twr, t);
+        rot_fft<N>(v, tw, t);
+        }
         const __amdgpu_buffer_rsrc_t phr = rot_rsrc(a.ph + (size_t)c * (M + 1), M + 1);
         // the post step's twiddles and phasors, loaded at their use (a pair ahead:
         // no faster at 3 or 4 waves per SIMD)
         auto ld = [&](int u, double2 (&w4)[4]) {
             const int k = t + u * TB;
             if (k <= H) {
-                w4[0] = rot_ld(twr, 16u * (unsigned)(k & (M - 1)), 0);
-                w4[1] = rot_ld(twr, 16u * (unsigned)((M - k) & (M - 1)), 0);
+                w4[0] = tw.post((unsigned)(k & (M - 1)));
+                w4[1] = tw.post((unsigned)((M - k) & (M - 1)));
                 w4[2] = rot_ld(phr, 16u * (unsigned)k, 0);
                 w4[3] = rot_ld(phr, 16u * (unsigned)(M - k), 0);
             }
@@ -3723,8 +3842,8 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 3 : 2) void k_rotate(Rot
             if (k <= H) {
                 const double2 wk = cw[0], wq = cw[1], pk = cw[2], pq = cw[3];
                 if (k == 0) {
-                    const double2 z = v[rsw(0)];
-                    const double X0 = z.x + z.y, XM = z.x - z.y;
+                    const double2 z0 = v[rsw(0)];
+                    const double X0 = z0.x + z0.y, XM = z0.x - z0.y;
                     const double Y0 = X0 * pk.x, YM = XM * pq.x;
                     v[rsw(0)] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
                 } else {
@@ -3741,17 +3860,28 @@ __global__ __launch_bounds__(RotCfg<N>::TB, N <= 1024 ? 3 : 2) void k_rotate(Rot
             }
         }
         gsync<TB / 64>();
-        rot_fft<N>(v, twr, t);
         float *o = a.out + p * (size_t)a.ldo;
+        if constexpr (DIRECT) {
+            rot_fft<N, 0, false, true>(v, tw, t, z);
 #pragma unroll
-        for (int u = 0; u < NJ; ++u) {
-            const int j2 = t + u * TB;
-            if ((M / 2) % TB != 0 && j2 >= M / 2) break;
-            const double2 r0 = v[rsw(2 * j2)], r1 = v[rsw(2 * j2 + 1)];
-            const float4 y = make_float4((float)(r0.x * inv), (float)((-r0.y) * inv), (float)(r1.x * inv),
-                                         (float)((-r1.y) * inv));
-            *(float4 *)(o + 4 * j2) = y;
-            if (a.out2) *(float4 *)(a.out2 + d_ofs(p, 4 * j2, (int)a.ldo2, a.out2_tiled)) = y;
+            for (int q = 0; q < 8; ++q) {
+                const int j = t + TB * q;
+                const float2 y = make_float2((float)(z[q].x * inv), (float)((-z[q].y) * inv));
+                *(float2 *)(o + 2 * j) = y;
+                if (a.out2) *(float2 *)(a.out2 + d_ofs(p, 2 * j, (int)a.ldo2, a.out2_tiled)) = y;
+            }
+        } else {
+            rot_fft<N>(v, tw, t);
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) {
+                const int j2 = t + u * TB;
+                if ((M / 2) % TB != 0 && j2 >= M / 2) break;
+                const double2 r0 = v[rsw(2 * j2)], r1 = v[rsw(2 * j2 + 1)];
+                const float4 y = make_float4((float)(r0.x * inv), (float)((-r0.y) * inv), (float)(r1.x * inv),
+                                             (float)((-r1.y) * inv));
+                *(float4 *)(o + 4 * j2) = y;
+                if (a.out2) *(float4 *)(a.out2 + d_ofs(p, 4 * j2, (int)a.ldo2, a.out2_tiled)) = y;
+            }
         }
         gsync<TB / 64>();   // v is reused by the block's next profile
     }
@@ -4901,10 +5031,10 @@ hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
         (a.ld_in & 3) || (a.ldo & 3) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 3))) ||
         (a.amp && (!a.T64 || !a.info)) || (a.in_tiled && (a.ld_in & 31)) || (a.out2_tiled && (a.ldo2 & 31)))
         return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)std::min<size_t>(P, 16384);
 #define IC_ROT(NN)                                                                                 \
     case NN:                                                                                       \
-        IC_GGL(k_rotate<NN>, dim3(grid), dim3(RotCfg<NN>::TB), 0, st, a);              \
+        IC_GGL(k_rotate<NN>, dim3((unsigned)std::min<size_t>(cdiv(P, RotCfg<NN>::WPB), 16384 / RotCfg<NN>::WPB)), \
+               dim3(RotCfg<NN>::TB * RotCfg<NN>::WPB), 0, st, a);                                  \
         break;
     switch (a.nbin) {
         IC_ROT(64) IC_ROT(128) IC_ROT(256) IC_ROT(512) IC_ROT(1024) IC_ROT(2048) IC_ROT(4096)
