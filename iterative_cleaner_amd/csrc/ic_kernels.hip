@@ -3205,11 +3205,40 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
     const RoundList rl(a.list, a.nctr, (long)P);
     const unsigned nslot = (unsigned)rl.n();
     const uint8_t *skip = a.skip;
-    auto next_slot = [&](unsigned sl) {   // the first slot >= sl this group measures (uniform)
-        if (skip)
-            while (sl < nslot && skip[rl.at(sl)]) sl += stride;
-        return sl;
+    // The group's upcoming slots, 64 at a time: lane j of each wave holds the
+    // profile of slot wb0 + j stride (-1: past the end, or skipped), so the next
+    // profile is a ballot bit away and the list and skip reads are one batch per
+    // 64 profiles, where a dependent pair of reads per profile stalled the
+    // prefetch of the next row (list and skip passes of the fork).
+    unsigned wb0 = 0;
+    int wkk = -1;
+    unsigned long long wmask = 0;
+    auto fill = [&](unsigned b) {
+        wb0 = b;
+        const unsigned sl = b + (unsigned)lane * stride;
+        int kk = -1;
+        if (sl < nslot && sl >= b) {
+            kk = (int)rl.at(sl);
+            if (skip && skip[kk]) kk = -1;
+        }
+        wkk = kk;
+        wmask = __ballot(kk >= 0);
     };
+    auto take = [&]() -> int {   // the next profile of the group (uniform), -1 when done
+        while (wmask == 0) {
+            const unsigned nb = wb0 + 64u * stride;
+            if (nb >= nslot || nb < wb0) return -1;
+            fill(nb);
+        }
+        const int j = __builtin_ctzll(wmask);
+        wmask &= wmask - 1;
+        return __builtin_amdgcn_readlane(wkk, j);
+    };
+    // a VGPR zero: the per-profile scalars of the next profile are read by
+    // vector loads (counted on vmcnt), not scalar ones, whose lgkmcnt would be
+    // waited on by the FFT's LDS waits
+    int zv;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
     const int ca = t >> 3, cc = t & 7;
     const int jb = 128 * ca + cc;   // first sample of the thread's chain
     // byte offsets in the work array: d of chain sample q at wb[q & 3] + 64 (q & ~3)
@@ -3226,22 +3255,25 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
 #pragma unroll
         for (int q = 0; q < 16; ++q) pv[q] = pn[8 * q];
     };
-    unsigned slot = next_slot(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
-    unsigned k = slot < nslot ? (unsigned)rl.at(slot) : 0u;
+    fill(__builtin_amdgcn_readfirstlane(blockIdx.x * gpb + group));
+    int kq = take();
+    unsigned k = kq >= 0 ? (unsigned)kq : 0u;
     double nx = 0.0;
     int nst = 0, nsh = 0;
     float nw = 0.0f, nb = 0.0f;
-    if (slot < nslot) {
-        loadrow(k);
+    auto prefetch = [&](unsigned kk) {
+        loadrow(kk);
+        const unsigned kv = kk + (unsigned)zv;
         if (!closed) {
-            nx = a.amp[k];
-            nst = a.info[k];
+            nx = a.amp[kv];
+            nst = a.info[kv];
         }
-        nb = a.base[k];
-        nw = a.w0[k];
-        nsh = a.shift[k % nchan];
-    }
-    for (unsigned snext; slot < nslot; slot = snext) {
+        nb = a.base[kv];
+        nw = a.w0[kv];
+        nsh = a.shift[kk % nchan + (unsigned)zv];
+    };
+    if (kq >= 0) prefetch(k);
+    for (; kq >= 0;) {
         // multi-wave groups: keep the FFT's LDS addresses inside the loop (hoisted,
         // they spill at N >= 2048; k_diag_p2); one wave: hoisted, 118 VGPRs
         if (WPP > 1) asm volatile("" : "+v"(t));
@@ -3304,18 +3336,10 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
             for (int q = 0; q < 16; ++q) X[q] = 0.0f * w;
         }
         const unsigned kc = k;   // this profile (the prefetch below moves k on)
-        snext = next_slot(slot + stride);
-        if (snext < nslot) {
-            const unsigned kn = (unsigned)rl.at(snext);
-            k = kn;
-            loadrow(kn);
-            if (!closed) {
-                nx = a.amp[kn];
-                nst = a.info[kn];
-            }
-            nb = a.base[kn];
-            nw = a.w0[kn];
-            nsh = a.shift[kn % nchan];
+        kq = take();
+        if (kq >= 0) {
+            k = (unsigned)kq;
+            prefetch(k);
         }
         double mean = 0.0, sd = 0.0, fftv = 0.0, ptp = (double)1e20f;
         if (valid) {
