@@ -154,8 +154,10 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True,
     ic_get_run_stats); every clean of the timed region is the same work.
       k_fit_pass       every profile-sweep reads its 4*nbin-byte profile once
                        (k_fit_tail: its own sweeps, the same);
-      k_fit_state      ~2 x 204 B of lmdif state per profile of a round (the
-                       rounds' inputs are the sweeps of k_fit_pass);
+      k_fit_state      ~2 x 188 B of lmdif state per profile of a round (read
+                       and written: 18 f64 + 4 i32 fields, the sweep's 3 f64
+                       outputs and the f32 first sample; the rounds' inputs are
+                       the sweeps of k_fit_pass);
       k_chan_partials  (every template-stage launch, k_chan_delta included)
                        prepare's window pass reads the cube (4N); iteration 1's
                        pass reads it and writes the fit cube (8N exact, 4N
@@ -181,7 +183,7 @@ def algorithmic_bytes(name, nsub, nchan, nbin, launches, run, steps, exact=True,
     if name == "k_fit_tail":
         return 4 * nbin * run["fit_tail_sweeps"] * steps
     if name == "k_fit_state":
-        return 2 * 204 * run["fit_profile_sweeps"] * steps
+        return 2 * 188 * run["fit_profile_sweeps"] * steps
     if name == "k_chan_partials":
         changed = sum(int(c) for c in run["changed"][:max(0, n_iter - 1)])
         per_run = (4 * N + (8 * N if exact and not fft else 4 * N) + (8 if fft else 4) * nbin * changed
