@@ -388,11 +388,15 @@ public:
     {
         if (!comm) return -1;
         if (settle(api->GroupStart()) != ncclSuccess) return check(ncclInternalError);
+        // inside a group a non-blocking communicator may report ncclInProgress
+        // for a queued call: that is not a failure, and every peer's send and
+        // receive must still join the group (a short group would deadlock)
+        auto queued = [](ncclResult_t r) { return r == ncclSuccess || r == ncclInProgress; };
         size_t so = 0, ro = 0;
         ncclResult_t rc = ncclSuccess;
-        for (int p = 0; p < world && rc == ncclSuccess; ++p) {
+        for (int p = 0; p < world && queued(rc); ++p) {
             if (sb[p]) rc = api->Send((const char *)send + so, sb[p], ncclUint8, p, comm, st);
-            if (rc == ncclSuccess && rb[p]) rc = api->Recv((char *)recv + ro, rb[p], ncclUint8, p, comm, st);
+            if (queued(rc) && rb[p]) rc = api->Recv((char *)recv + ro, rb[p], ncclUint8, p, comm, st);
             so += sb[p];
             ro += rb[p];
         }
