@@ -3182,6 +3182,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
     using C = CLay<N>;
     constexpr int L = C::L, WPP = C::WPP, M = C::M;
     constexpr bool closed = MODE == DIAG_CLOSED;
+    constexpr bool stats = MODE == DIAG_STATS;   // X = f32(D_row * w): the rows are the residual
     constexpr bool twder = WPP > 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double2 *tw = C::TWG ? a.tw_p2 : (const double2 *)smem;
@@ -3251,7 +3252,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
     }
     float pv[16];
     auto loadrow = [&](unsigned kk) {
-        const float *pn = a.raw + (size_t)kk * N + jb;
+        const float *pn = (stats ? a.D : a.raw) + (size_t)kk * N + jb;
 #pragma unroll
         for (int q = 0; q < 16; ++q) pv[q] = pn[8 * q];
     };
@@ -3264,13 +3265,15 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
     auto prefetch = [&](unsigned kk) {
         loadrow(kk);
         const unsigned kv = kk + (unsigned)zv;
-        if (!closed) {
+        if (!closed && !stats) {
             nx = a.amp[kv];
             nst = a.info[kv];
         }
-        nb = a.base[kv];
+        if (!stats) {
+            nb = a.base[kv];
+            nsh = a.shift[kk % nchan + (unsigned)zv];
+        }
         nw = a.w0[kv];
-        nsh = a.shift[kk % nchan + (unsigned)zv];
     };
     if (kq >= 0) prefetch(k);
     for (; kq >= 0;) {
@@ -3284,7 +3287,7 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
         const int sh = ufirst(nsh);
         // template at the dedispersed index of every chain sample
         double tg[16];
-        {
+        if constexpr (!stats) {
             const double *tb = a.T2 + ((unsigned)(jb - sh) & (unsigned)(N - 1));
 #pragma unroll
             for (int q = 0; q < 16; ++q) tg[q] = tb[8 * q];
@@ -3317,14 +3320,18 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
         }
         // residual (ic.py:279-288) of the dispersed-frame sample j, f32 store
         // (:272), apply_weights (:296): X_j = f32(f32(x T_i - D_i) * w), D_i = f32(raw_j - base0)
-        const bool ok = st >= 1 && st <= 4;
+        const bool ok = stats || (st >= 1 && st <= 4);
         const bool valid = w != 0.0f;
         float X[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const float pj = pv[q] - bk;
-            const double e = x * tg[q] - (double)pj;
-            X[q] = (float)e;
+            if constexpr (stats) {
+                X[q] = pv[q];
+            } else {
+                const float pj = pv[q] - bk;
+                const double e = x * tg[q] - (double)pj;
+                X[q] = (float)e;
+            }
         }
         if (w != 1.0f) {   // fractional weights (w * 1 = w exactly: skipped)
 #pragma unroll
@@ -4895,6 +4902,8 @@ static hipError_t launch_cl(hipStream_t st, const DiagArgs &a, size_t P)
     const unsigned grid = (unsigned)std::min<size_t>((P + gpb - 1) / gpb, 4096);
     if (a.mode == DIAG_EXACT)
         IC_GGL((k_diag_cl<NN, DIAG_EXACT>), dim3(grid), dim3(C::L * gpb), shm, st, a);
+    else if (a.mode == DIAG_STATS)
+        IC_GGL((k_diag_cl<NN, DIAG_STATS>), dim3(grid), dim3(C::L * gpb), shm, st, a);
     else
         IC_GGL((k_diag_cl<NN, DIAG_CLOSED>), dim3(grid), dim3(C::L * gpb), shm, st, a);
     return hipGetLastError();
@@ -4902,8 +4911,11 @@ static hipError_t launch_cl(hipStream_t st, const DiagArgs &a, size_t P)
 
 static bool uses_cl(const DiagArgs &a)
 {
-    return (a.mode == DIAG_EXACT || a.mode == DIAG_CLOSED) && a.T2 && a.raw && a.base && !a.pr_on && !a.data_f64 &&
-           (a.nbin == 1024 || a.nbin == 2048 || a.nbin == 4096) && a.chain;
+    if (!a.chain || a.data_f64 || !(a.nbin == 1024 || a.nbin == 2048 || a.nbin == 4096)) return false;
+    // STATS: row-major residual rows (the FFT mode's rotated residual; the
+    // pulse region was applied when they were formed)
+    if (a.mode == DIAG_STATS) return a.D && a.ldD == a.nbin && !a.dtiled;
+    return (a.mode == DIAG_EXACT || a.mode == DIAG_CLOSED) && a.T2 && a.raw && a.base && !a.pr_on;
 }
 
 // profile lists / skips: k_diag_cl, and k_diag_p2 in the exact mode and on
