@@ -3762,6 +3762,18 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         const unsigned c = (unsigned)(item / nsub), s = (unsigned)(item % nsub);
         const size_t p = (size_t)s * nchan + c;
         if (skip(p, s)) continue;
+        const __amdgpu_buffer_rsrc_t phr = rot_rsrc(a.ph + (size_t)c * (M + 1), M + 1);
+        // the post step's phasors one round ahead: the first round's are
+        // requested with the rows, each later round's before the round before it
+        auto ldph = [&](int u, double2 (&pp)[2]) {
+            const int k = t + u * TB;
+            if (k <= H) {
+                pp[0] = rot_ld(phr, 16u * (unsigned)k, 0);
+                pp[1] = rot_ld(phr, 16u * (unsigned)(M - k), 0);
+            }
+        };
+        double2 phn[2];
+        ldph(0, phn);
         double2 z[8];
         if constexpr (DIRECT) {
             const size_t k = p;
@@ -3853,25 +3865,23 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         gsync<TB / 64>();
         rot_fft<N>(v, tw, t);
         }
-        const __amdgpu_buffer_rsrc_t phr = rot_rsrc(a.ph + (size_t)c * (M + 1), M + 1);
-        // the post step's twiddles and phasors, loaded at their use (a pair ahead:
-        // no faster at 3 or 4 waves per SIMD)
-        auto ld = [&](int u, double2 (&w4)[4]) {
+        // the post step's twiddles, at their use
+        auto ld = [&](int u, double2 (&w2)[2]) {
             const int k = t + u * TB;
             if (k <= H) {
-                w4[0] = tw.post((unsigned)(k & (M - 1)));
-                w4[1] = tw.post((unsigned)((M - k) & (M - 1)));
-                w4[2] = rot_ld(phr, 16u * (unsigned)k, 0);
-                w4[3] = rot_ld(phr, 16u * (unsigned)(M - k), 0);
+                w2[0] = tw.post((unsigned)(k & (M - 1)));
+                w2[1] = tw.post((unsigned)((M - k) & (M - 1)));
             }
         };
-        double2 cw[4];
+        double2 cw[2];
 #pragma unroll
         for (int u = 0; u < NK; ++u) {
             ld(u, cw);
+            const double2 pk = phn[0], pq = phn[1];
+            if (u + 1 < NK) ldph(u + 1, phn);
             const int k = t + u * TB;
             if (k <= H) {
-                const double2 wk = cw[0], wq = cw[1], pk = cw[2], pq = cw[3];
+                const double2 wk = cw[0], wq = cw[1];
                 if (k == 0) {
                     const double2 z0 = v[rsw(0)];
                     const double X0 = z0.x + z0.y, XM = z0.x - z0.y;
