@@ -491,7 +491,14 @@ def main():
     backend = os.environ.get("IC_BENCH_BACKEND", "nccl")
     # channel shards over "nccl" use the library's native RCCL transport;
     # IC_BENCH_TRANSPORT=torch keeps the torch.distributed callbacks (A/B)
-    native_rccl = backend == "nccl" and os.environ.get("IC_BENCH_TRANSPORT", "rccl") == "rccl"
+    # IC_BENCH_RCCL_LIBRARY=path (rehearsal only): the native transport loads that
+    # librccl instead (ic_rccl_set_library), e.g. the test stub
+    # tests/stub_rccl/libstubrccl.so, which lets N ranks share one GPU under
+    # IC_BENCH_BACKEND=gloo and still run the exact code path of the N-GPU line
+    rccl_lib = os.environ.get("IC_BENCH_RCCL_LIBRARY")
+    if rccl_lib:
+        _native.rccl_set_library(rccl_lib)
+    native_rccl = (backend == "nccl" or bool(rccl_lib)) and os.environ.get("IC_BENCH_TRANSPORT", "rccl") == "rccl"
     native_error, transport_note = None, None
     gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(gpu)
@@ -531,7 +538,8 @@ def main():
                 sess = _native.ShardSession(nsub, nchan, nbin, rank, world, rccl_id=share_rccl_id(), **kw)
             except _native.NativeError as e:
                 native_error = str(e)[:200]
-            ok = torch.tensor([1 if sess is not None else 0], dtype=torch.int32, device=dev)
+            ok = torch.tensor([1 if sess is not None else 0], dtype=torch.int32,
+                              device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             if int(ok.item()) == 0:
                 if sess is not None:
@@ -730,6 +738,8 @@ def main():
                           "3 all-gathers of owner results, 1 all-reduce; %s)" % (
                               world, "native RCCL communicator, collectives issued from C++" if native_rccl
                               else (transport_note or "torch.distributed callbacks"))
+            if rccl_lib:
+                parallelism += " [rehearsal: librccl = %s, process group %s]" % (os.path.basename(rccl_lib), backend)
         else:
             parallelism = "replicas" if world > 1 else "single"
         rec = {
