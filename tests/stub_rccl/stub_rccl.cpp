@@ -14,7 +14,7 @@
 // synchronised, its payload copied device -> shared memory, the peers'
 // payloads shared memory -> device (so the data path is host-staged, not
 // xGMI; only the semantics are RCCL's).  Each rank owns an outbox of
-// kOutbox bytes; a collective waits until every rank finished reading the
+// outbox bytes (32 MiB, or IC_STUB_RCCL_OUTBOX_MB, the same on every rank); a collective waits until every rank finished reading the
 // previous one before it overwrites its outbox.
 //
 // Failures propagate as they would have to for the library's error paths to
@@ -44,7 +44,7 @@
 namespace {
 
 constexpr int kMaxRanks = 16;
-constexpr size_t kOutbox = 32ull << 20;   // bytes a rank may send per collective
+constexpr size_t kOutboxDefault = 32ull << 20;   // bytes a rank may send per collective
 constexpr double kWaitSeconds = 120.0;
 
 struct Header {
@@ -62,7 +62,8 @@ struct Header {
 
 struct ncclComm {
     Header *h = nullptr;
-    char *box = nullptr;   // outboxes, kOutbox bytes per rank
+    char *box = nullptr;   // outboxes, `outbox` bytes per rank
+    size_t outbox = kOutboxDefault;
     size_t map_bytes = 0;
     int rank = 0, n = 0;
     uint64_t seq = 0;
@@ -153,7 +154,7 @@ ncclResult_t await_pub(ncclComm_t c, int p, uint64_t seq)
 
 void finish(ncclComm_t c, uint64_t seq) { c->h->done[c->rank].store(seq, std::memory_order_release); }
 
-char *outbox(ncclComm_t c, int p) { return c->box + (size_t)p * kOutbox; }
+char *outbox(ncclComm_t c, int p) { return c->box + (size_t)p * c->outbox; }
 
 size_t type_size(ncclDataType_t t)
 {
@@ -180,7 +181,7 @@ ncclResult_t group_end_ops(std::vector<Op> &ops)
     for (auto &o : ops) {
         if (!o.send) continue;
         if (c->h->len[c->rank][o.peer] != 0) return ncclInvalidUsage;   // one send per peer per group
-        if (pos + o.bytes > kOutbox) return ncclInvalidArgument;
+        if (pos + o.bytes > c->outbox) return ncclInvalidArgument;
         if (o.bytes && hipMemcpy(outbox(c, c->rank) + pos, o.buf, o.bytes, hipMemcpyDeviceToHost) != hipSuccess)
             return ncclUnhandledCudaError;
         c->h->off[c->rank][o.peer] = pos;
@@ -237,7 +238,11 @@ ncclResult_t ncclCommInitRankConfig(ncclComm_t *out, int nranks, ncclUniqueId id
     c->n = nranks;
     c->blocking = config && config->blocking == 0 ? 0 : 1;
     shm_name(id, c->name);
-    c->map_bytes = sizeof(Header) + (size_t)nranks * kOutbox;
+    if (const char *mb = getenv("IC_STUB_RCCL_OUTBOX_MB")) {   // test stub only
+        const long v = atol(mb);
+        if (v > 0 && v <= 4096) c->outbox = (size_t)v << 20;
+    }
+    c->map_bytes = sizeof(Header) + (size_t)nranks * c->outbox;
     const int fd = shm_open(c->name, O_CREAT | O_RDWR, 0600);
     if (fd < 0) {
         delete c;
@@ -353,7 +358,7 @@ ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataT
                            hipStream_t st)
 {
     const size_t bytes = count * type_size(t);
-    if (!c || bytes == 0 || bytes > kOutbox) return ncclInvalidArgument;
+    if (!c || bytes == 0 || bytes > c->outbox) return ncclInvalidArgument;
     uint64_t seq;
     if (ncclResult_t r = begin(c, st, &seq)) return r;
     if (hipMemcpy(outbox(c, c->rank), send, bytes, hipMemcpyDeviceToHost) != hipSuccess) return ncclUnhandledCudaError;
@@ -372,7 +377,7 @@ ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataT
 {
     if (!c || t != ncclInt32 || op != ncclSum) return ncclInvalidArgument;   // what RcclComm uses
     const size_t bytes = count * sizeof(int32_t);
-    if (bytes == 0 || bytes > kOutbox) return ncclInvalidArgument;
+    if (bytes == 0 || bytes > c->outbox) return ncclInvalidArgument;
     uint64_t seq;
     if (ncclResult_t r = begin(c, st, &seq)) return r;
     if (hipMemcpy(outbox(c, c->rank), send, bytes, hipMemcpyDeviceToHost) != hipSuccess) return ncclUnhandledCudaError;
