@@ -42,6 +42,10 @@ public:
     virtual void abort() {}
     // the transport lost a peer after the fact (RCCL's asynchronous errors)
     virtual bool remote_error() { return false; }
+    // longest wait of the transport's own host-side polling (RcclComm: a
+    // non-blocking call reported in progress), ms; the session's
+    // IC_OPT_SYNC_TIMEOUT_MS
+    virtual void set_timeout_ms(long long) {}
 };
 
 Comm *make_callback_comm(const ic_comm_ops &ops, int rank, int world);

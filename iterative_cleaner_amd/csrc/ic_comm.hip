@@ -294,10 +294,16 @@ RcclApi *rccl_api(std::string *err)
             paths.push_back(g_rccl_path);
         else
             paths = {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"};
-        for (const auto &p : paths)
+        // dlerror() clears its message: read it once per failed dlopen, and
+        // report every file tried with its own reason
+        std::string why;
+        for (const auto &p : paths) {
             if ((g_api.h = dlopen(p.c_str(), RTLD_NOW | RTLD_LOCAL))) break;
+            const char *de = dlerror();
+            why += (why.empty() ? "" : "; ") + p + ": " + (de ? de : "?");
+        }
         if (!g_api.h) {
-            g_api.err = "dlopen of " + paths[0] + " failed: " + std::string(dlerror() ? dlerror() : "?");
+            g_api.err = "dlopen failed (" + why + ")";
         } else {
 #define SYM(F)                                                   \
     if (g_api.err.empty()) {                                     \
@@ -418,6 +424,7 @@ public:
     }
     // a failure RCCL detected asynchronously (a peer's connection lost): the
     // session's host waits poll this between their event queries
+    void set_timeout_ms(long long ms) override { timeout_ms = ms; }
     bool remote_error() override
     {
         if (!comm) return aborted;
@@ -430,8 +437,12 @@ private:
     RcclApi *api = nullptr;
     ncclComm_t comm = nullptr;
     bool aborted = false;
+    long long timeout_ms = 600000;
     // a non-blocking communicator's call may return ncclInProgress: wait for
-    // its state to settle (enqueueing on the stream takes microseconds)
+    // its state to settle.  Enqueueing takes microseconds, but a grouped
+    // send / receive may stay in progress until its peer reaches the same
+    // exchange, so the wait is bounded by the session's own host-wait limit
+    // (IC_OPT_SYNC_TIMEOUT_MS, set_timeout_ms), not by a fixed figure.
     ncclResult_t settle(ncclResult_t rc)
     {
         if (rc != ncclInProgress) return rc;
@@ -440,7 +451,8 @@ private:
             ncclResult_t st = ncclSuccess;
             if (api->CommGetAsyncError(comm, &st) != ncclSuccess) return ncclInternalError;
             if (st != ncclInProgress) return st;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return ncclInternalError;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+                return ncclInternalError;
             std::this_thread::yield();
         }
     }

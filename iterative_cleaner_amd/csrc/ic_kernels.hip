@@ -1658,7 +1658,9 @@ __global__ __launch_bounds__(64) void k_fit_pass(const float *__restrict__ D, co
         ie.A = exA;
         ie.B = exB;
         ExactBody body(ie, T64, agiant);
-        sweep_dma(dt, nsw, body);
+        // the early tile pair is still pending when no fast sweep consumed it
+        const bool fast_ran = R0 ? anyA : (anyA || anyB);
+        sweep_dma(dt, nsw, body, !fast_ran);
         if (exA || exB) {
             if (exA) o.p0 = body.p00;
             o.sum = body.sum;
@@ -1875,8 +1877,12 @@ __global__ __launch_bounds__(BS) void k_fit_state(FitStateArrays S, long P, cons
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned fin = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (fin == (unsigned)nblk - 1) {
-            // (the last block only: an acquire orders its load of ctr after every
-            // block's offset atomic in the memory model too, not just on the hardware)
+            // (the last block only.  What makes its load of ctr see every
+            // block's offset atomic is the hardware order above: each block's
+            // returning offset atomic, then its vmcnt(0), then its count.  The
+            // counts are relaxed - no release pairs with this acquire - so the
+            // acquire fence only keeps the compiler and the L1 from serving the
+            // load early; it is not a memory-model synchronisation.)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const unsigned long long v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(host_n, (int32_t)((v & 0xffffffffull) + (v >> 32)), __ATOMIC_RELEASE,

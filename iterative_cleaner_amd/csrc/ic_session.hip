@@ -1084,6 +1084,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         int ccode = IC_EINVAL;
         s->comm = make_comm(&cerr, &ccode);
         if (!s->comm) return bail(fail(ccode, "shard transport: %s", cerr.empty() ? "failed" : cerr.c_str()));
+        s->comm->set_timeout_ms((long long)(s->sync_timeout_s * 1000.0 + 0.5));
         const size_t nchan_g = (size_t)p.nchan;
         AL(s->std_r, (size_t)s->rows_own * nchan_g);
         AL(s->mean_r, (size_t)s->rows_own * nchan_g);
@@ -1817,6 +1818,7 @@ int ic_set_option(void *session, int option, int64_t v)
     case IC_OPT_SYNC_TIMEOUT_MS:
         if (v < 1) return fail(IC_EINVAL, "IC_OPT_SYNC_TIMEOUT_MS=%lld < 1", (long long)v);
         s->sync_timeout_s = (double)v / 1000.0;
+        if (s->comm) s->comm->set_timeout_ms((long long)v);
         return IC_OK;
     case IC_OPT_FIT_SCHEDULE:
         // the persistent lanes schedule (round 4, measured slower than the

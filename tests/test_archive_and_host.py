@@ -228,3 +228,29 @@ def test_schedule_options_match_header_and_no_environment_knobs():
     assert lib.ic_set_option(None, 1, 0) == -1
     v = ctypes.c_int64()
     assert lib.ic_get_option(None, 1, ctypes.byref(v)) == -1
+
+
+def test_rccl_missing_library_is_an_error_code_not_a_crash():
+    """ic_rccl_set_library on a file that does not exist: ic_rccl_unique_id
+    returns IC_ECOMM with the failing path in the message (the
+    dlerror() message used to be read twice, the second read a null
+    std::string, an exception through the C-ABI).  A fresh process, because
+    the library load is process-wide."""
+    code = (
+        "import ctypes, sys\n"
+        "sys.path.insert(0, %r)\n"
+        "from iterative_cleaner_amd import _native\n"
+        "lib = _native.load_library()\n"
+        "assert lib.ic_rccl_set_library(b'/nonexistent/dir/librccl_missing.so') == 0\n"
+        "buf = ctypes.create_string_buffer(128)\n"
+        "rc = lib.ic_rccl_unique_id(ctypes.cast(buf, ctypes.c_void_p))\n"
+        "msg = lib.ic_last_error()\n"
+        "assert rc == -5, rc\n"
+        "assert b'/nonexistent/dir/librccl_missing.so' in msg, msg\n"
+        "rc2 = lib.ic_rccl_unique_id(ctypes.cast(buf, ctypes.c_void_p))\n"
+        "assert rc2 == -5, rc2\n"
+        "print('ok')\n" % REPO)
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout, r.stderr)
