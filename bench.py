@@ -469,9 +469,10 @@ def main():
                          "(profiling passes, whose kernel tallies it would mix in)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="a session schedule option (_native.OPTIONS; same bits under every setting), repeatable")
-    ap.add_argument("--dedisp", choices=("shift", "fft"), default="shift",
+    ap.add_argument("--dedisp", choices=("shift", "fft", "fft_pp"), default="shift",
                     help="shift: integer dedispersion shifts (default); fft: fractional delays, dedispersed by "
-                         "psrchive's FFT phase rotation (dedisp_mode IC_DEDISP_FFT)")
+                         "psrchive's FFT phase rotation (dedisp_mode IC_DEDISP_FFT); fft_pp: the same with one "
+                         "delay per profile (psrchive's per-Integration folding period, ic_set_delays2)")
     a = ap.parse_args()
 
     import torch
@@ -520,12 +521,15 @@ def main():
     if a.dedisp == "fft":
         from iterative_cleaner_amd import synth
         delay = synth.fractional_delays(np.arange(nchan) % 7, nbin)   # the generators' integer shifts + fractions
+    elif a.dedisp == "fft_pp":
+        from iterative_cleaner_amd import synth
+        delay = synth.per_profile_delays(np.arange(nchan) % 7, nbin, nsub)
     if sharded:
         chans, _ = _native.shard_layout(nsub, nchan, world)
         c0, c1 = chans[rank]
         cube, w0, shift = make_block_cube_device(nsub, nchan, nbin, seed, rfi, c0, c1, dev)
         comm = TorchComm(dev)
-        kw = dict(max_iter=5, device=local, fit_mode=fit_mode, delay=None if delay is None else delay[c0:c1])
+        kw = dict(max_iter=5, device=local, fit_mode=fit_mode, delay=None if delay is None else delay[..., c0:c1])
         sess = None
         if native_rccl:
             # the library's own RCCL communicator: every exchange issued from C++
@@ -674,7 +678,7 @@ def main():
         if fit_mode == _native.FIT_CLOSED:
             wl_key += "/closed"
         if delay is not None:
-            wl_key += "/fft"
+            wl_key += "/" + a.dedisp
         traffic, src = pmc_traffic(wl_key, dom)
         valu, vsrc = pmc_valu(wl_key)
         hbm = {"achieved": round(hbm_s8d, 1) if hbm_s8d else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -752,7 +756,9 @@ def main():
                                    % (workload, nsub, nchan, nbin,
                                       "exact leastsq fit" if fit_mode == _native.FIT_EXACT else
                                       "closed-form fit (fit_mode 1: fast mode, not the reference's arithmetic)")
-                                   + (", fractional dedispersion (FFT phase rotation)" if delay is not None else ""),
+                                   + (", fractional dedispersion (FFT phase rotation%s)"
+                                      % (", per-profile delays" if a.dedisp == "fft_pp" else "")
+                                      if delay is not None else ""),
                        "fit_mode": a.fit_mode, "dedisp": a.dedisp,
                        "profiles_per_archive": nsub * nchan, "loops": loops[-1], "iterations": n_iter,
                        "fit_rounds": stats["fit_rounds"],

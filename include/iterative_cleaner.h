@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define IC_ABI_VERSION 7
+#define IC_ABI_VERSION 8
 
 #define IC_OK 0
 #define IC_EINVAL -1   /* bad argument / shape                         */
@@ -61,6 +61,13 @@ typedef struct {
                                   sum and ptp, ptp scaled in f64.  The samples must
                                   still be f32 values (the archive's amplitudes).  */
     int32_t dedisp_mode;       /* IC_DEDISP_SHIFT (default) or IC_DEDISP_FFT       */
+    int32_t input_dedispersed; /* 1: the uploaded cube is the archive as stored
+                                  DEDISPERSED (psrchive get_dedispersed()): the
+                                  reference's dedisperse (:91, :100) is then a
+                                  no-op and only the residual's dededisperse (:104)
+                                  rotates.  IC_DEDISP_FFT only (with integer shifts
+                                  the host rolls the cube back to the dispersed
+                                  frame, which is exact); 0 otherwise.            */
 } ic_params;
 
 /* ic_params.fit_mode.
@@ -82,9 +89,11 @@ typedef struct {
  * :100, :104) move a channel's samples.
  *   IC_DEDISP_SHIFT  integer rotation by shift[c] bins (ded[i] = raw[(i+shift)%nbin]),
  *                    the archive stand-in's default.
- *   IC_DEDISP_FFT    psrchive's FFT phase rotation by a fractional delay of
- *                    delay[c] bins (ic_set_delays): forward real FFT, harmonic k
- *                    times exp(+-2 pi i k delay / nbin), inverse real FFT, in the
+ *   IC_DEDISP_FFT    psrchive's FFT phase rotation by a fractional delay
+ *                    (ic_set_delays: delay[c] bins per channel; ic_set_delays2:
+ *                    delay[s][c] per profile, psrchive's per-Integration folding
+ *                    period): forward real FFT, harmonic k times
+ *                    exp(+-2 pi i k delay / nbin), inverse real FFT, in the
  *                    arithmetic order written in iterative_cleaner_amd/
  *                    phase_rotation.py (bit-identical to it and to the C oracle;
  *                    within one f32 ulp of numpy's irfft(rfft(x) * phasor);
@@ -150,12 +159,23 @@ int ic_run(void *session, double *test_out, float *weights_out, int32_t *loops_o
  * dedisperse moves sample j + delay to j.  Required before ic_run; kept until
  * changed. */
 int ic_set_delays(void *session, const double *delay_bins);
+/* The same with one delay per profile: delay_bins [nsub*nchan] f64 (a shard:
+ * [nsub][nchan_loc]), profile (s, c) at s*nchan + c — psrchive dedisperses each
+ * Integration with its own folding period (delay_s,c = DM delay of channel c /
+ * period_s * nbin).  The phasors exp(2 pi i k delay / nbin) are then evaluated
+ * per profile on the device by the same f64 formula the channel table uses, so
+ * rows that are all equal give exactly ic_set_delays' results (and take its
+ * table). */
+int ic_set_delays2(void *session, const double *delay_bins);
 
 /* dedisperse (sign +1) or dededisperse (sign -1) a cube [nsub][nchan][nbin] f32
  * by the FFT phase rotation on the GPU (the operation IC_DEDISP_FFT applies at
  * iterative_cleaner.py:91/:100/:104).  Synchronous; in and out may alias. */
 int ic_rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, const double *delay_bins,
                        int sign, float *out);
+/* The same with per-profile delays delay_bins [nsub*nchan] (ic_set_delays2). */
+int ic_rotate_profiles2(int device, int nsub, int nchan, int nbin, const float *in, const double *delay_bins,
+                        int sign, float *out);
 
 /* The last iteration's residual cube (:101-108), dispersed frame, unweighted,
  * f32 [nsub][nchan][nbin] — what --unload_res writes (:161-162). */

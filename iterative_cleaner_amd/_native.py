@@ -13,7 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # IC_LIBRARY: an alternative build of the same library (A/B measurements)
 LIB_PATH = os.environ.get("IC_LIBRARY") or os.path.join(HERE, "libicgpu.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # symbols exported by libicgpu.so, as declared in include/iterative_cleaner.h
 EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session_destroy",
@@ -25,7 +25,8 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
            "ic_upload_pols", "ic_comprehensive_stats", "ic_get_bad_fits",
            "ic_fit_profiles", "ic_get_diagnostics_f64", "ic_set_delays", "ic_rotate_profiles",
            "ic_set_timing_kernel", "ic_set_option", "ic_get_option", "ic_comprehensive_stats_rowstat",
-           "ic_rccl_unique_id", "ic_session_create_rccl", "ic_rccl_set_library", "ic_rccl_set_init_timeout")
+           "ic_rccl_unique_id", "ic_session_create_rccl", "ic_rccl_set_library", "ic_rccl_set_init_timeout",
+           "ic_set_delays2", "ic_rotate_profiles2")
 
 # session schedule options (ic_set_option; include/iterative_cleaner.h): they
 # choose how the loop is scheduled, never its arithmetic
@@ -49,7 +50,8 @@ class Params(C.Structure):
                 ("max_iter", C.c_int32), ("chanthresh", C.c_double),
                 ("subintthresh", C.c_double), ("pr_on", C.c_int32), ("pr_factor", C.c_double),
                 ("pr_start", C.c_int32), ("pr_end", C.c_int32), ("baseline_duty", C.c_double),
-                ("fit_mode", C.c_int32), ("data_f64", C.c_int32), ("dedisp_mode", C.c_int32)]
+                ("fit_mode", C.c_int32), ("data_f64", C.c_int32), ("dedisp_mode", C.c_int32),
+                ("input_dedispersed", C.c_int32)]
 
 
 class RunStats(C.Structure):
@@ -155,7 +157,9 @@ def load_library(path: str = LIB_PATH):
     lib.ic_get_bad_fits.argtypes = [vp, vp, C.c_int]
     lib.ic_fit_profiles.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp]
     lib.ic_set_delays.argtypes = [vp, vp]
+    lib.ic_set_delays2.argtypes = [vp, vp]
     lib.ic_rotate_profiles.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp]
+    lib.ic_rotate_profiles2.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp]
     lib.ic_comprehensive_stats.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_double, C.c_double,
                                            vp, vp, vp, vp, vp]
     lib.ic_comprehensive_stats_rowstat.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_double,
@@ -195,7 +199,7 @@ class GpuSession:
 
     def __init__(self, nsub, nchan, nbin, max_iter=5, chanthresh=5.0, subintthresh=5.0,
                  pulse_region=(0, 0, 1), baseline_duty=0.15, device=0, fit_mode=FIT_EXACT, data_f64=False,
-                 delay=None, options=None):
+                 delay=None, options=None, input_dedispersed=False):
         self.lib = load_library()
         self.shape = (int(nsub), int(nchan), int(nbin))
         self.max_iter = int(max_iter)
@@ -203,7 +207,8 @@ class GpuSession:
         on, fac, a, b = normalise_pulse_region(list(pulse_region), int(nbin))
         self.params = Params(int(nsub), int(nchan), int(nbin), int(max_iter), float(chanthresh),
                              float(subintthresh), on, fac, a, b, float(baseline_duty), self.fit_mode,
-                             1 if data_f64 else 0, DEDISP_SHIFT if delay is None else DEDISP_FFT)
+                             1 if data_f64 else 0, DEDISP_SHIFT if delay is None else DEDISP_FFT,
+                             1 if input_dedispersed else 0)
         self.data_f64 = bool(data_f64)
         h = C.c_void_p()
         rc = self._create(int(device), h)
@@ -219,10 +224,16 @@ class GpuSession:
         self.set_delays(delay)
 
     def set_delays(self, delay):
-        """Fractional per-channel delays in bins (this session's channels) of a
-        session created with `delay` (dedisp_mode IC_DEDISP_FFT)."""
-        d = np.ascontiguousarray(delay, dtype=np.float64).reshape(self.shape[1])
-        self._check(self.lib.ic_set_delays(self.h, _ptr(d)), "ic_set_delays")
+        """Fractional delays in bins of a session created with `delay`
+        (dedisp_mode IC_DEDISP_FFT), for this session's channels: (nchan,) per
+        channel (ic_set_delays) or (nsub, nchan) per profile (ic_set_delays2)."""
+        nsub, nchan = self.shape[0], self.shape[1]
+        if np.ndim(delay) == 2:
+            d = np.ascontiguousarray(delay, dtype=np.float64).reshape(nsub, nchan)
+            self._check(self.lib.ic_set_delays2(self.h, _ptr(d)), "ic_set_delays2")
+        else:
+            d = np.ascontiguousarray(delay, dtype=np.float64).reshape(nchan)
+            self._check(self.lib.ic_set_delays(self.h, _ptr(d)), "ic_set_delays")
 
     _create_name = "ic_session_create"
 
@@ -403,17 +414,24 @@ def fit_profiles(profiles, template, fit_mode=FIT_EXACT, device=0):
 
 def rotate_profiles(cube, delay, sign=1, device=0):
     """Fractional dedispersion of a (nsub, nchan, nbin) cube on the GPU: the FFT
-    phase rotation by +delay (sign 1, dedisperse) or -delay (sign -1)."""
+    phase rotation by +delay (sign 1, dedisperse) or -delay (sign -1); delay
+    (nchan,) per channel (ic_rotate_profiles) or (nsub, nchan) per profile
+    (ic_rotate_profiles2)."""
     lib = load_library()
     cube = np.ascontiguousarray(cube, dtype=np.float32)
     if cube.ndim != 3:
         raise ValueError("rotate_profiles: cube must be (nsub, nchan, nbin)")
     nsub, nchan, nbin = cube.shape
-    d = np.ascontiguousarray(delay, dtype=np.float64).reshape(nchan)
     out = np.empty_like(cube)
-    rc = lib.ic_rotate_profiles(int(device), nsub, nchan, nbin, _ptr(cube), _ptr(d), int(sign), _ptr(out))
+    if np.ndim(delay) == 2:
+        d = np.ascontiguousarray(delay, dtype=np.float64).reshape(nsub, nchan)
+        fn, name = lib.ic_rotate_profiles2, "ic_rotate_profiles2"
+    else:
+        d = np.ascontiguousarray(delay, dtype=np.float64).reshape(nchan)
+        fn, name = lib.ic_rotate_profiles, "ic_rotate_profiles"
+    rc = fn(int(device), nsub, nchan, nbin, _ptr(cube), _ptr(d), int(sign), _ptr(out))
     if rc != 0:
-        raise NativeError("ic_rotate_profiles: %s (rc=%d)" % (_err(lib), rc))
+        raise NativeError("%s: %s (rc=%d)" % (name, _err(lib), rc))
     return out
 
 

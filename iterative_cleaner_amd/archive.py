@@ -17,9 +17,12 @@ order so that the HIP kernels can reproduce it bit-for-bit:
   pol 0 (= I) for Stokes data; the state becomes "Intensity";
 * ``dedisperse``/``dededisperse``: integer per-channel rotation by
   ``dm_shift[c]`` bins, ``ded[i] = raw[(i + shift) % nbin]``; an archive made
-  with fractional delays ``dm_delay[c]`` (f64 bins) rotates instead by
-  psrchive's FFT phase rotation, in the arithmetic order written in
-  :mod:`.phase_rotation` (power-of-two nbin);
+  with fractional delays ``dm_delay`` (f64 bins: ``[c]`` per channel, or
+  ``[s, c]`` per profile - psrchive's per-Integration folding period) rotates
+  instead by psrchive's FFT phase rotation, in the arithmetic order written in
+  :mod:`.phase_rotation` (power-of-two nbin); an archive stored dedispersed
+  (``dedispersed=True``) returns its samples as they are from the dedispersed
+  view, and only ``dededisperse`` moves them;
 * channel sums (baseline total, fscrunch) use the CANONICAL CHANNEL ORDER
   (:func:`chan_sum`): f64, sequential inside super-blocks of ``SUPER_BLOCK``
   channels; the super-block partials are combined by the halving tree of
@@ -174,7 +177,8 @@ class Archive:
             from .phase_rotation import is_supported
             if not is_supported(nbin):
                 raise ValueError("fractional dedispersion needs a power-of-two nbin (got %d)" % nbin)
-            self._delay = np.array(dm_delay, dtype=np.float64).reshape(nchan)
+            d = np.array(dm_delay, dtype=np.float64)
+            self._delay = d.reshape((nsub, nchan) if d.ndim == 2 else (nchan,))
         self._dedispersed = bool(dedispersed)
         self._filename = filename
         self._source = source
@@ -207,13 +211,14 @@ class Archive:
         return self._shift.copy()
 
     def get_dm_delay(self):
-        """Fractional per-channel delays in bins (f64), or None for an archive
-        dedispersed by integer shifts."""
+        """Fractional delays in bins (f64; (nchan,) per channel or (nsub, nchan)
+        per profile), or None for an archive dedispersed by integer shifts."""
         return None if self._delay is None else self._delay.copy()
 
     def _rotate(self, data: np.ndarray, sign: int) -> np.ndarray:
         from .phase_rotation import phasors, rotate
-        return rotate(data, phasors(self.get_nbin(), self._delay), sign)
+        d = self._delay if self._delay.ndim == 1 else self._delay[:, None, :]   # over (nsub, npol, nchan)
+        return rotate(data, phasors(self.get_nbin(), d), sign)
 
     def get_dedispersed(self) -> bool:
         return self._dedispersed
@@ -330,6 +335,8 @@ class Archive:
             prof = np.where(wt[None, :, None] != 0.0, num / wt[None, :, None], 0.0)
         self._data = np.ascontiguousarray(prof.astype(np.float32)[None])
         self._weights = wt.astype(np.float32)[None, :]
+        if self._delay is not None and self._delay.ndim == 2:
+            self._delay = self._delay[:1]
 
     # ---------------------------------------------------------------- I/O
     def unload(self, path: str) -> None:

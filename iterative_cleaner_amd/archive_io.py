@@ -10,7 +10,7 @@ Two formats:
 * otherwise an uncompressed ``.npz`` container (no pickles) holding ``data``
   (nsub, npol, nchan, nbin) f32, ``weights`` (nsub, nchan) f32, ``dm_shift``
   (nchan,) i64, ``dedispersed`` (bool scalar), a JSON ``meta`` string and,
-  for an archive with fractional delays, ``dm_delay`` (nchan,) f64.
+  for an archive with fractional delays, ``dm_delay`` (nchan,) or (nsub, nchan) f64.
 
 The extension of the path is kept as given (``*.ar`` works for both).
 """
@@ -103,7 +103,7 @@ def load(path: str, channels=None) -> Archive:
             raise ValueError("%s: channel range %s outside [0, %d)" % (path, (c0, c1), nchan_total))
         data = _npz_member(path, "data", (c0, c1))
         weights, shift = weights[:, c0:c1], shift[c0:c1]
-        delay = None if delay is None else delay[c0:c1]
+        delay = None if delay is None else delay[..., c0:c1]
     ar = Archive(data, weights, shift, dedispersed=dedispersed, filename=path, dm_delay=delay,
                  source=meta.get("source", "J0000+0000"),
                  centre_frequency=meta.get("centre_frequency", 1400.0),

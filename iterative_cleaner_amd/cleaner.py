@@ -114,30 +114,42 @@ def _load_shard(backend, arch, rank, world):
     return backend.Archive_load(arch)
 
 
-def _dm_shift(ar) -> np.ndarray:
-    """Per-channel dedispersion delay in bins (ded[i] = raw[(i+shift)%nbin])."""
+def _dedispersion(ar):
+    """(shift, delay) of the archive's dedisperse / dededisperse
+    (iterative_cleaner.py:91, :100, :104): integer shifts in bins
+    (ded[i] = raw[(i+shift)%nbin]) with delay None, or zero shifts and the
+    fractional delays in bins of psrchive's FFT phase rotation, (nchan,) or
+    (nsub, nchan).  The archive stand-in states its own (get_dm_shift /
+    get_dm_delay); any other archive (real psrchive) gets psrchive's delays from
+    its DM, channel frequencies and per-Integration folding periods
+    (dedispersion.py), integer only when every delay is integral, and an error
+    where the fractional rotation cannot serve its nbin."""
     if hasattr(ar, "get_dm_shift"):
-        return np.asarray(ar.get_dm_shift(), dtype=np.int64)
-    # real psrchive: integer-bin approximation of its phase rotation
-    nbin, nchan = ar.get_nbin(), ar.get_nchan()
-    dm = ar.get_dispersion_measure()
-    fref = ar.get_centre_frequency()
-    period = ar.get_Integration(0).get_folding_period()
-    out = np.zeros(nchan, dtype=np.int64)
-    for c in range(nchan):
-        f = ar.get_Profile(0, 0, c).get_centre_frequency()
-        delay = 4.148808e3 * dm * (f ** -2 - fref ** -2)
-        out[c] = int(round(delay / period * nbin)) % nbin
+        shift = np.asarray(ar.get_dm_shift(), dtype=np.int64)
+        get = getattr(ar, "get_dm_delay", None)
+        d = get() if get is not None else None
+        return shift, (None if d is None else np.asarray(d, dtype=np.float64))
+    from . import dedispersion
+    return dedispersion.plan(dedispersion.archive_delays(ar), ar.get_nbin(), ar.get_filename())
+
+
+def _stored_dedispersed(ar) -> bool:
+    """The archive holds its samples dedispersed (psrchive get_dedispersed()):
+    the reference's dedisperse (:91, :100) is then a no-op."""
+    get = getattr(ar, "get_dedispersed", None)
+    return bool(get()) if get is not None else False
+
+
+def _to_dispersed(cube, shift):
+    """Integer dedispersion of an archive stored dedispersed: its samples moved
+    back to the dispersed frame (raw[j] = ded[(j - shift) % nbin]), exactly, so
+    that the loop's own integer dedispersion reproduces the stored samples."""
+    nbin = cube.shape[-1]
+    out = np.empty_like(cube)
+    for c, sh in enumerate(np.asarray(shift, np.int64)):
+        idx = (np.arange(nbin) - int(sh)) % nbin
+        out[..., c, :] = cube[..., c, idx]
     return out
-
-
-def _dm_delay(ar):
-    """Fractional per-channel delays in bins when the archive dedisperses by
-    psrchive's FFT phase rotation (stand-in archives made with dm_delay), else
-    None (integer shifts, _dm_shift)."""
-    get = getattr(ar, "get_dm_delay", None)
-    d = get() if get is not None else None
-    return None if d is None else np.asarray(d, dtype=np.float64)
 
 
 def _state(ar) -> str:
@@ -180,14 +192,16 @@ def _device() -> int:
 
 
 def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_duty=0.15, nchan_total=None,
-             data_f64=False, delay=None):
+             data_f64=False, delay=None, input_dedispersed=False):
     """Run the GPU loop on a (nsub, nchan, nbin) f32 cube, or on full-polarisation
     data (nsub, npol, nchan, nbin) that the GPU pscrunches; returns the ic_run dict
     (+ ``residual`` when requested).  Under channel sharding (dist.channel_sharding)
     every rank runs its channel shard and gets the merged result: `cube` is then
     either the whole archive (sliced here) or, with ``nchan_total`` set, already
     this rank's channel slice (read slice-only from the file).  ``delay``:
-    fractional per-channel delays (dedispersion by FFT phase rotation)."""
+    fractional delays, (nchan,) or (nsub, nchan) (dedispersion by FFT phase
+    rotation); ``input_dedispersed``: the cube is stored dedispersed (FFT
+    dedispersion only)."""
     pols = cube.ndim == 4
     nsub, nchan, nbin = (cube.shape[0], cube.shape[2], cube.shape[3]) if pols else cube.shape
     from .dist import channel_sharding
@@ -203,18 +217,20 @@ def run_loop(cube, w0, shift, args, device=None, want_residual=False, baseline_d
             c0, c1 = chans[rank]
             cube = cube[:, :, c0:c1] if pols else cube[:, c0:c1]
             w0, shift = np.asarray(w0)[:, c0:c1], np.asarray(shift)[c0:c1]
-            delay = None if delay is None else np.asarray(delay)[c0:c1]
+            delay = None if delay is None else np.asarray(delay)[..., c0:c1]
             nchan_total = nchan
         return sharded.clean_cube_dist(
             np.ascontiguousarray(cube), np.ascontiguousarray(w0), np.asarray(shift), (nsub, nchan_total, nbin),
             dev, want_residual=want_residual,
             max_iter=args.max_iter, chanthresh=args.chanthresh, subintthresh=args.subintthresh,
-            pulse_region=args.pulse_region, baseline_duty=baseline_duty, data_f64=data_f64, delay=delay)
+            pulse_region=args.pulse_region, baseline_duty=baseline_duty, data_f64=data_f64, delay=delay,
+            input_dedispersed=input_dedispersed)
     if nchan_total is not None and nchan_total != nchan:
         raise ValueError("a channel slice of an archive needs channel sharding")
     with _native.GpuSession(nsub, nchan, nbin, args.max_iter, args.chanthresh, args.subintthresh,
                             args.pulse_region, baseline_duty,
-                            device=_device() if device is None else device, data_f64=data_f64, delay=delay) as s:
+                            device=_device() if device is None else device, data_f64=data_f64, delay=delay,
+                            input_dedispersed=input_dedispersed) as s:
         if pols:
             s.upload_pols(cube, w0, shift)
         else:
@@ -300,11 +316,14 @@ def clean(ar, args, arch):
         print("Total number of profiles: %s" % size)
 
     cube = _loop_input(ar)
-    shift = _dm_shift(ar)
-    delay = _dm_delay(ar)
+    shift, delay = _dedispersion(ar)
+    stored_ded = _stored_dedispersed(ar)
+    if stored_ded and delay is None:
+        cube = _to_dispersed(cube, shift)
     duty = ar.get_baseline_duty() if hasattr(ar, "get_baseline_duty") else 0.15
     out = run_loop(cube, orig_weights, shift, args, want_residual=args.unload_res, baseline_duty=duty,
-                   nchan_total=nchan_total, data_f64=_data_f64(ar), delay=delay)
+                   nchan_total=nchan_total, data_f64=_data_f64(ar), delay=delay,
+                   input_dedispersed=stored_ded and delay is not None)
     del cube
 
     x = 0
@@ -344,8 +363,7 @@ def clean(ar, args, arch):
         orig_weights = ar.get_weights()      # the residual archive's weights (pscrunch keeps them)
         if args.pscrunch:
             ar.pscrunch()
-        shift = _dm_shift(ar)
-        delay = _dm_delay(ar)
+        shift, delay = _dedispersion(ar)
     elif not args.pscrunch and not args.memory:
         ar = backend.Archive_load(arch)
     set_weights_archive(ar, avg_test_results)

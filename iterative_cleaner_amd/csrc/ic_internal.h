@@ -289,6 +289,59 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
                           const double *row_med, const double *row_mad, double chanthresh,
                           double subintthresh, double *test, float *W, float *hist, int iter,
                           int32_t *counters);
+// Phasor exp(+2 pi i k d / n) of harmonic k (0 <= k <= n/2) for a delay of d
+// bins, n a power of two (<= 8192): the phase rotation's multiplier
+// (phase_rotation.py phasors; oracle orc_phasor).  One fixed sequence of
+// separately rounded f64 operations, so that the host's per-channel table
+// (ic_set_delays), the device's per-profile evaluation (ic_set_delays2) and
+// the two restatements agree bit for bit:
+//   the delay is split (Veltkamp, 2^13 + 1) into dh (40 significant bits) and
+//   dl, so k dh and k dl are exact; t = k dh - n rint(k dh / n) is exact and
+//   |t| <= n/2; y = (t + k dl) 4/n counts quarter turns (one rounding); with
+//   q = rint(y), z = y - q (exact, |z| <= 1/2), the angle is (pi/2)(q + z):
+//   sin and cos of (pi/2) z by their Taylor polynomials in z^2 (through z^17
+//   and z^16, Horner; truncation < 1e-17), then the quadrant q mod 4.
+// Within 2.3e-16 of the exact phasor (measured against x87 long double).
+__host__ __device__ inline double2 ic_phasor(int k, double d, int n)
+{
+    const double c = d * 8193.0;
+    const double dh = c - (c - d);
+    const double dl = d - dh;
+    const double kk = (double)k, nn = (double)n;
+    const double xh = kk * dh, xl = kk * dl;
+    const double t = xh - nn * rint(xh * (1.0 / nn));
+    const double y = (t + xl) * (4.0 / nn);
+    const double q = rint(y);
+    const double z = y - q;
+    const double w = z * z;
+    // (-1)^j (pi/2)^(2j+1) / (2j+1)!  and  (-1)^j (pi/2)^(2j) / (2j)!
+    double sp = 0x1.aaec32af93359p-38;
+    sp = -0x1.6fadb9f155744p-31 + w * sp;
+    sp = 0x1.e8f434d018d63p-25 + w * sp;
+    sp = -0x1.e3074fde8871fp-19 + w * sp;
+    sp = 0x1.50783487ee782p-13 + w * sp;
+    sp = -0x1.32d2cce62bd86p-8 + w * sp;
+    sp = 0x1.466bc6775aae2p-4 + w * sp;
+    sp = -0x1.4abbce625be53p-1 + w * sp;
+    sp = 0x1.921fb54442d18p+0 + w * sp;
+    const double sn = z * sp;
+    double cp = 0x1.20c62c2f2d7f5p-34;
+    cp = -0x1.b6e24f44b128fp-28 + w * cp;
+    cp = 0x1.f9d38a3763cc3p-22 + w * cp;
+    cp = -0x1.a6d1f2a204a8cp-16 + w * cp;
+    cp = 0x1.e1f506891babbp-11 + w * cp;
+    cp = -0x1.55d3c7e3cbffap-6 + w * cp;
+    cp = 0x1.03c1f081b5ac4p-2 + w * cp;
+    cp = -0x1.3bd3cc9be45dep+0 + w * cp;
+    cp = 1.0 + w * cp;
+    switch ((int)q & 3) {
+    case 0: return make_double2(cp, sn);
+    case 1: return make_double2(-sn, cp);
+    case 2: return make_double2(-cp, -sn);
+    default: return make_double2(sn, -cp);
+    }
+}
+
 // Fractional dedispersion (dedisp_mode IC_DEDISP_FFT; phase_rotation.py):
 // out[p] = rot(f32(in[p] - base[p])) by the channel's phasors, sign +1 =
 // dedisperse, -1 = dededisperse.  Rows p = s*nchan + c of ld_in / ldo floats;
@@ -302,7 +355,11 @@ struct RotateArgs {
     const float *in;
     long ld_in;
     const float *base;          // [P] or nullptr (0)
-    const double2 *ph;          // [nchan][nbin/2 + 1]: exp(+2 pi i fmod(k s_c, nbin) / nbin)
+    const double2 *ph;          // [nchan][nbin/2 + 1]: ic_phasor(k, delay[c], nbin)
+    const double *delay2;       // [P] per-profile delays (ic_set_delays2): phasors
+                                // ic_phasor(k, delay2[p], nbin) evaluated in the kernel, ph unused
+    int identity;               // the rotation is the identity (an archive stored
+                                // dedispersed, sign +1): out = f32(in - base), no FFT
     int sign;
     const double2 *tw;          // [nbin]: exp(-2 pi i q / nbin)
     const int32_t *flags;       // [nsub] or nullptr (all)

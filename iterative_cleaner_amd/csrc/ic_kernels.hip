@@ -3709,7 +3709,9 @@ __device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
     return make_double2(er - oi, ei + orr);
 }
 
-template <int N>
+// PP: per-profile delays (a.delay2, ic_set_delays2): each lane evaluates its
+// phasors with ic_phasor instead of loading the channel's table row.
+template <int N, bool PP>
 // 3 waves per SIMD at N <= 1024 (4 spilled 21 VGPRs; 3, 154 VGPRs: C2 fft 57.0 -> 56.4 ms)
 __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) void k_rotate(RotateArgs a)
 {
@@ -3768,14 +3770,20 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         const unsigned c = (unsigned)(item / nsub), s = (unsigned)(item % nsub);
         const size_t p = (size_t)s * nchan + c;
         if (skip(p, s)) continue;
-        const __amdgpu_buffer_rsrc_t phr = rot_rsrc(a.ph + (size_t)c * (M + 1), M + 1);
+        const __amdgpu_buffer_rsrc_t phr = rot_rsrc(PP ? a.tw : a.ph + (size_t)c * (M + 1), M + 1);
+        const double dly = PP ? a.delay2[p] : 0.0;
         // the post step's phasors one round ahead: the first round's are
         // requested with the rows, each later round's before the round before it
         auto ldph = [&](int u, double2 (&pp)[2]) {
             const int k = t + u * TB;
             if (k <= H) {
-                pp[0] = rot_ld(phr, 16u * (unsigned)k, 0);
-                pp[1] = rot_ld(phr, 16u * (unsigned)(M - k), 0);
+                if constexpr (PP) {
+                    pp[0] = ic_phasor(k, dly, N);
+                    pp[1] = ic_phasor(M - k, dly, N);
+                } else {
+                    pp[0] = rot_ld(phr, 16u * (unsigned)k, 0);
+                    pp[1] = rot_ld(phr, 16u * (unsigned)(M - k), 0);
+                }
             }
         };
         double2 phn[2];
@@ -5075,18 +5083,49 @@ bool rotate_supported(int nbin)
     }
 }
 
+// The identity "rotation" of an archive stored dedispersed (its dedisperse is a
+// no-op, archive.py dedisperse): out[p] = f32(in[p] - base[p]) (and out2), for
+// the subints flags selects; a wave per profile, 16-byte rows.
+__global__ __launch_bounds__(256) void k_rotate_identity(RotateArgs a)
+{
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const size_t P = (size_t)a.nsub * a.nchan;
+    for (size_t p = (size_t)blockIdx.x * 4 + wave; p < P; p += (size_t)gridDim.x * 4) {
+        if (a.flags && a.flags[p / (unsigned)a.nchan] == 0) continue;
+        const float b = a.base ? a.base[p] : 0.0f;
+        for (int j = 4 * lane; j < a.nbin; j += 256) {
+            const float4 x = *(const float4 *)(a.in + d_ofs(p, j, (int)a.ld_in, a.in_tiled));
+            const float4 y = make_float4(x.x - b, x.y - b, x.z - b, x.w - b);
+            *(float4 *)(a.out + p * (size_t)a.ldo + j) = y;
+            if (a.out2) *(float4 *)(a.out2 + d_ofs(p, j, (int)a.ldo2, a.out2_tiled)) = y;
+        }
+    }
+}
+
 hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
 {
     const size_t P = (size_t)a.nsub * a.nchan;
     if (P == 0) return hipSuccess;
-    if (!rotate_supported(a.nbin) || !a.in || !a.out || !a.ph || !a.tw || a.ld_in < a.nbin || a.ldo < a.nbin ||
+    if (!rotate_supported(a.nbin) || !a.in || !a.out || !a.tw || a.ld_in < a.nbin || a.ldo < a.nbin ||
+        (!a.ph && !a.delay2 && !a.identity) ||
         (a.ld_in & 3) || (a.ldo & 3) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 3))) ||
-        (a.amp && (!a.T64 || !a.info)) || (a.in_tiled && (a.ld_in & 31)) || (a.out2_tiled && (a.ldo2 & 31)))
+        (a.amp && (!a.T64 || !a.info)) || (a.in_tiled && (a.ld_in & 31)) || (a.out2_tiled && (a.ldo2 & 31)) ||
+        (a.identity && (a.amp || a.late)))
         return hipErrorInvalidValue;
+    if (a.identity) {
+        IC_GGL(k_rotate_identity, dim3((unsigned)std::min<size_t>(cdiv(P, 4), 16384)), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
 #define IC_ROT(NN)                                                                                 \
     case NN:                                                                                       \
-        IC_GGL(k_rotate<NN>, dim3((unsigned)std::min<size_t>(cdiv(P, RotCfg<NN>::WPB), 16384 / RotCfg<NN>::WPB)), \
-               dim3(RotCfg<NN>::TB * RotCfg<NN>::WPB), 0, st, a);                                  \
+        if (a.delay2)                                                                              \
+            IC_GGL((k_rotate<NN, true>),                                                           \
+                   dim3((unsigned)std::min<size_t>(cdiv(P, RotCfg<NN>::WPB), 16384 / RotCfg<NN>::WPB)), \
+                   dim3(RotCfg<NN>::TB * RotCfg<NN>::WPB), 0, st, a);                              \
+        else                                                                                       \
+            IC_GGL((k_rotate<NN, false>),                                                          \
+                   dim3((unsigned)std::min<size_t>(cdiv(P, RotCfg<NN>::WPB), 16384 / RotCfg<NN>::WPB)), \
+                   dim3(RotCfg<NN>::TB * RotCfg<NN>::WPB), 0, st, a);                              \
         break;
     switch (a.nbin) {
         IC_ROT(64) IC_ROT(128) IC_ROT(256) IC_ROT(512) IC_ROT(1024) IC_ROT(2048) IC_ROT(4096)

@@ -180,6 +180,7 @@ struct Session {
     float *dr = nullptr, *Tc = nullptr, *R = nullptr, *zbase = nullptr;
     int32_t *zshift = nullptr;
     double2 *ph = nullptr;
+    double *delay2 = nullptr;        // [P] per-profile delays (ic_set_delays2), else nullptr
     // timing
     bool timing = false;
     int timing_only = -1;            // >= 0: time only this kernel id
@@ -380,7 +381,8 @@ void free_all(Session *s)
                     s->T,    s->ptp,   s->hist, s->valid, s->win, s->info, s->comm ? nullptr : s->counters,
                     s->part, s->wpart, s->T64,  s->amp, s->std_, s->mean, s->fft,  s->test,
                     s->lstat, s->tw,   s->plan, s->fs_block, s->lists, s->rcount, s->tw_p2, s->part2,
-                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph, s->T2, s->fs.U, s->tmark};
+                    s->wflag, s->TT, s->dr, s->Tc, s->R, s->zbase, s->zshift, s->ph, s->T2, s->fs.U, s->tmark,
+                    s->delay2};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     void *rbufs[] = {s->std_r, s->mean_r, s->fft_r, s->ptp_r, s->valid_r};
@@ -531,19 +533,15 @@ int scrunch_stage(Session *s)
     return 0;
 }
 
-// phasors exp(+2 pi i fmod(k s_c, nbin) / nbin), k <= nbin/2, in x87 long double
-// (phase_rotation.py phasors; oracle orc_phasors)
+// phasor table ic_phasor(k, delay[c], nbin), k <= nbin/2 (phase_rotation.py
+// phasors; oracle orc_phasors): the same function the per-profile kernel
+// evaluates on the device, so a table row and a profile with that delay agree
 std::vector<double2> make_phasors(int nbin, int nchan, const double *delay)
 {
-    const long double pi = 3.141592653589793238462643383279502884L;
     const int m = nbin / 2;
     std::vector<double2> ph((size_t)nchan * (m + 1));
     for (int c = 0; c < nchan; ++c)
-        for (int k = 0; k <= m; ++k) {
-            const long double t = fmodl((long double)k * (long double)delay[c], (long double)nbin);
-            const long double ang = 2.0L * pi * t / (long double)nbin;
-            ph[(size_t)c * (m + 1) + k] = make_double2((double)cosl(ang), (double)sinl(ang));
-        }
+        for (int k = 0; k <= m; ++k) ph[(size_t)c * (m + 1) + k] = ic_phasor(k, delay[c], nbin);
     return ph;
 }
 
@@ -555,6 +553,10 @@ RotateArgs rotate_args(Session *s, const float *in, const float *base, int sign,
     a.ld_in = s->p.nbin;
     a.base = base;
     a.ph = s->ph;
+    a.delay2 = s->delay2;
+    // an archive stored dedispersed: its dedisperse is a no-op (archive.py),
+    // only the residual's dededisperse rotates
+    a.identity = sign > 0 && s->p.input_dedispersed;
     a.sign = sign;
     a.tw = s->tw;
     a.flags = flags;
@@ -918,6 +920,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         return fail(IC_EINVAL, "fit_mode %d unsupported", p.fit_mode);
     if (p.dedisp_mode != IC_DEDISP_SHIFT && p.dedisp_mode != IC_DEDISP_FFT)
         return fail(IC_EINVAL, "dedisp_mode %d unsupported", p.dedisp_mode);
+    if (p.input_dedispersed != 0 && (p.input_dedispersed != 1 || p.dedisp_mode != IC_DEDISP_FFT))
+        return fail(IC_EINVAL, "input_dedispersed=%d needs dedisp_mode IC_DEDISP_FFT (0 or 1)", p.input_dedispersed);
     if (p.dedisp_mode == IC_DEDISP_FFT && !rotate_supported(p.nbin))
         return fail(IC_EINVAL, "fractional dedispersion needs a power-of-two nbin in 64..4096 (nbin=%d)", p.nbin);
     if (diag_lds_bytes(p.nbin) > 160 * 1024)
@@ -1700,25 +1704,58 @@ int ic_set_delays(void *session, const double *delay_bins)
     const std::vector<double2> ph = make_phasors(s->p.nbin, s->nchan, delay_bins);
     CK(hipMemcpyAsync(s->ph, ph.data(), sizeof(double2) * ph.size(), hipMemcpyHostToDevice, s->stream));
     CK(hipStreamSynchronize(s->stream));
+    if (s->delay2) {
+        CK(hipFree(s->delay2));
+        s->delay2 = nullptr;
+    }
     s->delays_set = true;
     return IC_OK;
 }
 
-int ic_rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, const double *delay_bins,
-                       int sign, float *out)
+int ic_set_delays2(void *session, const double *delay_bins)
+{
+    Session *s = (Session *)session;
+    if (!s || !delay_bins) return fail(IC_EINVAL, "null argument");
+    if (s->failed) return failed_session();
+    if (!s->fftded) return fail(IC_ESTATE, "ic_set_delays2 on a session with dedisp_mode %d", s->p.dedisp_mode);
+    const int nsub = s->p.nsub, nchan = s->nchan;
+    for (size_t k = 0; k < (size_t)nsub * nchan; ++k)
+        if (!isfinite(delay_bins[k])) return fail(IC_EINVAL, "delay[%zu] is not finite", k);
+    // one delay row for every subint: the channel table (the same phasors)
+    bool rows_equal = true;
+    for (int sb = 1; sb < nsub && rows_equal; ++sb)
+        rows_equal = memcmp(delay_bins, delay_bins + (size_t)sb * nchan, sizeof(double) * nchan) == 0;
+    if (rows_equal) return ic_set_delays(session, delay_bins);
+    CK(hipSetDevice(s->device));
+    if (!s->delay2 && hipMalloc((void **)&s->delay2, sizeof(double) * s->P) != hipSuccess) {
+        s->delay2 = nullptr;
+        return fail(IC_ENOMEM, "hipMalloc(per-profile delays) failed");
+    }
+    CK(hipMemcpyAsync(s->delay2, delay_bins, sizeof(double) * s->P, hipMemcpyHostToDevice, s->stream));
+    CK(hipStreamSynchronize(s->stream));
+    s->delays_set = true;
+    return IC_OK;
+}
+
+namespace {
+// ic_rotate_profiles(2): per_profile = 0: delay_bins [nchan] (the phasor
+// table), 1: [nsub*nchan] (phasors evaluated per profile in the kernel)
+int rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, const double *delay_bins,
+                    int per_profile, int sign, float *out)
 {
     if (!in || !delay_bins || !out || nsub <= 0 || nchan <= 0) return fail(IC_EINVAL, "bad argument");
     if (!rotate_supported(nbin))
         return fail(IC_EINVAL, "fractional dedispersion needs a power-of-two nbin in 64..4096 (nbin=%d)", nbin);
     if (sign != 1 && sign != -1) return fail(IC_EINVAL, "sign must be +1 or -1");
-    for (int c = 0; c < nchan; ++c)
-        if (!isfinite(delay_bins[c])) return fail(IC_EINVAL, "delay[%d] is not finite", c);
+    const size_t nd = per_profile ? (size_t)nsub * nchan : (size_t)nchan;
+    for (size_t c = 0; c < nd; ++c)
+        if (!isfinite(delay_bins[c])) return fail(IC_EINVAL, "delay[%zu] is not finite", c);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(IC_EHIP, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
     CK(hipSetDevice(device));
     const size_t N = (size_t)nsub * nchan * nbin;
-    const std::vector<double2> ph = make_phasors(nbin, nchan, delay_bins);
+    const std::vector<double2> ph = per_profile ? std::vector<double2>(1) : make_phasors(nbin, nchan, delay_bins);
     std::vector<double2> tw(nbin);
     for (int q = 0; q < nbin; ++q) {
         const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)q / (long double)nbin;
@@ -1726,9 +1763,13 @@ int ic_rotate_profiles(int device, int nsub, int nchan, int nbin, const float *i
     }
     float *d = nullptr;
     double2 *dph = nullptr, *dtw = nullptr;
+    double *ddl = nullptr;
     hipStream_t st = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc((void **)&d, sizeof(float) * N);
+    if (e == hipSuccess && per_profile) e = hipMalloc((void **)&ddl, sizeof(double) * nd);
+    if (e == hipSuccess && per_profile)
+        e = hipMemcpyAsync(ddl, delay_bins, sizeof(double) * nd, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMalloc((void **)&dph, sizeof(double2) * ph.size());
     if (e == hipSuccess) e = hipMalloc((void **)&dtw, sizeof(double2) * tw.size());
     if (e == hipSuccess) e = hipMemcpyAsync(d, in, sizeof(float) * N, hipMemcpyHostToDevice, st);
@@ -1738,7 +1779,8 @@ int ic_rotate_profiles(int device, int nsub, int nchan, int nbin, const float *i
         RotateArgs a{};
         a.in = d;
         a.ld_in = nbin;
-        a.ph = dph;
+        a.ph = per_profile ? nullptr : dph;
+        a.delay2 = ddl;
         a.sign = sign;
         a.tw = dtw;
         a.nsub = nsub;
@@ -1753,9 +1795,23 @@ int ic_rotate_profiles(int device, int nsub, int nchan, int nbin, const float *i
     if (d) (void)hipFree(d);
     if (dph) (void)hipFree(dph);
     if (dtw) (void)hipFree(dtw);
+    if (ddl) (void)hipFree(ddl);
     if (st) (void)hipStreamDestroy(st);
     if (e != hipSuccess) return fail(IC_EHIP, "ic_rotate_profiles: %s", hipGetErrorString(e));
     return IC_OK;
+}
+}  // namespace
+
+int ic_rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, const double *delay_bins,
+                       int sign, float *out)
+{
+    return rotate_profiles(device, nsub, nchan, nbin, in, delay_bins, 0, sign, out);
+}
+
+int ic_rotate_profiles2(int device, int nsub, int nchan, int nbin, const float *in, const double *delay_bins,
+                        int sign, float *out)
+{
+    return rotate_profiles(device, nsub, nchan, nbin, in, delay_bins, 1, sign, out);
 }
 
 int ic_get_bad_fits(void *session, int32_t *per_iter, int n)

@@ -33,10 +33,12 @@ of s bins (``y[j] = x[j + s]`` for integer s; ``dedisperse`` rotates by +s,
    out[2j+1] = f32((-r[j].i) * (1/M)).
 
 Every step is a single IEEE f64 operation in the written order (no fused
-multiply-add).  Tables: tw[q] = exp(-2 pi i q / N) and
-P_c[k] = exp(+2 pi i fmod(k s_c, N) / N), evaluated in x87 long double
-(cosl/sinl) and rounded to f64, exactly as the C library builds them
-(ic_session.hip).
+multiply-add).  Tables: tw[q] = exp(-2 pi i q / N), evaluated in x87 long
+double (cosl/sinl) and rounded to f64, and the phasors P[k] = exp(+2 pi i k s / N)
+of a delay s, evaluated by the f64 formula of :func:`phasors` (the GPU's
+ic_phasor, ic_internal.h), so that the library's per-channel table and its
+per-profile evaluation (psrchive's per-Integration folding period: one delay
+per subint and channel) give the same bits.
 """
 from __future__ import annotations
 
@@ -59,14 +61,57 @@ def twiddles(nbin: int) -> np.ndarray:
     return np.stack([np.cos(ang).astype(np.float64), np.sin(ang).astype(np.float64)])
 
 
+# Taylor coefficients of sin((pi/2) z) and cos((pi/2) z):
+# (-1)^j (pi/2)^(2j+1) / (2j+1)!  and  (-1)^j (pi/2)^(2j) / (2j)!, j = 0 .. 8,
+# each the f64 nearest the exact value
+_PH_S = tuple(float.fromhex(h) for h in (
+    "0x1.921fb54442d18p+0", "-0x1.4abbce625be53p-1", "0x1.466bc6775aae2p-4", "-0x1.32d2cce62bd86p-8",
+    "0x1.50783487ee782p-13", "-0x1.e3074fde8871fp-19", "0x1.e8f434d018d63p-25", "-0x1.6fadb9f155744p-31",
+    "0x1.aaec32af93359p-38"))
+_PH_C = tuple(float.fromhex(h) for h in (
+    "0x1.0000000000000p+0", "-0x1.3bd3cc9be45dep+0", "0x1.03c1f081b5ac4p-2", "-0x1.55d3c7e3cbffap-6",
+    "0x1.e1f506891babbp-11", "-0x1.a6d1f2a204a8cp-16", "0x1.f9d38a3763cc3p-22", "-0x1.b6e24f44b128fp-28",
+    "0x1.20c62c2f2d7f5p-34"))
+
+
 def phasors(nbin: int, delays) -> np.ndarray:
-    """(2, nchan, nbin/2 + 1) f64: exp(+2 pi i fmod(k s_c, nbin) / nbin)."""
+    """(2, *delays.shape, nbin/2 + 1) f64: exp(+2 pi i k s / nbin) for every
+    delay s (bins) and harmonic k <= nbin/2, in this f64 operation order:
+
+    * Veltkamp split s = sh + sl (c = s * 8193; sh = c - (c - s); sl = s - sh):
+      sh has 40 significant bits, so k*sh and k*sl are exact (k < 2^13);
+    * t = k sh - nbin rint(k sh / nbin)   (exact; |t| <= nbin/2)
+    * y = (t + k sl) * (4 / nbin)          quarter turns, one rounding
+    * q = rint(y); z = y - q               (exact; |z| <= 1/2)
+    * w = z*z; sin = z * (S0 + w (S1 + ... w S8)); cos = C0 + w (C1 + ... w C8)
+    * quadrant q mod 4: (cos, sin), (-sin, cos), (-cos, -sin), (sin, -cos).
+
+    Within 2.3e-16 of the exact phasor (tests/test_phase_rotation.py checks it
+    against x87 long double)."""
     m = nbin // 2
-    k = np.arange(m + 1).astype(np.longdouble)
-    s = np.asarray(delays, dtype=np.float64).reshape(-1).astype(np.longdouble)
-    t = np.fmod(k[None, :] * s[:, None], np.longdouble(nbin))
-    ang = (np.longdouble(2.0) * PI_L) * t / np.longdouble(nbin)
-    return np.stack([np.cos(ang).astype(np.float64), np.sin(ang).astype(np.float64)])
+    k = np.arange(m + 1, dtype=np.float64)
+    s = np.asarray(delays, dtype=np.float64)[..., None]
+    nn = float(nbin)
+    c = s * 8193.0
+    sh = c - (c - s)
+    sl = s - sh
+    xh = k * sh
+    xl = k * sl
+    t = xh - nn * np.rint(xh * (1.0 / nn))
+    y = (t + xl) * (4.0 / nn)
+    q = np.rint(y)
+    z = y - q
+    w = z * z
+    sp = np.full_like(z, _PH_S[8])
+    cp = np.full_like(z, _PH_C[8])
+    for j in range(7, -1, -1):
+        sp = _PH_S[j] + w * sp
+        cp = _PH_C[j] + w * cp
+    sn = z * sp
+    qi = q.astype(np.int64) & 3
+    re = np.where(qi == 0, cp, np.where(qi == 1, -sn, np.where(qi == 2, -cp, sn)))
+    im = np.where(qi == 0, sn, np.where(qi == 1, cp, np.where(qi == 2, -sn, -cp)))
+    return np.stack([re, im])
 
 
 def _stockham(vr: np.ndarray, vi: np.ndarray, tw: np.ndarray):
@@ -116,9 +161,10 @@ def _pre(yar, yai, ybr, ybi, wr, wi):
 
 def rotate(x: np.ndarray, ph: np.ndarray, sign: int, tw: np.ndarray | None = None,
            base: np.ndarray | None = None) -> np.ndarray:
-    """Rotate profiles x (..., nchan, nbin) f32 by their channel's delay.
+    """Rotate profiles x (..., nchan, nbin) f32 by their delays.
 
-    ph: phasors(nbin, delays) for the nchan channels (axis -2 of x); sign +1 =
+    ph: phasors(nbin, delays) for the nchan channels (axis -2 of x), or for
+    every profile (delays of x's leading shape, e.g. (nsub, nchan)); sign +1 =
     dedisperse (y[j] = x[j + s]), -1 = dededisperse; base (..., nchan) f32 is
     subtracted first in f32 (remove_baseline's levels)."""
     x = np.asarray(x, dtype=np.float32)

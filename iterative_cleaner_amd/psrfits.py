@@ -12,11 +12,13 @@ Samples are int16 with a per-(subint, pol, channel) scale and offset:
 value = f32(f32(DATA) * DAT_SCL + DAT_OFFS), the decoding psrchive applies.
 The stand-in's own metadata rides in extra keywords / one extra column that
 other PSRFITS readers ignore: IC_SHIFT (nchan J, integer dedispersion delays in
-bins), IC_DELAY (nchan D, fractional delays in bins of an archive dedispersed
-by FFT phase rotation), IC_DEDSP (dedispersed flag), IC_DUTY (baseline duty),
-IC_MJDE (end MJD).  Files without IC_SHIFT get integer delays from DM, DAT_FREQ
-and PERIOD (the same integer approximation cleaner._dm_shift makes for real
-psrchive), or, with IC_DEDISPERSION=fft, the exact fractional delays.
+bins), IC_DELAY (nchan D per row, fractional delays in bins of an archive
+dedispersed by FFT phase rotation; rows that differ are per-profile delays),
+IC_DEDSP (dedispersed flag), IC_DUTY (baseline duty), IC_MJDE (end MJD).  Files
+without IC_SHIFT (a foreign writer's) are dedispersed as psrchive would:
+delays from DM, DAT_FREQ, OBSFREQ and each row's PERIOD (dedispersion.py),
+integer shifts when every delay is integral, else the fractional FFT rotation
+(an error at an nbin it cannot serve, never a silent rounding).
 """
 from __future__ import annotations
 
@@ -142,14 +144,6 @@ def decode(q: np.ndarray, scl: np.ndarray, offs: np.ndarray) -> np.ndarray:
     return (q.astype(np.float32) * scl[..., None] + offs[..., None]).astype(np.float32)
 
 
-def fractional_dedispersion() -> bool:
-    """IC_DEDISPERSION=fft: archives whose delays come from DM / DAT_FREQ /
-    PERIOD are dedispersed by psrchive's FFT phase rotation with the exact
-    fractional delay (phase_rotation.py) instead of the rounded integer shift."""
-    import os
-    return os.environ.get("IC_DEDISPERSION", "").strip().lower() == "fft"
-
-
 # ------------------------------------------------------------------ write
 def save(ar, path: str, stand_in_meta: bool = True) -> None:
     """Write `ar` as fold-mode PSRFITS (stand_in_meta=False: standard columns
@@ -164,11 +158,11 @@ def save(ar, path: str, stand_in_meta: bool = True) -> None:
     freqs = getattr(ar, "_chan_freqs", None)
     if freqs is None or len(freqs) != nchan:
         freqs = cfreq + (np.arange(nchan) - (nchan - 1) / 2.0) * 1.0
-    period = float(getattr(ar, "_period", 1.0))
+    period = np.broadcast_to(np.asarray(getattr(ar, "_period", 1.0), np.float64), (nsub,))
     tsub = float(getattr(ar, "_tsubint", 10.0))
     cols = [("TSUBINT", "1D", None, (nsub,), np.full(nsub, tsub)),
             ("OFFS_SUB", "1D", None, (nsub,), (np.arange(nsub) + 0.5) * tsub),
-            ("PERIOD", "1D", None, (nsub,), np.full(nsub, period)),
+            ("PERIOD", "1D", None, (nsub,), period),
             ("DAT_FREQ", "%dD" % nchan, None, (nsub, nchan), np.broadcast_to(freqs, (nsub, nchan))),
             ("DAT_WTS", "%dE" % nchan, None, (nsub, nchan), ar._weights),
             ("DAT_OFFS", "%dE" % (nchan * npol), None, (nsub, npol * nchan), offs.reshape(nsub, -1)),
@@ -291,27 +285,24 @@ def load(path: str, channels=None):
     weights = np.array(rows["DAT_WTS"].reshape(nsub, nchan_total)[:, c0:c1], np.float32)
     freqs = np.array(rows["DAT_FREQ"].reshape(nsub, nchan_total)[0, c0:c1], np.float64) \
         if "DAT_FREQ" in dt.names else None
-    period = float(np.asarray(rows["PERIOD"]).reshape(-1)[0]) if "PERIOD" in dt.names else 1.0
+    period = np.array(rows["PERIOD"], np.float64).reshape(nsub) if "PERIOD" in dt.names \
+        else np.ones(nsub, np.float64)
     cfreq = float(primary.get("OBSFREQ", 1400.0))
     dm = float(hdr.get("DM", 0.0))
     frac = None
     if "IC_DELAY" in dt.names:
-        frac = np.array(rows["IC_DELAY"].reshape(nsub, nchan_total)[0, c0:c1], np.float64)
+        frac = np.array(rows["IC_DELAY"].reshape(nsub, nchan_total)[:, c0:c1], np.float64)
+        if np.all(frac == frac[:1]):
+            frac = np.ascontiguousarray(frac[0])
     if "IC_SHIFT" in dt.names:
         shift = np.array(rows["IC_SHIFT"].reshape(nsub, nchan_total)[0, c0:c1], np.int64)
-    elif freqs is not None and dm != 0.0:
-        delay = 4.148808e3 * dm * (freqs ** -2 - cfreq ** -2)
-        shift = np.rint(delay / period * nbin).astype(np.int64) % nbin
-        if fractional_dedispersion():
-            from . import phase_rotation
-            if phase_rotation.is_supported(nbin) and 64 <= nbin <= 4096:
-                frac = delay / period * nbin
-            else:
-                # the rotation kernels take power-of-two nbin in 64..4096: keep the
-                # integer shift for this archive rather than fail its load / session
-                import warnings
-                warnings.warn("IC_DEDISPERSION=fft: nbin=%d is not a power of two in 64..4096; "
-                              "%s is dedispersed by the integer shift" % (nbin, path))
+    elif freqs is not None:
+        # a foreign writer's file: psrchive's delays (DM, channel frequency, each
+        # row's folding period) over the WHOLE band, then this slice's channels
+        from . import dedispersion
+        allf = np.array(rows["DAT_FREQ"].reshape(nsub, nchan_total)[0], np.float64)
+        delay = dedispersion.delays_from_dm(dm, allf, cfreq, period, nbin)[:, c0:c1]
+        shift, frac = dedispersion.plan(delay, nbin, path)
     else:
         shift = np.zeros(nchan, np.int64)
     mjd0 = float(primary.get("STT_IMJD", 60000)) + (float(primary.get("STT_SMJD", 0))
@@ -332,6 +323,6 @@ def load(path: str, channels=None):
     ar._psrfits_q = (q, scl, offs)
     ar._format = "PSRFITS"
     ar._chan_freqs = freqs
-    ar._period = period
+    ar._period = period if np.any(period != period[:1]) else float(period[0])
     ar._dm = dm
     return ar

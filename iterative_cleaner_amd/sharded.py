@@ -31,7 +31,8 @@ def _loop_kwargs(args):
                 subintthresh=args.get("subintthresh", 5.0),
                 pulse_region=args.get("pulse_region", (0, 0, 1)),
                 baseline_duty=args.get("baseline_duty", 0.15), fit_mode=args.get("fit_mode", 0),
-                data_f64=args.get("data_f64", False), options=args.get("options"))
+                data_f64=args.get("data_f64", False), options=args.get("options"),
+                input_dedispersed=args.get("input_dedispersed", False))
 
 
 def clean_cube_local(cube, w0, shift, world, devices=None, want_details=False, fit_tail=None, **args):
@@ -49,7 +50,7 @@ def clean_cube_local(cube, w0, shift, world, devices=None, want_details=False, f
     errors = []
     with _native.ShardGroup(world) as group:
         sessions = [_native.ShardSession(nsub, nchan, nbin, r, world, group=group, device=devices[r],
-                                         delay=None if delay is None else np.asarray(delay)[chans[r][0]:chans[r][1]],
+                                         delay=None if delay is None else np.asarray(delay)[..., chans[r][0]:chans[r][1]],
                                          **kw)
                     for r in range(world)]
         try:
@@ -113,7 +114,7 @@ def clean_cube_dist(cube_slice, w0_slice, shift_slice, global_shape, device, gro
     `cube_slice` etc. are the rank's channel range (``_native.shard_layout``);
     returns the merged full-archive dict on every rank (with want_residual, the
     full residual cube on rank 0 only).  ``delay`` (in args): the slice's
-    fractional delays (FFT-rotation dedispersion)."""
+    fractional delays (FFT-rotation dedispersion; (nchan_r,) or (nsub, nchan_r))."""
     import torch.distributed as dist
 
     from .dist import TorchComm

@@ -86,6 +86,16 @@ def fractional_delays(shift, nbin):
             + np.where(c % 5 == 4, 3.0 * nbin, 0.0))
 
 
+def per_profile_delays(shift, nbin, nsub):
+    """Deterministic per-(subint, channel) delays: :func:`fractional_delays`
+    scaled by P_0 / P_s for a folding period that drifts by up to 2e-4 across
+    the subints, as psrchive's per-Integration dedispersion sees it
+    (delay[s, c] = dm_delay_c / P_s * nbin)."""
+    s = np.arange(nsub)
+    scale = 1.0 + 2e-4 * np.sin(0.7 * s + 0.3)
+    return fractional_delays(shift, nbin)[None, :] * scale[:, None]
+
+
 def make_archive(nsub, nchan, nbin, seed=0, rfi_frac=0.05, npol=1,
                  filename="synthetic.ar", **kw) -> Archive:
     data, weights, shift = make_cube(nsub, nchan, nbin, seed, rfi_frac, npol, **kw)

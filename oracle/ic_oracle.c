@@ -514,19 +514,51 @@ void orc_twiddles(int n, double *tw)
     }
 }
 
-/* ph[(c*(n/2+1) + k)*2 + {0,1}] = cos, sin of 2 pi fmod(k s_c, n) / n */
+/* o[0], o[1] = cos, sin of 2 pi k d / n, harmonic k of a delay of d bins (n a
+ * power of two), in the written f64 order of phase_rotation.py phasors (the
+ * GPU's ic_phasor):
+ *   Veltkamp split d = dh + dl with dh of 40 bits (c = d * 8193), so that
+ *   k dh and k dl are exact; t = k dh - n rint(k dh / n) (exact, |t| <= n/2);
+ *   y = (t + k dl) * (4/n) quarter turns; q = rint(y), z = y - q;
+ *   sin / cos of (pi/2) z by Horner in w = z^2 on the Taylor coefficients
+ *   (-1)^j (pi/2)^(2j+1)/(2j+1)!, j <= 8, and (-1)^j (pi/2)^(2j)/(2j)!, j <= 8;
+ *   then the quadrant q mod 4. */
+static const double PH_S[9] = {0x1.921fb54442d18p+0,  -0x1.4abbce625be53p-1, 0x1.466bc6775aae2p-4,
+                               -0x1.32d2cce62bd86p-8, 0x1.50783487ee782p-13, -0x1.e3074fde8871fp-19,
+                               0x1.e8f434d018d63p-25, -0x1.6fadb9f155744p-31, 0x1.aaec32af93359p-38};
+static const double PH_C[9] = {1.0,                   -0x1.3bd3cc9be45dep+0, 0x1.03c1f081b5ac4p-2,
+                               -0x1.55d3c7e3cbffap-6, 0x1.e1f506891babbp-11, -0x1.a6d1f2a204a8cp-16,
+                               0x1.f9d38a3763cc3p-22, -0x1.b6e24f44b128fp-28, 0x1.20c62c2f2d7f5p-34};
+static void orc_phasor(int k, double d, int n, double *o)
+{
+    const double c = d * 8193.0;
+    const double dh = c - (c - d), dl = d - dh;
+    const double nn = (double)n;
+    const double xh = (double)k * dh, xl = (double)k * dl;
+    const double t = xh - nn * rint(xh * (1.0 / nn));
+    const double y = (t + xl) * (4.0 / nn);
+    const double q = rint(y);
+    const double z = y - q, w = z * z;
+    double sp = PH_S[8], cp = PH_C[8];
+    for (int j = 7; j >= 0; --j) {
+        sp = PH_S[j] + w * sp;
+        cp = PH_C[j] + w * cp;
+    }
+    const double sn = z * sp;
+    switch ((int)q & 3) {
+    case 0: o[0] = cp;  o[1] = sn;  break;
+    case 1: o[0] = -sn; o[1] = cp;  break;
+    case 2: o[0] = -cp; o[1] = -sn; break;
+    default: o[0] = sn; o[1] = -cp; break;
+    }
+}
+
+/* ph[(c*(n/2+1) + k)*2 + {0,1}] = orc_phasor(k, delay[c], n) */
 void orc_phasors(int n, int nchan, const double *delay, double *ph)
 {
-    const long double pi = 3.141592653589793238462643383279502884L;
     const int m = n / 2;
     for (int c = 0; c < nchan; ++c)
-        for (int k = 0; k <= m; ++k) {
-            const long double t = fmodl((long double)k * (long double)delay[c], (long double)n);
-            const long double ang = 2.0L * pi * t / (long double)n;
-            double *o = ph + ((size_t)c * (m + 1) + k) * 2;
-            o[0] = (double)cosl(ang);
-            o[1] = (double)sinl(ang);
-        }
+        for (int k = 0; k <= m; ++k) orc_phasor(k, delay[c], n, ph + ((size_t)c * (m + 1) + k) * 2);
 }
 
 /* radix-2 Stockham FFT of m complex points (re/im interleaved) through `tmp` */
@@ -618,30 +650,46 @@ static void rotate1(int n, const float *x, float b, const double *p, int sign, c
     }
 }
 
-/* Rotate every profile of a (nsub, nchan, n) cube by its channel's delay:
- * out = rot(f32(in - base)) (base may be NULL = 0).  n a power of two >= 4. */
-void orc_rotate(int nsub, int nchan, int n, const float *in, const float *base, const double *delay,
-                int sign, float *out)
+/* Rotate every profile of a (nsub, nchan, n) cube by its delay:
+ * out = rot(f32(in - base)) (base may be NULL = 0).  n a power of two >= 4.
+ * per_profile 0: delay [nchan] (a channel's delay for every subint);
+ * 1: delay [nsub*nchan], profile k's own (psrchive's per-Integration period).
+ * identity: the rotation of an archive stored dedispersed, whose dedisperse is
+ * a no-op: out = f32(in - base). */
+void orc_rotate_ex(int nsub, int nchan, int n, const float *in, const float *base, const double *delay,
+                   int per_profile, int identity, int sign, float *out)
 {
     const int m = n / 2;
+    const size_t P = (size_t)nsub * nchan;
+    if (identity) {
+        for (size_t k = 0; k < P; ++k) {
+            const float b = base ? base[k] : 0.0f;
+            for (int j = 0; j < n; ++j) out[k * n + j] = in[k * n + j] - b;
+        }
+        return;
+    }
     double *tw = (double *)malloc(sizeof(double) * 2 * (size_t)n);
-    double *ph = (double *)malloc(sizeof(double) * 2 * (size_t)nchan * (m + 1));
-    double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
+    double *ph = (double *)malloc(sizeof(double) * 2 * (per_profile ? P : (size_t)nchan) * (m + 1));
     orc_twiddles(n, tw);
-    orc_phasors(n, nchan, delay, ph);
-    free(work);
+    orc_phasors(n, per_profile ? (int)P : nchan, delay, ph);
 #pragma omp parallel
     {
     double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
 #pragma omp for schedule(dynamic, 64)
-    for (long k = 0; k < (long)nsub * nchan; ++k) {
-        const int c = (int)(k % nchan);
-        rotate1(n, in + (size_t)k * n, base ? base[k] : 0.0f, ph + (size_t)c * (m + 1) * 2, sign, tw, work,
+    for (long k = 0; k < (long)P; ++k) {
+        const size_t row = per_profile ? (size_t)k : (size_t)(k % nchan);
+        rotate1(n, in + (size_t)k * n, base ? base[k] : 0.0f, ph + row * (m + 1) * 2, sign, tw, work,
                 out + (size_t)k * n);
     }
     free(work);
     }
     free(tw); free(ph);
+}
+
+void orc_rotate(int nsub, int nchan, int n, const float *in, const float *base, const double *delay,
+                int sign, float *out)
+{
+    orc_rotate_ex(nsub, nchan, n, in, base, delay, 0, 0, sign, out);
 }
 
 /* ------------------------------------------------------ pairwise sums */
@@ -1135,6 +1183,8 @@ typedef struct {
     int32_t fit_mode;   /* 0: exact leastsq (orc_fit_residual), 1: closed form (orc_fit_closed) */
     int32_t data_f64;   /* 1: get_data returns f64 (orc_diagnostics_f64 / orc_test_f64) */
     int32_t dedisp_mode; /* 0: integer shifts; 1: FFT phase rotation by `delay` (orc_rotate) */
+    int32_t input_dedispersed; /* 1 (dedisp_mode 1): raw is stored dedispersed, its dedisperse a no-op */
+    int32_t delay_per_profile; /* 1 (dedisp_mode 1): `delay` is [nsub*nchan] */
 } orc_params;
 
 /* One full clean loop (iterative_cleaner.py:83-146).
@@ -1143,8 +1193,10 @@ typedef struct {
  * optional (may be NULL): R_last (P*nbin, dispersed frame, unweighted),
  * T_all (max_iter*nbin), amp_last/info_last (P),
  * diag_last: std, mean (P f64), ptp (P, f64 storage: f32 values unless data_f64), fft (P f64).
- * dedisp_mode 1: `delay` [nchan] f64 bins; every dedisperse / dededisperse of the
- * reference is the FFT phase rotation (archive.py with dm_delay), `shift` unused. */
+ * dedisp_mode 1: `delay` [nchan] f64 bins ([nsub*nchan] with delay_per_profile);
+ * every dedisperse / dededisperse of the reference is the FFT phase rotation
+ * (archive.py with dm_delay), `shift` unused; with input_dedispersed the raw
+ * cube is stored dedispersed, so only the dededisperse (:104) rotates. */
 int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, const int32_t *shift,
                    double *test, float *weights, int32_t *loops_out, int32_t *changed,
                    int32_t *nzero, float *R_last, float *T_all, double *amp_last,
@@ -1173,6 +1225,7 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
     memcpy(Wcur, w0, sizeof(float) * P);
     int nhist = 1;
     const int fftded = pp->dedisp_mode == 1;
+    const int ppd = fftded && pp->delay_per_profile, ided = fftded && pp->input_dedispersed;
     int32_t *zsh = fftded ? (int32_t *)calloc((size_t)nchan, sizeof(int32_t)) : NULL;
     float *dr = NULL, *Tc = NULL, *bs = NULL, *Rx = NULL;
     if (fftded) {
@@ -1182,9 +1235,9 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
         Tc = (float *)malloc(sizeof(float) * N);
         Rx = (float *)malloc(sizeof(float) * N);
         bs = (float *)malloc(sizeof(float) * P);
-        orc_rotate(nsub, nchan, n, raw, NULL, delay, 1, dr);
+        orc_rotate_ex(nsub, nchan, n, raw, NULL, delay, ppd, ided, 1, dr);
         orc_baseline(nsub, nchan, n, dr, w0, zsh, pp->baseline_duty, bs, NULL);
-        orc_rotate(nsub, nchan, n, raw, bs, delay, 1, D);
+        orc_rotate_ex(nsub, nchan, n, raw, bs, delay, ppd, ided, 1, D);
     } else {
         orc_fit_cube(nsub, nchan, n, raw, w0, shift, pp->baseline_duty, D);
     }
@@ -1193,7 +1246,7 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
         x += 1;
         if (fftded) {
             orc_baseline(nsub, nchan, n, dr, Wcur, zsh, pp->baseline_duty, bs, NULL);
-            orc_rotate(nsub, nchan, n, raw, bs, delay, 1, Tc);
+            orc_rotate_ex(nsub, nchan, n, raw, bs, delay, ppd, ided, 1, Tc);
             for (size_t k = 0; k < P; ++k) bs[k] = 0.0f;
             orc_scrunch(nsub, nchan, n, Tc, Wcur, zsh, bs, T);
         } else {
@@ -1205,7 +1258,7 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
         else
             orc_fit_residual((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
         /* dededisperse + apply_weights */
-        if (fftded) orc_rotate(nsub, nchan, n, Rd, NULL, delay, -1, Rx);
+        if (fftded) orc_rotate_ex(nsub, nchan, n, Rd, NULL, delay, ppd, 0, -1, Rx);
 #pragma omp parallel for schedule(static)
         for (int s = 0; s < nsub; ++s)
             for (int c = 0; c < nchan; ++c) {

@@ -25,7 +25,8 @@ class OrcParams(C.Structure):
                 ("subintthresh", C.c_double), ("pr_on", C.c_int32),
                 ("pr_factor", C.c_double), ("pr_start", C.c_int32), ("pr_end", C.c_int32),
                 ("baseline_duty", C.c_double), ("fit_mode", C.c_int32), ("data_f64", C.c_int32),
-                ("dedisp_mode", C.c_int32)]
+                ("dedisp_mode", C.c_int32), ("input_dedispersed", C.c_int32),
+                ("delay_per_profile", C.c_int32)]
 
 
 def _p(a):
@@ -60,6 +61,7 @@ def lib():
         _lib.orc_twiddles.argtypes = [C.c_int, C.c_void_p]
         _lib.orc_phasors.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         _lib.orc_rotate.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_int, C.c_void_p]
+        _lib.orc_rotate_ex.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_int] * 3 + [C.c_void_p]
     return _lib
 
 
@@ -142,14 +144,20 @@ def phasors(n, delay):
     return np.ascontiguousarray(np.moveaxis(ph, -1, 0))
 
 
-def rotate(cube, delay, sign=1, base=None):
+def rotate(cube, delay, sign=1, base=None, identity=False):
     """FFT phase rotation (fractional dedispersion) of a (nsub, nchan, n) cube:
-    rot(f32(cube - base)) by +delay (sign 1) or -delay (sign -1)."""
+    rot(f32(cube - base)) by +delay (sign 1) or -delay (sign -1); delay (nchan,)
+    per channel or (nsub, nchan) per profile (orc_rotate_ex); identity: the
+    no-op dedisperse of an archive stored dedispersed (f32(cube - base))."""
     cube = f32(cube)
     nsub, nchan, n = cube.shape
     out = np.empty_like(cube)
-    lib().orc_rotate(nsub, nchan, n, _p(cube), _p(None if base is None else f32(base)),
-                     _p(np.ascontiguousarray(delay, np.float64)), int(sign), _p(out))
+    d = np.ascontiguousarray(delay, np.float64)
+    per_profile = d.size == nsub * nchan and d.ndim == 2
+    if not per_profile:
+        d = d.reshape(nchan)
+    lib().orc_rotate_ex(nsub, nchan, n, _p(cube), _p(None if base is None else f32(base)), _p(d),
+                        1 if per_profile else 0, 1 if identity else 0, int(sign), _p(out))
     return out
 
 
@@ -189,20 +197,24 @@ def test_values(valid, std, mean, ptp, fft, ct, st):
 
 
 def clean_loop(raw, w0, shift, chanthresh=5.0, subintthresh=5.0, max_iter=5, pulse_region=None,
-               duty=0.15, want_residual=False, want_details=False, fit_mode=0, data_f64=False, delay=None):
+               duty=0.15, want_residual=False, want_details=False, fit_mode=0, data_f64=False, delay=None,
+               input_dedispersed=False):
     """Whole loop; returns dict(test, weights, loops, changed, nzero, [...]).
-    delay (nchan f64 bins): fractional dedispersion by FFT phase rotation
-    (dedisp_mode 1) instead of the integer `shift`."""
+    delay (nchan,) or (nsub, nchan) f64 bins: fractional dedispersion by FFT
+    phase rotation (dedisp_mode 1) instead of the integer `shift`;
+    input_dedispersed: raw is stored dedispersed (its dedisperse a no-op)."""
     raw = f32(raw)
     nsub, nchan, n = raw.shape
     P = nsub * nchan
     pr_on, fac, a, b = 0, 1.0, 0, 0
     if pulse_region is not None:
         pr_on, fac, a, b = 1, float(pulse_region[0]), int(pulse_region[1]), int(pulse_region[2])
+    per_profile = delay is not None and np.ndim(delay) == 2
     prm = OrcParams(nsub, nchan, n, max_iter, float(chanthresh), float(subintthresh), pr_on, fac, a, b, duty,
-                    int(fit_mode), 1 if data_f64 else 0, 0 if delay is None else 1)
+                    int(fit_mode), 1 if data_f64 else 0, 0 if delay is None else 1,
+                    1 if input_dedispersed else 0, 1 if per_profile else 0)
     if delay is not None:
-        delay = np.ascontiguousarray(delay, np.float64).reshape(nchan)
+        delay = np.ascontiguousarray(delay, np.float64).reshape((nsub, nchan) if per_profile else (nchan,))
     test = np.empty((nsub, nchan), np.float64)
     weights = np.empty((nsub, nchan), np.float32)
     loops = np.zeros(1, np.int32)

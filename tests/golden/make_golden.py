@@ -151,7 +151,8 @@ def _load_f64(path):
 
 def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
                    keep_cubes=True, npol=1, workdir=None, out_dir=HERE, residual_full=True, data_f64=False,
-                   frac_weights=False, frac_delay=False, poke=(), weights_zero=False):
+                   frac_weights=False, frac_delay=False, poke=(), weights_zero=False, frac_delay2=False,
+                   stored_dedispersed=False):
     data, weights, shift = synth.make_cube(nsub, nchan, nbin, seed, rfi, npol=npol)
     if weights_zero:                  # every profile zapped before the first loop
         weights = np.zeros_like(weights)
@@ -161,7 +162,12 @@ def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
         weights = synth.fractional_weights(weights)
     path = os.path.join(workdir, "%s.ar" % name)
     delay = synth.fractional_delays(shift, nbin) if frac_delay else None
+    if frac_delay2:            # per-(subint, channel): psrchive's per-Integration folding period
+        frac_delay = True
+        delay = synth.per_profile_delays(shift, nbin, nsub)
     ar = ica.Archive(data, weights, shift, filename=path, dm_delay=delay)
+    if stored_dedispersed:     # the archive is stored dedispersed: its dedisperse is a no-op
+        ar.dedisperse()
     ar.unload(path)
     loader = _load_f64 if data_f64 else ica.Archive_load
     ar = loader(path)
@@ -194,6 +200,8 @@ def run_clean_case(ic, name, nsub, nchan, nbin, seed, rfi, extra_args=(),
             "name": name, "nsub": nsub, "nchan": nchan, "nbin": nbin, "seed": seed,
             "rfi": rfi, "npol": npol, "extra_args": list(extra_args), "data_f64": bool(data_f64),
             "frac_weights": bool(frac_weights), "frac_delay": bool(frac_delay),
+            **({"frac_delay2": True} if frac_delay2 else {}),
+            **({"stored_dedispersed": True} if stored_dedispersed else {}),
             "args": {k: v for k, v in vars(args).items() if k != "archive"},
             "numpy": np.__version__, "scipy": scipy.__version__,
             **({"poke": [[int(a_), int(b_), int(c_), repr(float(v_))] for (a_, b_, c_, v_) in poke]}
@@ -593,7 +601,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--skip-big", action="store_true")
-    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64,fft,edge,cli_memory (later rounds' fixtures only)")
+    ap.add_argument("--only", default="", help="comma list: long,stats_long,zap,nonfinite,f64,fft,edge,cli_memory,"
+                                                "fft2 (later rounds' fixtures only)")
     a = ap.parse_args()
     ic = import_reference()
     only = set(filter(None, a.only.split(",")))
@@ -612,6 +621,8 @@ def main():
             run_fft_cases(ic, a.out)
         if "edge" in only:
             run_edge_cases(ic, a.out)
+        if "fft2" in only:
+            run_fft2_cases(ic, a.out)
         if "cli_memory" in only:
             run_cli_memory_case(ic, a.out)
             run_cli_std_name_case(ic, a.out)
@@ -643,6 +654,26 @@ def main():
     run_edge_cases(ic, a.out)
     run_cli_memory_case(ic, a.out)
     run_cli_std_name_case(ic, a.out)
+    run_fft2_cases(ic, a.out)
+
+
+def run_fft2_cases(ic, out_dir=HERE):
+    """Round 6: archives as psrchive holds them.  Per-(subint, channel) delays
+    (each Integration's own folding period: every dedisperse / dededisperse is
+    the FFT rotation by that profile's delay), and archives stored dedispersed
+    (dedisperse at ic.py:91 / :100 a no-op, only :104 rotates), with integer
+    shifts and with fractional delays."""
+    with tempfile.TemporaryDirectory() as wd:
+        run_clean_case(ic, "s12x48x128_fft_pp", 12, 48, 128, 3, 0.05, frac_delay2=True, workdir=wd,
+                       out_dir=out_dir)
+        run_clean_case(ic, "s6x48x1024_fft_pp_u", 6, 48, 1024, 43, 0.05, extra_args=("-u",), frac_delay2=True,
+                       keep_cubes=False, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s8x40x256_fft_ded", 8, 40, 256, 21, 0.2, frac_delay=True, stored_dedispersed=True,
+                       keep_cubes=False, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s6x40x128_fft_pp_ded_u", 6, 40, 128, 22, 0.2, extra_args=("-u",), frac_delay2=True,
+                       stored_dedispersed=True, keep_cubes=False, workdir=wd, out_dir=out_dir)
+        run_clean_case(ic, "s10x40x128_ded_u", 10, 40, 128, 23, 0.2, extra_args=("-u",), stored_dedispersed=True,
+                       keep_cubes=False, workdir=wd, out_dir=out_dir)
 
 
 def run_edge_cases(ic, out_dir=HERE):

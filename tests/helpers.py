@@ -35,18 +35,36 @@ def load_clean_case(path):
     if meta.get("weights_zero"):
         w0 = np.zeros_like(w0)
     raw = data[:, 0] if meta["npol"] == 1 else (data[:, 0] + data[:, 1]).astype(np.float32)
-    return z, meta, np.ascontiguousarray(raw), w0, shift, meta["args"]
+    raw = np.ascontiguousarray(raw)
+    if meta.get("stored_dedispersed") and meta.get("frac_delay"):
+        # the archive as stored: dedispersed by the stand-in's FFT rotation; the
+        # session takes it with input_dedispersed (case_kwargs).  (Integer
+        # shifts: the host rolls a stored-dedispersed cube back exactly, so the
+        # session's input is the dispersed synthetic cube itself.)
+        from iterative_cleaner_amd import phase_rotation as pr
+        d = case_delay(z, meta)
+        raw = pr.rotate(raw, pr.phasors(meta["nbin"], d), 1)
+    return z, meta, raw, w0, shift, meta["args"]
 
 
 def case_delay(z, meta):
-    """The fractional per-channel delays of a fixture made with frac_delay (FFT
-    phase-rotation dedispersion), else None (integer shifts)."""
+    """The fractional delays of a fixture made with frac_delay (FFT
+    phase-rotation dedispersion): (nchan,), or (nsub, nchan) with frac_delay2
+    (per-Integration periods); else None (integer shifts)."""
     if not meta.get("frac_delay"):
         return None
     d = np.asarray(z["dm_delay"], dtype=np.float64)
-    assert np.array_equal(d, synth.fractional_delays(synth.make_cube(1, meta["nchan"], meta["nbin"], 0, 0.0)[2],
-                                                     meta["nbin"])), "delay generator drifted"
+    shift = synth.make_cube(1, meta["nchan"], meta["nbin"], 0, 0.0)[2]
+    want = synth.per_profile_delays(shift, meta["nbin"], meta["nsub"]) if meta.get("frac_delay2") \
+        else synth.fractional_delays(shift, meta["nbin"])
+    assert np.array_equal(d, want), "delay generator drifted"
     return d
+
+
+def case_kwargs(z, meta):
+    """Session keywords of a fixture's dedispersion: delay and input_dedispersed."""
+    d = case_delay(z, meta)
+    return dict(delay=d, input_dedispersed=bool(meta.get("stored_dedispersed")) and d is not None)
 
 
 def bits_equal(a, b):

@@ -90,3 +90,43 @@ def test_slice_without_sharding_is_refused():
     with pytest.raises(ValueError):
         cleaner.run_loop(np.zeros((2, 3, 8), np.float32), np.ones((2, 3), np.float32), np.zeros(3, np.int64),
                          args, nchan_total=6)
+
+
+# ------------------------------------------------------------ psrchive's dedispersion
+def test_dedispersion_of_a_psrchive_like_archive():
+    """An archive with only psrchive's methods: delays from DM, channel
+    frequencies and each Integration's folding period (dedispersion.py);
+    per-profile when the periods differ, per-channel when they agree, integer
+    shifts when every delay is integral, an error at an nbin the rotation cannot
+    serve (never a silent rounding)."""
+    from psrchive_like import PsrchiveLike
+
+    from iterative_cleaner_amd import cleaner, dedispersion
+    data = np.zeros((4, 1, 6, 128), np.float32)
+    w = np.ones((4, 6), np.float32)
+    freqs = 150.0 + np.arange(6) * 0.5
+    per = np.array([0.1, 0.1000001, 0.0999999, 0.1])
+    shift, delay = cleaner._dedispersion(PsrchiveLike(data, w, 12.0, freqs, per, 151.0))
+    assert np.array_equal(shift, np.zeros(6)) and delay.shape == (4, 6)
+    assert np.array_equal(delay, dedispersion.delays_from_dm(12.0, freqs, 151.0, per, 128))
+    shift, delay = cleaner._dedispersion(PsrchiveLike(data, w, 12.0, freqs, np.full(4, 0.1), 151.0))
+    assert delay.shape == (6,)
+    shift, delay = cleaner._dedispersion(PsrchiveLike(data, w, 0.0, freqs, per, 151.0))
+    assert delay is None and np.array_equal(shift, np.zeros(6))
+    with pytest.raises(ValueError, match="power-of-two nbin"):
+        cleaner._dedispersion(PsrchiveLike(np.zeros((4, 1, 6, 100), np.float32), w, 12.0, freqs, per, 151.0))
+
+
+def test_stored_dedispersed_integer_archive_rolls_back_exactly():
+    """An archive stored dedispersed with integer shifts: the host moves its
+    samples back to the dispersed frame (cleaner._to_dispersed), exactly: the
+    stand-in's own dedisperse of that gives the stored samples bit for bit."""
+    from iterative_cleaner_amd import archive as ica
+    from iterative_cleaner_amd import cleaner, synth
+    data, w, shift = synth.make_cube(3, 10, 64, 2, 0.2, npol=2)
+    src = ica.Archive(data, w, shift)
+    src.dedisperse()
+    stored = src.get_data()
+    back = cleaner._to_dispersed(stored, shift)
+    assert np.array_equal(back, data)
+    assert cleaner._stored_dedispersed(src) and not cleaner._stored_dedispersed(ica.Archive(data, w, shift))

@@ -8,7 +8,8 @@ import os
 import numpy as np
 import pytest
 
-from helpers import bits_equal, bits_equal_nan, case_delay, clean_fixtures, load_clean_case, nan_equal, poke_cube
+from helpers import (bits_equal, bits_equal_nan, case_delay, case_kwargs, clean_fixtures, load_clean_case, nan_equal,
+                     poke_cube)
 
 pytestmark = pytest.mark.gpu
 
@@ -20,12 +21,12 @@ TEST_ATOL = 1e-9
 FIT_MODES = {"rounds": 0, "tail": 1 << 40, "default": None}
 
 
-def _session(shape, args, duty=0.15, fit_mode="default", data_f64=False, delay=None):
+def _session(shape, args, duty=0.15, fit_mode="default", data_f64=False, delay=None, input_dedispersed=False):
     from iterative_cleaner_amd import _native
     nsub, nchan, nbin = shape
     s = _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"],
                            args["subintthresh"], args["pulse_region"], duty, device=0, data_f64=data_f64,
-                           delay=delay)
+                           delay=delay, input_dedispersed=input_dedispersed)
     if FIT_MODES[fit_mode] is not None:
         s.set_fit_tail(FIT_MODES[fit_mode])
     return s
@@ -53,7 +54,7 @@ def test_loop_matches_reference(path, fit_mode):
     z, meta, raw, w0, shift, args = load_clean_case(path)
     nit = int(z["n_iter"])
     with _session(raw.shape, args, fit_mode=fit_mode, data_f64=meta.get("data_f64", False),
-                  delay=case_delay(z, meta)) as s:
+                  **case_kwargs(z, meta)) as s:
         s.upload(raw, w0, shift)
         out = s.run()
         T = s.template()
@@ -90,7 +91,7 @@ def test_every_iteration_matches_reference(path):
     nit = int(z["n_iter"])
     for k in range(1, nit):
         a = dict(args, max_iter=k)
-        with _session(raw.shape, a, data_f64=meta.get("data_f64", False), delay=case_delay(z, meta)) as s:
+        with _session(raw.shape, a, data_f64=meta.get("data_f64", False), **case_kwargs(z, meta)) as s:
             s.upload(raw, w0, shift)
             out = s.run()
             T = s.template()
@@ -124,7 +125,10 @@ def test_clean_stdout_matches_reference(path, tmp_path, monkeypatch, capsys):
     poke_cube(data, meta)
     monkeypatch.chdir(tmp_path)
     arpath = str(tmp_path / ("%s.ar" % meta["name"]))
-    ica.Archive(data, w0_, shift_, filename=arpath, dm_delay=case_delay(z, meta)).unload(arpath)
+    src = ica.Archive(data, w0_, shift_, filename=arpath, dm_delay=case_delay(z, meta))
+    if meta.get("stored_dedispersed"):
+        src.dedisperse()
+    src.unload(arpath)
     ar = ica.Archive_load(arpath)
     plain_load = ica.Archive_load       # the fixture read the residual archive through this one
     if meta.get("data_f64"):

@@ -6,7 +6,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import (GOLDEN, bits_equal, bits_equal_nan, case_delay, clean_fixtures, load_clean_case, long_stats_cases, nan_equal,
+from helpers import (GOLDEN, bits_equal, bits_equal_nan, case_delay, case_kwargs, clean_fixtures, load_clean_case, long_stats_cases, nan_equal,
                      thresholds)
 
 
@@ -145,7 +145,7 @@ def test_clean_loop_c_oracle(path, oracle_lib):
         pr = (fac, a, b)
     out = oracle_lib.clean_loop(raw, w0, shift, args["chanthresh"], args["subintthresh"],
                                 args["max_iter"], pr, want_details=True, data_f64=meta.get("data_f64", False),
-                                delay=case_delay(z, meta))
+                                **case_kwargs(z, meta))
     nit = int(z["n_iter"])
     assert out["loops"] == int(z["loops"])
     for k in range(1, nit + 1):
@@ -166,7 +166,8 @@ def test_first_iteration_residual_and_diagnostics(oracle_lib):
     """Iteration-1 residual cube (f32, dedispersed) bit-exact on the small fixtures."""
     for path in clean_fixtures():
         z, meta, raw, w0, shift, args = load_clean_case(path)
-        if "residual_ded_1" not in z.files or args["pulse_region"] != [0, 0, 1] or meta.get("frac_delay"):
+        if "residual_ded_1" not in z.files or args["pulse_region"] != [0, 0, 1] or meta.get("frac_delay") \
+                or meta.get("stored_dedispersed"):
             continue
         D = oracle_lib.fit_cube(raw, w0, shift)
         T = oracle_lib.template(raw, w0, shift)

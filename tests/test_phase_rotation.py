@@ -92,19 +92,15 @@ def test_archive_fft_dedisperse_roundtrip_and_io(tmp_path):
         assert np.array_equal(sl.get_dm_delay(), delay[4:9])
     with pytest.raises(ValueError):
         ica.Archive(data[..., :48], w, shift, dm_delay=delay)
-    # a foreign PSRFITS file (no stand-in columns): fractional delays from DM only on request
+    # a foreign PSRFITS file (no stand-in columns): psrchive's fractional delays from DM
+    from iterative_cleaner_amd import dedispersion
     fr = ica.Archive(data, w, shift)
     fr._chan_freqs = 1400.0 + np.arange(12) * 8.0
     fr._period = 0.05
     fr._dm = 30.0
     p = str(tmp_path / "foreign.sf")
     psrfits.save(fr, p, stand_in_meta=False)
-    assert psrfits.load(p).get_dm_delay() is None
-    import os
-    os.environ["IC_DEDISPERSION"] = "fft"
-    try:
-        fa = psrfits.load(p)
-    finally:
-        del os.environ["IC_DEDISPERSION"]
-    fd = fa.get_dm_delay()
-    assert fd is not None and np.array_equal(np.rint(fd).astype(np.int64) % 64, fa.get_dm_shift())
+    fa = psrfits.load(p)
+    want = dedispersion.delays_from_dm(30.0, fr._chan_freqs, 1400.0, [0.05] * 3, 64)[0]
+    assert np.array_equal(fa.get_dm_delay(), want)
+    assert np.array_equal(fa.get_dm_shift(), np.zeros(12, np.int64))

@@ -63,18 +63,61 @@ def test_header_cards_and_columns(tmp_path):
     assert all(32 <= b < 127 for b in raw[:psrfits.BLOCK])
 
 
-def test_foreign_file_shifts_from_dm(tmp_path):
-    """Without the stand-in's IC_SHIFT column the integer delays come from DM,
-    DAT_FREQ and PERIOD (cleaner._dm_shift's integer approximation)."""
+def test_foreign_file_delays_from_dm(tmp_path):
+    """Without the stand-in's IC_SHIFT column a file is dedispersed as psrchive
+    would (dedispersion.py): fractional delays from DM, DAT_FREQ, OBSFREQ and the
+    row's PERIOD, taken by the FFT phase rotation, never rounded; one row per
+    channel when every row has the same period."""
+    from iterative_cleaner_amd import dedispersion
     ar = synth.make_archive(2, 8, 64, seed=2)
     ar._dm, ar._period = 30.0, 0.05
     ar._chan_freqs = 1400.0 + np.arange(8) * 10.0 - 35.0
     p = str(tmp_path / "f.fits")
     psrfits.save(ar, p, stand_in_meta=False)
     br = psrfits.load(p)
-    delay = 4.148808e3 * 30.0 * (ar._chan_freqs ** -2 - 1400.0 ** -2)
-    assert np.array_equal(br.get_dm_shift(), np.rint(delay / 0.05 * 64).astype(np.int64) % 64)
+    f = ar._chan_freqs
+    want = (30.0 * (1.0 / 2.41e-4)) * (1.0 / (f * f) - 1.0 / (1400.0 * 1400.0)) / 0.05 * 64
+    assert np.array_equal(br.get_dm_delay(), want)
+    assert np.array_equal(br.get_dm_delay(), dedispersion.delays_from_dm(30.0, ar._chan_freqs, 1400.0,
+                                                                          [0.05, 0.05], 64)[0])
+    assert np.array_equal(br.get_dm_shift(), np.zeros(8, np.int64))
     assert br.get_dedispersed() is False and br.get_baseline_duty() == 0.15
+    # a channel slice carries the whole band's delays for its channels
+    sl = psrfits.load(p, channels=(2, 6))
+    assert np.array_equal(sl.get_dm_delay(), want[2:6])
+
+
+def test_foreign_file_per_row_periods_give_per_profile_delays(tmp_path):
+    """psrchive dedisperses each Integration with its own folding period: rows
+    of different PERIOD give (nsub, nchan) delays (ic_set_delays2), and the file
+    round-trips them through the stand-in's IC_DELAY column."""
+    ar = synth.make_archive(3, 8, 128, seed=5)
+    ar._dm, ar._period = 12.5, np.array([0.0331, 0.03310002, 0.0330998])
+    ar._chan_freqs = 150.0 + np.arange(8) * 0.2
+    ar._cfreq = 150.7
+    p = str(tmp_path / "g.fits")
+    psrfits.save(ar, p, stand_in_meta=False)
+    br = psrfits.load(p)
+    d = br.get_dm_delay()
+    assert d.shape == (3, 8)
+    f = ar._chan_freqs
+    t = (12.5 * (1.0 / 2.41e-4)) * (1.0 / (f * f) - 1.0 / (150.7 * 150.7))
+    assert np.array_equal(d, t[None, :] / ar._period[:, None] * 128.0)
+    q = str(tmp_path / "g2.fits")
+    br.unload(q)
+    assert np.array_equal(psrfits.load(q).get_dm_delay(), d)
+
+
+def test_foreign_file_integral_delays_are_shifts(tmp_path):
+    """DM 0 (or any set of integral delays): integer shifts, no FFT rotation."""
+    ar = synth.make_archive(2, 8, 100, seed=2)
+    ar._dm, ar._period = 0.0, 0.05
+    ar._chan_freqs = 1400.0 + np.arange(8) * 10.0 - 35.0
+    p = str(tmp_path / "z.fits")
+    psrfits.save(ar, p, stand_in_meta=False)
+    br = psrfits.load(p)
+    assert br.get_dm_delay() is None
+    assert np.array_equal(br.get_dm_shift(), np.zeros(8, np.int64))
 
 
 def test_npz_archives_stay_npz(tmp_path):
@@ -86,18 +129,14 @@ def test_npz_archives_stay_npz(tmp_path):
 
 
 @pytest.mark.parametrize("nbin", [100, 32])
-def test_fft_dedispersion_falls_back_for_unsupported_nbin(tmp_path, monkeypatch, nbin):
-    """IC_DEDISPERSION=fft with a profile length the rotation kernels do not take
-    (not a power of two in 64..4096): the archive still loads, with the integer
-    shift and a warning, instead of failing the load or the GPU session."""
+def test_fractional_delays_at_unsupported_nbin_fail_loudly(tmp_path, nbin):
+    """Fractional delays with a profile length the rotation kernels do not take
+    (not a power of two in 64..4096): the load fails with the reason instead of
+    rounding the delays (which would change which profiles get zapped)."""
     ar = synth.make_archive(2, 8, nbin, seed=4)
     ar._dm, ar._period = 30.0, 0.05
     ar._chan_freqs = 1400.0 + np.arange(8) * 10.0 - 35.0
     p = str(tmp_path / "u.fits")
     psrfits.save(ar, p, stand_in_meta=False)
-    monkeypatch.setenv("IC_DEDISPERSION", "fft")
-    with pytest.warns(UserWarning, match="integer shift"):
-        br = psrfits.load(p)
-    delay = 4.148808e3 * 30.0 * (ar._chan_freqs ** -2 - 1400.0 ** -2)
-    assert np.array_equal(br.get_dm_shift(), np.rint(delay / 0.05 * nbin).astype(np.int64) % nbin)
-    assert br.get_dm_delay() is None
+    with pytest.raises(ValueError, match="power-of-two nbin"):
+        psrfits.load(p)

@@ -58,24 +58,29 @@ def test_cli_stokes_archive_cleans_total_intensity(tmp_path, monkeypatch, capsys
     assert bits_equal(res.get_weights(), ref["weights"])
 
 
-def test_cli_foreign_psrfits_fractional_dedispersion(tmp_path, monkeypatch, capsys, oracle_lib):
+@pytest.mark.parametrize("periods", ["constant", "per_row"])
+def test_cli_foreign_psrfits_fractional_dedispersion(tmp_path, monkeypatch, capsys, oracle_lib, periods):
     """A PSRFITS file without the stand-in's columns, with DM / DAT_FREQ / PERIOD:
-    IC_DEDISPERSION=fft dedisperses by the FFT phase rotation with the exact
-    fractional delays (psrfits.fractional_dedispersion); the zap mask equals the
-    C oracle's loop with those delays."""
+    dedispersed as psrchive would, by default (no switch): the FFT phase rotation
+    by the fractional delays from DM, the channel frequencies and each row's
+    folding period (per-profile delays, ic_set_delays2, when the rows' periods
+    differ).  The zap mask equals the C oracle's loop with those delays."""
     from iterative_cleaner_amd import archive as ica
-    from iterative_cleaner_amd import cleaner, psrfits, synth
+    from iterative_cleaner_amd import cleaner, dedispersion, psrfits, synth
     monkeypatch.chdir(tmp_path)
+    monkeypatch.delenv("IC_DEDISPERSION", raising=False)
     data, w, shift = synth.make_cube(10, 64, 256, 61, 0.2, npol=2)
     ar = ica.Archive(data, w, np.zeros(64, np.int64), filename="dm.sf")
     ar._chan_freqs = 1300.0 + np.arange(64) * 3.0
-    ar._period = 0.0125
+    ar._period = 0.0125 if periods == "constant" else 0.0125 * (1.0 + 3e-4 * np.cos(np.arange(10)))
     ar._dm = 20.0
     psrfits.save(ar, "dm.sf", stand_in_meta=False)
-    monkeypatch.setenv("IC_DEDISPERSION", "fft")
     src = psrfits.load("dm.sf")
     delay = src.get_dm_delay()
     assert delay is not None and np.any(delay != np.rint(delay))
+    assert delay.shape == ((64,) if periods == "constant" else (10, 64))
+    want = dedispersion.delays_from_dm(20.0, ar._chan_freqs, 1400.0, np.broadcast_to(ar._period, (10,)), 256)
+    assert np.array_equal(delay, want[0] if periods == "constant" else want)
     dec = src.get_data()
     cube = (dec[:, 0] + dec[:, 1]).astype(np.float32)
     ref = oracle_lib.clean_loop(cube, src.get_weights(), src.get_dm_shift(), delay=delay)
