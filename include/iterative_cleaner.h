@@ -263,6 +263,11 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  *                          on the second stream beside the tail, only the
  *                          tail's profiles after it: IC_TAIL_SPLIT_OFF, _ON, or
  *                          _AUTO (on for nbin >= 2048); IC_TAIL_SPLIT_AUTO
+ *   IC_OPT_ROT_STATS       FFT dedispersion at nbin 1024 (f32 data): 1 = the
+ *                          residual's inverse rotation measures its rows in the
+ *                          same kernel (the rotated residual never goes to
+ *                          HBM), 0 = it writes them and a statistics pass reads
+ *                          them back; 1
  *   IC_OPT_SYNC_TIMEOUT_MS longest host wait for the GPU, >= 1 ms; 600000.  A
  *                          wait that runs out fails its call with IC_EHIP and
  *                          marks the session failed: every later call on it
@@ -282,6 +287,7 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
 /* 11, 12: IC_OPT_FIT_LANE_WAVES, IC_OPT_FIT_LATE_LANES until round 4 (removed
  * with the lanes schedule) */
 #define IC_OPT_TAIL_SPLIT 13
+#define IC_OPT_ROT_STATS 14
 #define IC_TAIL_SPLIT_OFF 0
 #define IC_TAIL_SPLIT_ON 1
 #define IC_TAIL_SPLIT_AUTO 2

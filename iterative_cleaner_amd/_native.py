@@ -32,7 +32,7 @@ EXPORTS = ("ic_abi_version", "ic_device_count", "ic_session_create", "ic_session
 # choose how the loop is scheduled, never its arithmetic
 OPTIONS = {"fit_tail": 1, "diag_fork": 2, "fork_delay": 3, "template_incr": 4, "fit_tiled": 5,
            "rowstat_waves": 6, "rowstat_minlen": 7, "diag_chain": 8, "sync_timeout_ms": 9,
-           "fit_schedule": 10, "tail_split": 13}
+           "fit_schedule": 10, "tail_split": 13, "rot_stats": 14}
 FIT_ROUNDS = 0   # IC_FIT_ROUNDS: sweep / state rounds (k_fit_pass, k_fit_state, k_fit_tail); the only schedule
 
 FIT_EXACT = 0    # IC_FIT_EXACT: scipy leastsq emulated bit for bit (the reference's arithmetic)

@@ -379,9 +379,19 @@ struct RotateArgs {
     int in_tiled, out2_tiled;
     const uint8_t *late;
     int late_sel;
+    // statistics of the rotated rows (std_o != nullptr; residual input, sign
+    // -1, rotate_stats_supported): instead of writing row p to out, the kernel
+    // measures X = f32(row * w0[p]) as k_diag's DIAG_STATS pass would (ic.py:
+    // 111-117, :206-212) and writes std / mean / ptp / fftmax of p; out unused
+    const float *w0;
+    const double2 *tw_p2;       // k_diag_p2's twiddle table (p2_twiddles)
+    double *std_o, *mean_o, *ptp_o, *fft_o;
 };
 hipError_t launch_rotate(hipStream_t st, const RotateArgs &a);
 bool rotate_supported(int nbin);
+// the residual rotation can carry the statistics (RotateArgs.std_o): f32 rows
+// whose rotation keeps a profile in one wave's registers (nbin 1024)
+bool rotate_stats_supported(int nbin, bool data_f64);
 // D == nullptr: fit-cube rows formed from raw and base (fit_mode 1)
 hipError_t launch_residual(hipStream_t st, const float *D, const float *raw, const float *base, const double *T64,
                            const double *amp, const int32_t *info, const int32_t *shift, int nsub, int nchan,

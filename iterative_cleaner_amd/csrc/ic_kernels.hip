@@ -3709,9 +3709,157 @@ __device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
     return make_double2(er - oi, ei + orr);
 }
 
+// comprehensive_stats (ic.py:206-212) of the rotated residual row held by one
+// wave in the direct layout: z[q] = point j = t + TB q, i.e. R[2j] = f32(z.re /
+// M), R[2j + 1] = f32(-z.im / M) (k_rotate's store), X = f32(R w) (apply_weights,
+// ic.py:111-117, 296).  Every value is k_diag_cl<N, DIAG_STATS>'s, bit for bit:
+// - mean / var / ptp: X goes through the wave's LDS slots once (the padded
+//   xaddr image) and each lane reads its pairwise chain (leaf t/8, accumulator
+//   t%8: samples 128(t/8) + t%8 + 8q); the trees are chain_total's;
+// - fftmax: k_diag_cl's first radix-8 stage reads the points t + 64 r of d =
+//   f64(X) - mean, which is exactly the direct layout this lane holds, so the
+//   rFFT starts from registers; the later stages are p2_fft's with its table
+//   (tw_p2: through L1, the LDS holds only the rotation's tables), the
+//   spectrum's post twiddles tw[k < M] come from the rotation's plain LDS table
+//   (the same long double values: exp(-2 pi i q / N) built by one formula).
+template <int N, typename TW>
+__device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2 *v, const TW &tw, int t,
+                                          double2 (&z)[8], double inv, float w)
+{
+    constexpr int M = RotCfg<N>::M, H = M / 2, TB = RotCfg<N>::TB, L = TB;
+    static_assert(N == 1024 && TB == 64 && CLay<N>::L == 64, "one wave per profile, 16 samples per lane");
+    float xr[16];   // sample 2(t + 64 q) + e at xr[2q + e]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        xr[2 * q] = (float)(z[q].x * inv);
+        xr[2 * q + 1] = (float)((-z[q].y) * inv);
+    }
+    if (w != 1.0f) {   // fractional weights (w * 1 = w exactly: skipped)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) xr[e] = xr[e] * w;
+    }
+    const bool valid = w != 0.0f;
+    double mean = 0.0, sd = 0.0, fftv = 0.0, ptp = (double)1e20f;
+    if (valid) {
+        // the row into LDS (the last pass's reads of v are done: rot_pass ends
+        // with gsync), float pairs at xaddr(2j) = 2t + 136 q
+        float *xs = (float *)v;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) *(float2 *)(xs + 2 * t + 136 * q) = make_float2(xr[2 * q], xr[2 * q + 1]);
+        wave_sync();
+        float X[16];
+        {
+            const float *xc = xs + 136 * (t >> 3) + (t & 7);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) X[q] = xc[8 * q];
+        }
+        float s = X[0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) s = s + X[q];
+        float fs[1] = {s};
+        const float s32 = 0.0f + chain_total<N, float>(fs, (float *)nullptr, 0, t);
+        mean = (double)s32 / (double)N;
+        double r = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const double d = (double)X[q] - mean;
+            const double sq = d * d;
+            r = q == 0 ? sq : r + sq;
+        }
+        double rs[1] = {r};
+        const double ss = 0.0 + chain_total<N, double>(rs, (double *)nullptr, 0, t);
+        sd = sqrt(ss / (double)N);
+        float mx = -INFINITY, mn = INFINITY;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            mx = OpMaxF()(mx, X[q]);
+            mn = OpMinF()(mn, X[q]);
+        }
+        mx = group_tree<1, 64>(mx, OpMaxF(), (float *)nullptr, 0, t);
+        mn = group_tree<1, 64>(mn, OpMinF(), (float *)nullptr, 0, t);
+        int nan = 0;
+        if (isnan(s32)) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) nan |= isnan(X[q]);
+            nan = group_tree<1, 64>(nan, OpOr(), (int *)nullptr, 0, t);
+        }
+        ptp = nan ? (double)NAN : (double)(float)(mx - mn);
+        // rfft of d (ic.py:210-212): stage 1 (radix 8, no twiddles) on the
+        // lane's points t + 64 r, then k_diag_p2's stages in the complex work
+        // array Cb = v (cidx slots, M entries: inside the rotation's padded
+        // array).  The chain reads above precede the stores (one wave: its LDS
+        // operations stay in order)
+        double2 c8[8];
+#pragma unroll
+        for (int r8 = 0; r8 < 8; ++r8) c8[r8] = make_double2((double)xr[2 * r8] - mean, (double)xr[2 * r8 + 1] - mean);
+        dft_small<8>(c8);
+        double2 *Cb = v;
+        {
+            const int A = 8 * t + (t & 7);   // cidx(8t + r) = A ^ r
+#pragma unroll
+            for (int r8 = 0; r8 < 8; ++r8) Cb[A ^ r8] = c8[r8];
+        }
+        wave_sync();
+        p2_fft<M, L, CLay<N>::LG, 3, 8, M, float, false>(Cb, (const float *)nullptr, 0.0, a.tw_p2, t);
+        // the spectrum in conjugate bin pairs (k_diag_cl's post, 2 X_k)
+        constexpr int JF = H / L;
+        double best2 = 0.0;
+        auto post = [&](const double2 zk, const double2 zm, const double2 wv) {
+            const double er = zk.x + zm.x, ei = zk.y - zm.y;
+            const double orr = zk.y + zm.y, oi = zm.x - zk.x;
+            const double tr = __builtin_fma(orr, wv.x, -(oi * wv.y));
+            const double ti = __builtin_fma(orr, wv.y, oi * wv.x);
+            const double re = er + tr, im = ei + ti;
+            const double rm = er - tr, imm = ti - ei;
+            const double a2 = __builtin_fma(re, re, im * im);
+            const double b2 = __builtin_fma(rm, rm, imm * imm);
+            best2 = fmax(best2, fmax(a2, b2));
+        };
+#pragma unroll
+        for (int j = 0; j < JF; ++j) {
+            const int kk = t + L * j;
+            const double2 zk = Cb[cidx(t) + L * j];
+            const double2 zm = Cb[kk == 0 ? 0 : cidx(L - t) + (M - L * (j + 1))];
+            post(zk, zm, tw.post((unsigned)kk));
+        }
+        {
+            // the self-paired bin k = M/2 (k_diag_cl)
+            const double2 zc = Cb[cidx(H)], wv = tw.post((unsigned)H);
+            const double er = zc.x + zc.x, orr = zc.y + zc.y;
+            const double tr = orr * wv.x, ti = orr * wv.y;
+            const double re = er + tr, rm = er - tr, q2 = ti * ti;
+            best2 = fmax(best2, fmax(__builtin_fma(re, re, q2), __builtin_fma(rm, rm, q2)));
+        }
+        best2 = group_tree<1, 64>(best2, OpMaxF(), (double *)nullptr, 0, t);
+        // a non-finite f32 sum means a NaN / Inf sample: some bin is NaN (k_diag_cl)
+        fftv = isfinite(s32) ? 0.5 * sqrt(best2) : (double)NAN;
+    } else {
+        // w = 0: rfft of f64(X) = +-0 -> 0, unless R was non-finite (X NaN)
+        int nanx = 0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) nanx |= isnan(xr[e]);
+        nanx = group_tree<1, 64>(nanx, OpOr(), (int *)nullptr, 0, t);
+        fftv = nanx ? NAN : 0.0;
+    }
+    if (t == 0) {
+        a.std_o[p] = valid && isfinite(mean) ? sd : 0.0;   // numpy.ma: a non-finite mean is masked -> std 0
+        a.mean_o[p] = valid ? mean : 0.0;
+        a.ptp_o[p] = ptp;
+        a.fft_o[p] = fftv;
+    }
+}
+
 // PP: per-profile delays (a.delay2, ic_set_delays2): each lane evaluates its
 // phasors with ic_phasor instead of loading the channel's table row.
-template <int N, bool PP>
+// ST: the residual's rotation measures its rows instead of storing them
+// (RotateArgs.std_o; the direct layout only): the rotated row R, still in the
+// lane's registers, becomes X = f32(R w0), whose mean / var / ptp run on the
+// numpy pairwise chains (one LDS transposition into k_diag_cl's chain layout,
+// the same trees: the same bits) and whose real spectrum comes from a third
+// pass of the rotation's own FFT (max |rfft|, within 1e-9 of numpy like every
+// diagnostics kernel's).  R never goes to HBM: the residual's 4N write and the
+// statistics pass's 4N read are gone, and so is the R buffer.
+template <int N, bool PP, bool ST = false>
 // 3 waves per SIMD at N <= 1024 (4 spilled 21 VGPRs; 3, 154 VGPRs: C2 fft 57.0 -> 56.4 ms)
 __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) void k_rotate(RotateArgs a)
 {
@@ -3789,6 +3937,9 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         double2 phn[2];
         ldph(0, phn);
         double2 z[8];
+        static_assert(!ST || DIRECT, "the statistics epilogue needs the direct layout");
+        float wst = 1.0f;   // ST: the profile's weight, requested with the rows
+        if constexpr (ST) wst = a.w0[p];
         if constexpr (DIRECT) {
             const size_t k = p;
             float2 x2[8];
@@ -3916,7 +4067,10 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         }
         gsync<TB / 64>();
         float *o = a.out + p * (size_t)a.ldo;
-        if constexpr (DIRECT) {
+        if constexpr (ST) {
+            rot_fft<N, 0, false, true>(v, tw, t, z);
+            rot_stats<N>(a, p, v, tw, t, z, inv, wst);
+        } else if constexpr (DIRECT) {
             rot_fft<N, 0, false, true>(v, tw, t, z);
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -5083,6 +5237,8 @@ bool rotate_supported(int nbin)
     }
 }
 
+bool rotate_stats_supported(int nbin, bool data_f64) { return nbin == 1024 && !data_f64; }
+
 // The identity "rotation" of an archive stored dedispersed (its dedisperse is a
 // no-op, archive.py dedisperse): out[p] = f32(in[p] - base[p]) (and out2), for
 // the subints flags selects; a wave per profile, 16-byte rows.
@@ -5106,7 +5262,12 @@ hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
 {
     const size_t P = (size_t)a.nsub * a.nchan;
     if (P == 0) return hipSuccess;
-    if (!rotate_supported(a.nbin) || !a.in || !a.out || !a.tw || a.ld_in < a.nbin || a.ldo < a.nbin ||
+    const bool stats = a.std_o != nullptr;
+    if (stats && (!rotate_stats_supported(a.nbin, false) || !a.amp || a.sign > 0 || a.out2 || !a.w0 || !a.tw_p2 || !a.mean_o ||
+                  !a.ptp_o || !a.fft_o))
+        return hipErrorInvalidValue;
+    if (!rotate_supported(a.nbin) || !a.in || (!a.out && !stats) || !a.tw || a.ld_in < a.nbin ||
+        (!stats && a.ldo < a.nbin) ||
         (!a.ph && !a.delay2 && !a.identity) ||
         (a.ld_in & 3) || (a.ldo & 3) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 3))) ||
         (a.amp && (!a.T64 || !a.info)) || (a.in_tiled && (a.ld_in & 31)) || (a.out2_tiled && (a.ldo2 & 31)) ||
@@ -5127,6 +5288,13 @@ hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
                    dim3((unsigned)std::min<size_t>(cdiv(P, RotCfg<NN>::WPB), 16384 / RotCfg<NN>::WPB)), \
                    dim3(RotCfg<NN>::TB * RotCfg<NN>::WPB), 0, st, a);                              \
         break;
+    if (stats) {   // nbin 1024 (rotate_stats_supported)
+        const dim3 grid((unsigned)std::min<size_t>(cdiv(P, RotCfg<1024>::WPB), 16384 / RotCfg<1024>::WPB));
+        const dim3 block(RotCfg<1024>::TB * RotCfg<1024>::WPB);
+        if (a.delay2) IC_GGL((k_rotate<1024, true, true>), grid, block, 0, st, a);
+        else IC_GGL((k_rotate<1024, false, true>), grid, block, 0, st, a);
+        return hipGetLastError();
+    }
     switch (a.nbin) {
         IC_ROT(64) IC_ROT(128) IC_ROT(256) IC_ROT(512) IC_ROT(1024) IC_ROT(2048) IC_ROT(4096)
     default: return hipErrorInvalidValue;

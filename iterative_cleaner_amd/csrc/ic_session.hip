@@ -162,6 +162,10 @@ struct Session {
     int fork_round = -1;           // this iteration's fork round (-1: none)
     // the second fork (run_fit): the tail's list, marked in tmark, measured after the fit
     bool tail_split = false;
+    // FFT mode: the residual's rotation measures its rows itself (k_rotate's
+    // statistics epilogue, nbin 1024) instead of a k_diag STATS pass over R
+    // (IC_OPT_ROT_STATS)
+    bool rot_stats = true;
     int tail_split_mode = IC_TAIL_SPLIT_AUTO;   // IC_OPT_TAIL_SPLIT
     const int32_t *tail_list = nullptr;
     const unsigned long long *tail_cin = nullptr;
@@ -585,6 +589,23 @@ RotateArgs residual_rotate_args(Session *s, int pr_start, int pr_end)
     return a;
 }
 
+// the FFT mode's residual rotation also computes comprehensive_stats of its rows
+// (no R, no DIAG_STATS pass): when the option is on and the kernel serves nbin
+bool rot_stats_on(const Session *s)
+{
+    return s->fftded && s->rot_stats && rotate_stats_supported(s->p.nbin, s->p.data_f64 != 0);
+}
+void with_stats(Session *s, RotateArgs &a)
+{
+    a.out = nullptr;
+    a.w0 = s->w0;
+    a.tw_p2 = s->tw_p2;
+    a.std_o = s->std_;
+    a.mean_o = s->mean;
+    a.ptp_o = s->ptp;
+    a.fft_o = s->fft;
+}
+
 // fit-cube preparation (iterative_cleaner.py:96-100): baseline with w0, dedisperse.
 // The w0 baseline (window + per-profile levels) is also the template stage's
 // baseline of the first iteration (W == w0).  A shard also hands the validity
@@ -864,11 +885,14 @@ int fork_diag(Session *s, const DiagArgs &da, int r)
         RotateArgs ra = residual_rotate_args(s, s->pr_lo, s->pr_hi);
         ra.late = s->late;
         ra.late_sel = 0;
+        if (rot_stats_on(s)) with_stats(s, ra);
         LAUNCH_ON(s, K_ROTATE, s->dstream, launch_rotate(s->dstream, ra));
     }
-    DiagArgs a = da;
-    a.skip = s->late;
-    LAUNCH_ON(s, K_DIAG, s->dstream, launch_diag(s->dstream, a));
+    if (!rot_stats_on(s)) {
+        DiagArgs a = da;
+        a.skip = s->late;
+        LAUNCH_ON(s, K_DIAG, s->dstream, launch_diag(s->dstream, a));
+    }
     CK(hipEventRecord(s->join_ev, s->dstream));
     s->fork_round = r;
     return 0;
@@ -1033,7 +1057,8 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     if (s->fftded) {
         AL(s->dr, N);
         AL(s->Tc, N);
-        AL(s->R, N);
+        // R (the rotated residual rows) only when a run measures them in a
+        // separate pass (run_impl: !rot_stats_on)
         AL(s->zbase, P);
         AL(s->zshift, (size_t)nchan);
         AL(s->ph, (size_t)nchan * (nbin / 2 + 1));
@@ -1508,6 +1533,10 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
     if (s->events.size() > 4096)
         if (int rc = collect_timing(s)) return rc;
     if (s->fftded && !s->delays_set) return fail(IC_ESTATE, "ic_run before ic_set_delays (dedisp_mode FFT)");
+    if (s->fftded && !rot_stats_on(s) && !s->R && dalloc(&s->R, s->N) != hipSuccess) {
+        s->R = nullptr;
+        return fail(IC_ENOMEM, "hipMalloc(R: %zu floats) failed", s->N);
+    }
     // the second fork's tail marks are cleared at the end of each iteration; a
     // run that failed in between may have left some set
     if (s->tmark) CK(hipMemsetAsync(s->tmark, 0, s->P, s->stream));
@@ -1575,10 +1604,14 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
                 ra.late = s->late;
                 ra.late_sel = 1;
             }
+            if (rot_stats_on(s)) with_stats(s, ra);
             LAUNCH(s, K_ROTATE, launch_rotate(s->stream, ra));
             da = ds;
         }
-        if (s->tail_split) {
+        if (rot_stats_on(s)) {
+            // the rotation measured its rows (after a fork: pass A's on dstream)
+            if (s->fork_round >= 0) CK(hipStreamWaitEvent(s->stream, s->join_ev, 0));
+        } else if (s->tail_split) {
             // the tail's profiles (the rest of pass B ran beside the tail), then
             // join dstream and clear the marks for the next iteration
             DiagArgs b = da;
@@ -1885,6 +1918,10 @@ int ic_set_option(void *session, int option, int64_t v)
         if (v < 0 || v > 2) return fail(IC_EINVAL, "IC_OPT_TAIL_SPLIT=%lld (0, 1 or 2)", (long long)v);
         s->tail_split_mode = (int)v;
         return IC_OK;
+    case IC_OPT_ROT_STATS:
+        if (v != 0 && v != 1) return fail(IC_EINVAL, "IC_OPT_ROT_STATS=%lld (0 or 1)", (long long)v);
+        s->rot_stats = v != 0;
+        return IC_OK;
     default:
         return fail(IC_EINVAL, "unknown option %d", option);
     }
@@ -1906,6 +1943,7 @@ int ic_get_option(void *session, int option, int64_t *out)
     case IC_OPT_SYNC_TIMEOUT_MS: *out = (int64_t)(s->sync_timeout_s * 1000.0 + 0.5); return IC_OK;
     case IC_OPT_FIT_SCHEDULE: *out = IC_FIT_ROUNDS; return IC_OK;
     case IC_OPT_TAIL_SPLIT: *out = s->tail_split_mode; return IC_OK;
+    case IC_OPT_ROT_STATS: *out = s->rot_stats ? 1 : 0; return IC_OK;
     default: return fail(IC_EINVAL, "unknown option %d", option);
     }
 }

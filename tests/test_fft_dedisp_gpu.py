@@ -107,12 +107,15 @@ def test_fft_loop_matches_c_oracle(case, fit_tail, oracle_lib):
 
 
 SCHEDULES = [
-    # (diag_fork, template_incr, fit_tiled, fit_tail): the round-3 schedule on
-    # the FFT mode against its plain form
-    (0, 0, 0, None),
-    (1, 1, 1, 0),
-    (3, 1, 0, 512),
-    (5, 0, 1, None),
+    # (diag_fork, template_incr, fit_tiled, fit_tail, rot_stats): the round-3
+    # schedule on the FFT mode against its plain form, and (nbin 1024) the
+    # residual rotation that measures its rows against the rotation + STATS pass
+    (0, 0, 0, None, 1),
+    (1, 1, 1, 0, 1),
+    (3, 1, 0, 512, 0),
+    (5, 0, 1, None, 1),
+    (0, 1, 1, None, 0),
+    (3, 1, 1, None, 1),
 ]
 
 
@@ -150,8 +153,8 @@ def test_fft_schedules_are_bit_identical(case, oracle_lib):
                                 _pr(args, nbin), want_residual=True, want_details=True, delay=delay)
     assert base["loops"] == ref["loops"] and bits_equal(base["weights"], ref["weights"])
     assert bits_equal(base["amp"], ref["amp"]) and _same(base["R"], ref["residual"])
-    for fork, incr, tiled, tail in SCHEDULES:
-        got = run({"diag_fork": fork, "template_incr": incr, "fit_tiled": tiled}, tail)
+    for fork, incr, tiled, tail, rst in SCHEDULES:
+        got = run({"diag_fork": fork, "template_incr": incr, "fit_tiled": tiled, "rot_stats": rst}, tail)
         assert got["loops"] == base["loops"] and np.array_equal(got["changed"], base["changed"])
         for key in ("weights", "test", "T", "amp", "info"):
             assert bits_equal(got[key], base[key]), (fork, incr, tiled, key)
