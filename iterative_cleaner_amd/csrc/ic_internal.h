@@ -115,7 +115,10 @@ struct FitStateArrays {
     int32_t *iter, *nfev, *mode, *slow;
     // sweep outputs (k_fit_pass -> k_fit_state): the norms carry the flags in
     // their sign bits (fnorm: the A sweep took the exact path; acnorm: J(1) ==
-    // T in round 0), o_sum the dot of a B sweep (or round 0's fused one)
+    // T in round 0), o_sum the dot of a B sweep (or round 0's fused one).
+    // The two norms are stored as one double2 (fnorm, acnorm) per profile,
+    // ((double2 *)o_fnorm)[k], over the o_fnorm and o_acnorm arrays (adjacent,
+    // 2 x 8P bytes): one 16-B store per A sweep
     double *o_fnorm, *o_acnorm, *o_sum;
     float *p0;            // first sample of every profile's fit-cube row (round 0)
     const double *T64;    // the iteration's template (k_fit_state recomputes f0 / J0 from it)

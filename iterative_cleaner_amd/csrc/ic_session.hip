@@ -128,7 +128,6 @@ struct Session {
     int32_t *h_small = nullptr;   // pinned readback of the per-iteration counters and run stats
                                   // (a pageable D2H copy is staged synchronously, ~30 us each)
     int32_t *d_h_rcount = nullptr;  // its device address
-    hipEvent_t rev[2] = {nullptr, nullptr};
     void *fs_block = nullptr;   // one allocation backing fs
     int fit_rounds = 0;
     int plan_ub = 0;            // max(leaves, ops) of the pairwise plan (k_tnorm scratch)
@@ -264,11 +263,12 @@ static hipError_t take_event(Session *s, hipEvent_t *e)
 // up with hipErrorLaunchTimeOut and marks the session failed, so a kernel
 // that never finishes fails the run instead of hanging its caller, and no
 // later call reuses buffers its kernels may still be using.
+static const auto kBusyPoll = std::chrono::microseconds(200);
 static hipError_t poll_event(Session *s, hipEvent_t ev)
 {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    const auto spin = std::chrono::microseconds(200);
+    const auto spin = kBusyPoll;
     const auto limit = std::chrono::duration<double>(s->sync_timeout_s);
     hipError_t e;
     unsigned n = 0;
@@ -290,6 +290,35 @@ static hipError_t poll_event(Session *s, hipEvent_t ev)
         }
     }
     return e;
+}
+
+// Wait for a round's survivor count, which k_fit_state's last block publishes
+// into host-mapped memory (a system-scope release store): the same polling as
+// poll_event, on the value itself, so the round needs no event (a marker packet
+// between the state kernel and the next sweep costs ~7 us per round boundary)
+static hipError_t poll_count(Session *s, const int32_t *cnt)
+{
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const auto spin = kBusyPoll;
+    const auto limit = std::chrono::duration<double>(s->sync_timeout_s);
+    unsigned n = 0;
+    while (__atomic_load_n(cnt, __ATOMIC_ACQUIRE) < 0) {
+        const auto dt = clk::now() - t0;
+        if (dt > limit) {
+            s->failed = true;
+            return hipErrorLaunchTimeOut;
+        }
+        if (dt > spin) {
+            sched_yield();
+            if (s->comm && (++n & 255) == 0 && s->comm->remote_error()) {
+                s->failed = true;
+                s->comm_lost = true;
+                return hipErrorLaunchTimeOut;
+            }
+        }
+    }
+    return hipSuccess;
 }
 
 static hipError_t spin_sync(Session *s)
@@ -403,8 +432,6 @@ void free_all(Session *s)
     }
     if (s->h_rcount) (void)hipHostFree(s->h_rcount);
     if (s->h_small) (void)hipHostFree(s->h_small);
-    for (auto &e : s->rev)
-        if (e) (void)hipEventDestroy(e);
     if (s->sev) (void)hipEventDestroy(s->sev);
     for (auto &e : s->epool) (void)hipEventDestroy(e);
     s->epool.clear();
@@ -830,10 +857,9 @@ int run_fit(Session *s, const DiagArgs *fork)
         int32_t *next = fork_here ? bufs[2] : bufs[r & 1];
         LAUNCH(s, K_FIT_PASS, launch_fit_pass(s->stream, s->D, s->T64, P, nbin, s->ldD, s->dtiled, cur, cin, bound,
                                                 s->fs, r == 0));
-        s->h_rcount[r] = -1;
+        __atomic_store_n(s->h_rcount + r, -1, __ATOMIC_RELAXED);
         LAUNCH(s, K_FIT_STATE, launch_fit_state(s->stream, s->fs, P, cur, cin, bound, s->amp, s->info, next,
                                                 ctr + r, done + r, s->d_h_rcount + r, fork_here ? s->late : nullptr));
-        CK(hipEventRecord(s->rev[r & 1], s->stream));
         if (fork_here) flagged = r;
         // pass A is queued fork_delay rounds after the flags: the first late
         // rounds are the largest and run alone
@@ -846,7 +872,7 @@ int run_fit(Session *s, const DiagArgs *fork)
         cin = ctr + r;   // packed A / B counts of the next round's list
         if (r >= 1) {
             // count after round r-1 (= input of round r) bounds the count after round r
-            CK(poll_event(s, s->rev[(r - 1) & 1]));
+            CK(poll_count(s, s->h_rcount + (r - 1)));
             const long c = s->h_rcount[r - 1];
             if (c == 0) break;   // round r had nothing to do
             bound = c;
@@ -1169,9 +1195,6 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&s->d_h_rcount, s->h_rcount, 0) != hipSuccess)
         return bail(fail(IC_ENOMEM, "hipHostMalloc(round counts) failed"));
-    for (auto &e : s->rev)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-            return bail(fail(IC_EHIP, "hipEventCreate failed"));
     if (hipEventCreateWithFlags(&s->sev, hipEventDisableTiming) != hipSuccess)
         return bail(fail(IC_EHIP, "hipEventCreate failed"));
     if (hipHostMalloc((void **)&s->h_small, sizeof(int32_t) * ((size_t)p.max_iter + 20)) != hipSuccess)

@@ -16,11 +16,12 @@ def test_option_ranges_and_modes():
         defaults = {name: s.get_option(name) for name in _native.OPTIONS}
         assert defaults == {"fit_tail": 8192, "diag_fork": 3, "fork_delay": 1, "template_incr": 1,
                             "fit_tiled": 1, "rowstat_waves": 8, "rowstat_minlen": 1024, "diag_chain": 1,
-                            "sync_timeout_ms": 600000, "fit_schedule": 0, "tail_split": 2}
+                            "sync_timeout_ms": 600000, "fit_schedule": 0, "tail_split": 2, "rot_stats": 1}
         for name, bad in (("fit_tail", -1), ("diag_fork", 65), ("diag_fork", -1), ("fork_delay", 9),
                           ("template_incr", 2), ("fit_tiled", -1), ("rowstat_waves", 2),
                           ("rowstat_minlen", 0), ("diag_chain", 3), ("sync_timeout_ms", 0),
-                          ("fit_schedule", 1), ("fit_schedule", 2), ("tail_split", 3)):
+                          ("fit_schedule", 1), ("fit_schedule", 2), ("tail_split", 3), ("rot_stats", 2),
+                          ("rot_stats", -1)):
             with pytest.raises(_native.NativeError, match="IC_OPT"):
                 s.set_option(name, bad)
             assert s.get_option(name) == defaults[name]
@@ -41,7 +42,7 @@ def test_option_ranges_and_modes():
     with _native.GpuSession(4, 64, 256, device=0, delay=np.zeros(64)) as s:
         assert s.get_option("diag_fork") == 0 and s.get_option("template_incr") == 1
         assert s.get_option("fit_tiled") == 1
-        for name in ("template_incr", "fit_tiled", "diag_fork"):
+        for name in ("template_incr", "fit_tiled", "diag_fork", "rot_stats"):
             s.set_option(name, 0)
             s.set_option(name, 1)
     with _native.GpuSession(4, 64, 256, device=0, delay=np.zeros(64), fit_mode=_native.FIT_CLOSED) as s:
