@@ -304,8 +304,14 @@ hipError_t launch_combine(hipStream_t st, int nsub, int nchan, const uint8_t *va
 //   q = rint(y), z = y - q (exact, |z| <= 1/2), the angle is (pi/2)(q + z):
 //   sin and cos of (pi/2) z by their Taylor polynomials in z^2 (through z^17
 //   and z^16, Horner; truncation < 1e-17), then the quadrant q mod 4.
-// Within 2.3e-16 of the exact phasor (measured against x87 long double).
-__host__ __device__ inline double2 ic_phasor(int k, double d, int n)
+// ic_phasor0 is within 2.3e-16 of the exact phasor (measured against x87 long
+// double); ic_phasor, the definition, takes it directly for k < 64 and for
+// multiples of 64, and otherwise forms it as the product of its two parts,
+// P(k) = P0(k mod 64) P0(k - k mod 64), one complex multiply of separately
+// rounded operations ((a.x b.x - a.y b.y), (a.x b.y + a.y b.x)): a profile's
+// n/2 + 1 phasors then need 64 + n/128 polynomial evaluations instead of one
+// each (k_rotate's per-profile delays), within 7e-16 of the exact phasor.
+__host__ __device__ inline double2 ic_phasor0(int k, double d, int n)
 {
     const double c = d * 8193.0;
     const double dh = c - (c - d);
@@ -343,6 +349,16 @@ __host__ __device__ inline double2 ic_phasor(int k, double d, int n)
     case 2: return make_double2(-cp, -sn);
     default: return make_double2(sn, -cp);
     }
+}
+__host__ __device__ inline double2 ic_phasor_mul(double2 a, double2 b)
+{
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__host__ __device__ inline double2 ic_phasor(int k, double d, int n)
+{
+    const int lo = k & 63, hi = k - lo;
+    if (lo == 0 || hi == 0) return ic_phasor0(k, d, n);
+    return ic_phasor_mul(ic_phasor0(lo, d, n), ic_phasor0(hi, d, n));
 }
 
 // Fractional dedispersion (dedisp_mode IC_DEDISP_FFT; phase_rotation.py):

@@ -3922,11 +3922,42 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         if (skip(p, s)) continue;
         const __amdgpu_buffer_rsrc_t phr = rot_rsrc(PP ? a.tw : a.ph + (size_t)c * (M + 1), M + 1);
         const double dly = PP ? a.delay2[p] : 0.0;
+        // PP, N >= 256 (M a multiple of 64): the lane's harmonics k = t + u TB
+        // and M - k have the low parts lo1 = t mod 64 and lo2 = -t mod 64 in
+        // every round, and high parts that are the same across the wave: w0 + u
+        // TB for k, and M - 64 - w0 - u TB for M - k (M - w0 - u TB where lo1 =
+        // 0), w0 = t - lo1.  So a lane evaluates P0(lo1), P0(lo2) and one of
+        // the wave's 3 NK high parts (lane j), and every round reads its high
+        // parts from lanes u, NK + u, 2 NK + u (ic_phasor's product form: 3
+        // polynomials per lane instead of 2 NK)
+        constexpr bool PPX = PP && N >= 256;
+        const int lo1 = t & 63, w0 = t - lo1;
+        double2 A1{}, A2{}, Bh{};
+        if constexpr (PPX) {
+            const int lo2 = (64 - lo1) & 63, j = lo1;
+            int hv = j < NK ? w0 + j * TB : (j < 2 * NK ? M - 64 - w0 - (j - NK) * TB : M - w0 - (j - 2 * NK) * TB);
+            if (j >= 3 * NK || hv < 0) hv = 0;
+            A1 = ic_phasor0(lo1, dly, N);
+            A2 = ic_phasor0(lo2, dly, N);
+            Bh = ic_phasor0(hv, dly, N);
+        }
+        auto bcast = [&](int lane) {
+            return make_double2(__hiloint2double(__builtin_amdgcn_readlane(__double2hiint(Bh.x), lane),
+                                                 __builtin_amdgcn_readlane(__double2loint(Bh.x), lane)),
+                                __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(Bh.y), lane),
+                                                 __builtin_amdgcn_readlane(__double2loint(Bh.y), lane)));
+        };
         // the post step's phasors one round ahead: the first round's are
         // requested with the rows, each later round's before the round before it
         auto ldph = [&](int u, double2 (&pp)[2]) {
             const int k = t + u * TB;
-            if (k <= H) {
+            if constexpr (PPX) {
+                const double2 b1 = bcast(u), b2 = bcast(NK + u), b3 = bcast(2 * NK + u);
+                if (k <= H) {
+                    pp[0] = lo1 == 0 ? b1 : (w0 + u * TB == 0 ? A1 : ic_phasor_mul(A1, b1));
+                    pp[1] = lo1 == 0 ? b3 : (M - 64 - w0 - u * TB == 0 ? A2 : ic_phasor_mul(A2, b2));
+                }
+            } else if (k <= H) {
                 if constexpr (PP) {
                     pp[0] = ic_phasor(k, dly, N);
                     pp[1] = ic_phasor(M - k, dly, N);

@@ -86,8 +86,12 @@ def phasors(nbin: int, delays) -> np.ndarray:
     * w = z*z; sin = z * (S0 + w (S1 + ... w S8)); cos = C0 + w (C1 + ... w C8)
     * quadrant q mod 4: (cos, sin), (-sin, cos), (-cos, -sin), (sin, -cos).
 
-    Within 2.3e-16 of the exact phasor (tests/test_phase_rotation.py checks it
-    against x87 long double)."""
+    That is P0(k); the phasor itself (the GPU's ic_phasor) is P0(k) for k < 64
+    and for multiples of 64, else the product P0(k mod 64) * P0(k - k mod 64)
+    with separately rounded operations (re = a.re b.re - a.im b.im, im = a.re
+    b.im + a.im b.re), so that a profile's phasors take 64 + nbin/128
+    polynomial evaluations.  Within 7e-16 of the exact phasor
+    (tests/test_phase_rotation.py checks it against x87 long double)."""
     m = nbin // 2
     k = np.arange(m + 1, dtype=np.float64)
     s = np.asarray(delays, dtype=np.float64)[..., None]
@@ -111,6 +115,17 @@ def phasors(nbin: int, delays) -> np.ndarray:
     qi = q.astype(np.int64) & 3
     re = np.where(qi == 0, cp, np.where(qi == 1, -sn, np.where(qi == 2, -cp, sn)))
     im = np.where(qi == 0, sn, np.where(qi == 1, cp, np.where(qi == 2, -sn, -cp)))
+    # the product form: P(k) = P0(k mod 64) P0(k - k mod 64) where both parts are nonzero
+    ki = np.arange(m + 1)
+    lo, hi = ki & 63, ki - (ki & 63)
+    sel = (lo != 0) & (hi != 0)
+    if sel.any():
+        ar, ai = re[..., lo[sel]], im[..., lo[sel]]
+        br, bi = re[..., hi[sel]], im[..., hi[sel]]
+        re = re.copy()
+        im = im.copy()
+        re[..., sel] = ar * br - ai * bi
+        im[..., sel] = ar * bi + ai * br
     return np.stack([re, im])
 
 

@@ -529,7 +529,7 @@ static const double PH_S[9] = {0x1.921fb54442d18p+0,  -0x1.4abbce625be53p-1, 0x1
 static const double PH_C[9] = {1.0,                   -0x1.3bd3cc9be45dep+0, 0x1.03c1f081b5ac4p-2,
                                -0x1.55d3c7e3cbffap-6, 0x1.e1f506891babbp-11, -0x1.a6d1f2a204a8cp-16,
                                0x1.f9d38a3763cc3p-22, -0x1.b6e24f44b128fp-28, 0x1.20c62c2f2d7f5p-34};
-static void orc_phasor(int k, double d, int n, double *o)
+static void orc_phasor0(int k, double d, int n, double *o)
 {
     const double c = d * 8193.0;
     const double dh = c - (c - d), dl = d - dh;
@@ -551,6 +551,25 @@ static void orc_phasor(int k, double d, int n, double *o)
     case 2: o[0] = -cp; o[1] = -sn; break;
     default: o[0] = sn; o[1] = -cp; break;
     }
+}
+
+/* The phasor of harmonic k (ic_phasor): orc_phasor0 for k < 64 and multiples
+ * of 64, else the product P0(k mod 64) P0(k - k mod 64) of separately rounded
+ * operations (re = a.re b.re - a.im b.im, im = a.re b.im + a.im b.re). */
+static void orc_phasor(int k, double d, int n, double *o)
+{
+    const int lo = k & 63, hi = k - lo;
+    if (lo == 0 || hi == 0) {
+        orc_phasor0(k, d, n, o);
+        return;
+    }
+    double a[2], b[2];
+    orc_phasor0(lo, d, n, a);
+    orc_phasor0(hi, d, n, b);
+    const double re1 = a[0] * b[0], re2 = a[1] * b[1];
+    const double im1 = a[0] * b[1], im2 = a[1] * b[0];
+    o[0] = re1 - re2;
+    o[1] = im1 + im2;
 }
 
 /* ph[(c*(n/2+1) + k)*2 + {0,1}] = orc_phasor(k, delay[c], n) */

@@ -104,3 +104,20 @@ def test_archive_fft_dedisperse_roundtrip_and_io(tmp_path):
     want = dedispersion.delays_from_dm(30.0, fr._chan_freqs, 1400.0, [0.05] * 3, 64)[0]
     assert np.array_equal(fa.get_dm_delay(), want)
     assert np.array_equal(fa.get_dm_shift(), np.zeros(12, np.int64))
+
+
+@pytest.mark.parametrize("n", [64, 256, 1024, 4096])
+def test_phasors_within_7e16_of_exact(n):
+    """The product form P0(k mod 64) P0(k - k mod 64) (ic_phasor) against the
+    phasor exp(2 pi i k d / n) evaluated in x87 long double."""
+    from iterative_cleaner_amd import phase_rotation as pr
+    rng = np.random.default_rng(n)
+    d = np.concatenate([rng.uniform(-3 * n, 3 * n, 40), [0.0, 0.5, -1.25, 7.0, n * 0.37]])
+    ph = pr.phasors(n, d)
+    # k d is exact in the 64-bit long double mantissa (k <= 2^11), so is its
+    # remainder mod n; then the angle 2 pi r / n with pi to long double precision
+    k = np.arange(n // 2 + 1, dtype=np.longdouble)
+    r = np.fmod(k[None, :] * d.astype(np.longdouble)[:, None], np.longdouble(n))
+    ang = 2 * np.longdouble("3.141592653589793238462643383279502884") * r / np.longdouble(n)
+    err = np.maximum(np.abs(ph[0] - np.cos(ang)), np.abs(ph[1] - np.sin(ang)))
+    assert float(err.max()) < 7e-16
