@@ -10,7 +10,7 @@
 set -o pipefail
 TAG=${1:?tag}; WL=${2:?workload}; FM=${3:-exact}; DD=${4:-shift}; shift 4
 RND=${IC_ROUND:-r05}
-lc=$(echo $WL | tr A-Z a-z); [ "$FM" = closed ] && lc=${lc}c; [ "$DD" = fft ] && lc=${lc}fft
+lc=$(echo $WL | tr A-Z a-z); [ "$FM" = closed ] && lc=${lc}c; [ "$DD" != shift ] && lc=${lc}${DD/_/}
 OUT=gpurun_out/evidence_$TAG
 mkdir -p $OUT
 tools/profile_c2.sh ${TAG}_$lc $WL $FM $DD || exit 1

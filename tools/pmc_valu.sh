@@ -9,7 +9,7 @@ TAG=${1:?tag}
 WL=${2:-C2}
 FM=${3:-exact}            # bench.py --fit-mode (closed: summaries keyed WL/closed)
 DD=${4:-shift}            # bench.py --dedisp (fft: summaries keyed .../fft)
-KEY=$WL; [ "$FM" = closed ] && KEY=$WL/closed; [ "$DD" = fft ] && KEY=$KEY/fft
+KEY=$WL; [ "$FM" = closed ] && KEY=$WL/closed; [ "$DD" != shift ] && KEY=$KEY/$DD
 OUT=gpurun_out/valu_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
