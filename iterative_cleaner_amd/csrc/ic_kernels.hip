@@ -3567,35 +3567,84 @@ __device__ __forceinline__ double2 rot_ld(__amdgpu_buffer_rsrc_t r, unsigned vof
     return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-// Twiddle sources: the table in global memory (through L1/L2) or staged in LDS.
-// TW(voff, soff) = tw entry at byte offset voff + soff.
-// pass(k, kl): twiddle of global stage s = LGS + l for butterfly k + kl 2^LGS,
-// tw[(k + kl 2^LGS) N / 2^(s+1)];  post(i): tw[i].
+// Twiddle sources: k_diag_p2's table (p2_twiddles: M plain entries tw[i] =
+// exp(-2 pi i i / N), then for every Stockham stage after the first, of radix
+// R and span ns, the entries w^(q k), w = exp(-2 pi i / (R ns)), as [k][q - 1]
+// at M + ns - 8: the spans are 8, 64, 512, so the earlier tables fill ns - 8
+// slots), in global memory (through L1/L2) or staged in LDS.  Its entries are
+// the plain table's tw[q k N / (R ns)], the same long-double values.
 template <int N>
 struct TwGlobal {
     __amdgpu_buffer_rsrc_t r;
-    template <int LGS>
-    __device__ __forceinline__ double2 pass(unsigned k, unsigned kl, int l) const
+    template <int NS, int R>
+    __device__ __forceinline__ double2 stage(unsigned k, int q) const
     {
-        constexpr unsigned S0 = 16u * (N >> (LGS + 1));
-        return rot_ld(r, (k * S0) >> l, (kl << LGS) * (S0 >> l));
+        return rot_ld(r, 16u * (unsigned)(k * (R - 1)), 16u * (unsigned)(N / 2 + NS - 8 + q - 1));
     }
     __device__ __forceinline__ double2 post(unsigned i) const { return rot_ld(r, 16u * i, 0); }
 };
-// LDS: stage s's 2^s twiddles contiguous at 2^s - 1 (a stage's lanes read
-// consecutive slots: no bank conflicts, where the strided plain table was up to
-// 8-way), and the plain table for the post step
 template <int N>
 struct TwLds {
-    const double2 *stage, *plain;
-    template <int LGS>
-    __device__ __forceinline__ double2 pass(unsigned k, unsigned kl, int l) const
+    const double2 *t;
+    template <int NS, int R>
+    __device__ __forceinline__ double2 stage(unsigned k, int q) const
     {
-        return stage[(1u << (LGS + l)) - 1u + k + (kl << LGS)];
+        return t[N / 2 + NS - 8 + q - 1 + k * (R - 1)];
     }
-    __device__ __forceinline__ double2 post(unsigned i) const { return plain[i]; }
+    __device__ __forceinline__ double2 post(unsigned i) const { return t[i]; }
 };
 
+// the rotation's complex product: (a.r w.r - a.i w.i, a.r w.i + a.i w.r)
+__device__ __forceinline__ double2 rot_cmul(double2 a, double2 w)
+{
+    return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+// DFT of 4 / 8 points in place, natural output order, in the written order of
+// phase_rotation.py (_dft4, _dft8) and the oracle (dft4, dft8)
+__device__ __forceinline__ void rot_dft4(double2 *b)
+{
+    const double2 c0 = make_double2(b[0].x + b[2].x, b[0].y + b[2].y);
+    const double2 c1 = make_double2(b[0].x - b[2].x, b[0].y - b[2].y);
+    const double2 c2 = make_double2(b[1].x + b[3].x, b[1].y + b[3].y);
+    const double dr = b[1].x - b[3].x, di = b[1].y - b[3].y;
+    const double2 c3 = make_double2(di, -dr);
+    b[0] = make_double2(c0.x + c2.x, c0.y + c2.y);
+    b[1] = make_double2(c1.x + c3.x, c1.y + c3.y);
+    b[2] = make_double2(c0.x - c2.x, c0.y - c2.y);
+    b[3] = make_double2(c1.x - c3.x, c1.y - c3.y);
+}
+__device__ __forceinline__ void rot_dft8(double2 *b)
+{
+    constexpr double s = 0x1.6a09e667f3bcdp-1;   // f64(sqrt(2)/2)
+    double2 c[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        c[q] = make_double2(b[q].x + b[q + 4].x, b[q].y + b[q + 4].y);
+        c[q + 4] = make_double2(b[q].x - b[q + 4].x, b[q].y - b[q + 4].y);
+    }
+    {
+        const double t1 = c[5].x + c[5].y, t2 = c[5].y - c[5].x;
+        c[5] = make_double2(t1 * s, t2 * s);
+    }
+    c[6] = make_double2(c[6].y, -c[6].x);
+    {
+        const double t1 = c[7].y - c[7].x, t2 = c[7].x + c[7].y;
+        c[7] = make_double2(t1 * s, -(t2 * s));
+    }
+    rot_dft4(c);
+    rot_dft4(c + 4);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        b[2 * p] = c[p];
+        b[2 * p + 1] = c[p + 4];
+    }
+}
+
+// One Stockham stage of radix Q = 2^R and span ns = 2^LGS (phase_rotation.py
+// _stockham): group ja < G = M/Q holds the points v[ja + q G]; from the second
+// stage on they are multiplied by the stage's twiddles w^(q k), k = ja mod ns,
+// then transformed by DFT_Q, and y_p lands at v[(ja - k) Q + k + p ns].  One LDS
+// round trip per stage (8 points per lane at N = 1024, three stages per FFT).
 // IN_REG: the pass's input is z (one group per thread, G == TB) instead of
 // LDS; OUT_REG: its output stays in z.  The last pass's group ja holds points
 // ja + q G, the distribution the first pass reads, so a profile can enter and
@@ -3604,25 +3653,22 @@ template <int N, int R, int LGS, bool IN_REG = false, bool OUT_REG = false, type
 __device__ __forceinline__ void rot_pass(double2 *v, const TW &tw, int t, double2 *z = nullptr)
 {
     using C = RotCfg<N>;
-    constexpr int M = C::M, TB = C::TB, G = M >> R, Q = 1 << R, HALF = Q / 2;
+    constexpr int M = C::M, TB = C::TB, G = M >> R, Q = 1 << R;
     constexpr int GPT = (G + TB - 1) / TB;
     constexpr int ns = 1 << LGS;
     static_assert(!(IN_REG || OUT_REG) || G == TB, "register passes hold one group per thread");
+    static_assert(ns == 1 || ns >= 8, "stage spans are 1, 8, 64, 512");
     double2 u[GPT][Q];
-    // the pass's twiddles first (global/L1 latency overlaps the LDS reads and
-    // the barrier): local stage l uses 2^l distinct ones, w[2^l - 1 + kl]
+    // the stage's twiddles first (their latency overlaps the LDS reads and the barrier)
     double2 w[GPT][Q - 1];
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
         const int ja = t + TB * gi;
         const int k = ja & (ns - 1);
         if (G % TB == 0 || ja < G) {
+            if constexpr (ns > 1) {
 #pragma unroll
-            for (int l = 0; l < R; ++l) {
-                // tw[(kl ns + k) S], S = N / 2^(l + LGS + 1)
-#pragma unroll
-                for (int kl = 0; kl < (1 << l); ++kl)
-                    w[gi][(1 << l) - 1 + kl] = tw.template pass<LGS>((unsigned)k, (unsigned)kl, l);
+                for (int q = 1; q < Q; ++q) w[gi][q - 1] = tw.template stage<ns, Q>((unsigned)k, q);
             }
             if constexpr (IN_REG) {
 #pragma unroll
@@ -3643,23 +3689,18 @@ __device__ __forceinline__ void rot_pass(double2 *v, const TW &tw, int t, double
         const int ja = t + TB * gi;
         if (G % TB == 0 || ja < G) {
             const int k = ja & (ns - 1);
+            if constexpr (ns > 1) {
 #pragma unroll
-            for (int l = 0; l < R; ++l) {
-                const int nsl = 1 << l;
-                double2 w2[Q];
-#pragma unroll
-                for (int jl = 0; jl < HALF; ++jl) {
-                    const int kl = jl & (nsl - 1);
-                    const double2 ww = w[gi][nsl - 1 + kl];
-                    const double2 a = u[gi][jl], b = u[gi][jl + HALF];
-                    const double tr = ww.x * b.x - ww.y * b.y;
-                    const double ti = ww.x * b.y + ww.y * b.x;
-                    const int o = 2 * jl - kl;
-                    w2[o] = make_double2(a.x + tr, a.y + ti);
-                    w2[o + nsl] = make_double2(a.x - tr, a.y - ti);
-                }
-#pragma unroll
-                for (int q = 0; q < Q; ++q) u[gi][q] = w2[q];
+                for (int q = 1; q < Q; ++q) u[gi][q] = rot_cmul(u[gi][q], w[gi][q - 1]);
+            }
+            if constexpr (Q == 8) {
+                rot_dft8(u[gi]);
+            } else if constexpr (Q == 4) {
+                rot_dft4(u[gi]);
+            } else {
+                const double2 a = u[gi][0], b = u[gi][1];
+                u[gi][0] = make_double2(a.x + b.x, a.y + b.y);
+                u[gi][1] = make_double2(a.x - b.x, a.y - b.y);
             }
             const int base = ((ja >> LGS) << (LGS + R)) + k;
             if constexpr (OUT_REG) {
@@ -3721,9 +3762,8 @@ __device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
 // - fftmax: k_diag_cl's first radix-8 stage reads the points t + 64 r of d =
 //   f64(X) - mean, which is exactly the direct layout this lane holds, so the
 //   rFFT starts from registers; the later stages are p2_fft's with its table
-//   (tw_p2: through L1, the LDS holds only the rotation's tables), the
-//   spectrum's post twiddles tw[k < M] come from the rotation's plain LDS table
-//   (the same long double values: exp(-2 pi i q / N) built by one formula).
+//   (tw_p2, which k_rotate stages in LDS for its own stages), the spectrum's
+//   post twiddles tw[k < M] from the same table's plain part.
 template <int N, typename TW>
 __device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2 *v, const TW &tw, int t,
                                           double2 (&z)[8], double inv, float w)
@@ -3802,7 +3842,7 @@ __device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2
             for (int r8 = 0; r8 < 8; ++r8) Cb[A ^ r8] = c8[r8];
         }
         wave_sync();
-        p2_fft<M, L, CLay<N>::LG, 3, 8, M, float, false>(Cb, (const float *)nullptr, 0.0, a.tw_p2, t);
+        p2_fft<M, L, CLay<N>::LG, 3, 8, M, float, false>(Cb, (const float *)nullptr, 0.0, tw.t, t);
         // the spectrum in conjugate bin pairs (k_diag_cl's post, 2 X_k)
         constexpr int JF = H / L;
         double best2 = 0.0;
@@ -3882,19 +3922,15 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
     const size_t P = (size_t)nsub * nchan;
     const double sg = a.sign > 0 ? 1.0 : -1.0;
     const double inv = 1.0 / (double)M;
-    const __amdgpu_buffer_rsrc_t twr = rot_rsrc(a.tw, N);
+    constexpr int TWE = p2_tw_entries(N);   // k_diag_p2's table: M plain + the stage tables
+    static_assert(TWE <= 2 * M, "the staged table fits tws");
+    const __amdgpu_buffer_rsrc_t twr = rot_rsrc(a.tw_p2, TWE);
     const auto tw = [&]() {
-        if constexpr (C::TW_LDS) return TwLds<N>{tws + M, tws};
+        if constexpr (C::TW_LDS) return TwLds<N>{tws};
         else return TwGlobal<N>{twr};
     }();
     if constexpr (C::TW_LDS) {
-        for (int i = threadIdx.x; i < M; i += TB * WPB) {
-            tws[i] = a.tw[i];
-            // compact slot i: stage s = floor(log2(i + 1)), j = i + 1 - 2^s
-            // (slot M - 1 is unused: s = LG)
-            const int s = 31 - __clz(i + 1), j = i + 1 - (1 << s);
-            tws[M + i] = a.tw[(size_t)j * (N >> (s + 1))];
-        }
+        for (int i = threadIdx.x; i < TWE; i += TB * WPB) tws[i] = a.tw_p2[i];
         __syncthreads();
     }
     // every global load of a profile in flight at once: one memory latency
@@ -5296,10 +5332,10 @@ hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
     const size_t P = (size_t)a.nsub * a.nchan;
     if (P == 0) return hipSuccess;
     const bool stats = a.std_o != nullptr;
-    if (stats && (!rotate_stats_supported(a.nbin, false) || !a.amp || a.sign > 0 || a.out2 || !a.w0 || !a.tw_p2 || !a.mean_o ||
+    if (stats && (!rotate_stats_supported(a.nbin, false) || !a.amp || a.sign > 0 || a.out2 || !a.w0 || !a.mean_o ||
                   !a.ptp_o || !a.fft_o))
         return hipErrorInvalidValue;
-    if (!rotate_supported(a.nbin) || !a.in || (!a.out && !stats) || !a.tw || a.ld_in < a.nbin ||
+    if (!rotate_supported(a.nbin) || !a.in || (!a.out && !stats) || !a.tw || !a.tw_p2 || a.ld_in < a.nbin ||
         (!stats && a.ldo < a.nbin) ||
         (!a.ph && !a.delay2 && !a.identity) ||
         (a.ld_in & 3) || (a.ldo & 3) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 3))) ||

@@ -590,6 +590,7 @@ RotateArgs rotate_args(Session *s, const float *in, const float *base, int sign,
     a.identity = sign > 0 && s->p.input_dedispersed;
     a.sign = sign;
     a.tw = s->tw;
+    a.tw_p2 = s->tw_p2;
     a.flags = flags;
     a.nsub = s->p.nsub;
     a.nchan = s->nchan;
@@ -1817,8 +1818,9 @@ int rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, 
         const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)q / (long double)nbin;
         tw[q] = make_double2((double)cosl(ang), (double)sinl(ang));
     }
+    const std::vector<double2> tw2 = p2_twiddles(nbin);   // the rotation's stage tables
     float *d = nullptr;
-    double2 *dph = nullptr, *dtw = nullptr;
+    double2 *dph = nullptr, *dtw = nullptr, *dtw2 = nullptr;
     double *ddl = nullptr;
     hipStream_t st = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
@@ -1831,6 +1833,8 @@ int rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, 
     if (e == hipSuccess) e = hipMemcpyAsync(d, in, sizeof(float) * N, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(dph, ph.data(), sizeof(double2) * ph.size(), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(dtw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMalloc((void **)&dtw2, sizeof(double2) * tw2.size());
+    if (e == hipSuccess) e = hipMemcpyAsync(dtw2, tw2.data(), sizeof(double2) * tw2.size(), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         RotateArgs a{};
         a.in = d;
@@ -1839,6 +1843,7 @@ int rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, 
         a.delay2 = ddl;
         a.sign = sign;
         a.tw = dtw;
+        a.tw_p2 = dtw2;
         a.nsub = nsub;
         a.nchan = nchan;
         a.nbin = nbin;
@@ -1851,6 +1856,7 @@ int rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, 
     if (d) (void)hipFree(d);
     if (dph) (void)hipFree(dph);
     if (dtw) (void)hipFree(dtw);
+    if (dtw2) (void)hipFree(dtw2);
     if (ddl) (void)hipFree(ddl);
     if (st) (void)hipStreamDestroy(st);
     if (e != hipSuccess) return fail(IC_EHIP, "ic_rotate_profiles: %s", hipGetErrorString(e));

@@ -580,25 +580,86 @@ void orc_phasors(int n, int nchan, const double *delay, double *ph)
         for (int k = 0; k <= m; ++k) orc_phasor(k, delay[c], n, ph + ((size_t)c * (m + 1) + k) * 2);
 }
 
-/* radix-2 Stockham FFT of m complex points (re/im interleaved) through `tmp` */
+/* FFT of m complex points (re/im interleaved) through `tmp`: Stockham stages of
+ * radix 8 while three or more of the log2 m levels remain, then one of radix 4
+ * or 2 (phase_rotation.py _stockham, the GPU's rot_pass).  Stage (R, ns),
+ * butterfly j < m/R: k = j mod ns, a_q = v[j + q m/R]; for ns > 1, b_q = a_q
+ * times tw[q k n/(R ns)] (q >= 1); y = DFT_R(b) in the written order below;
+ * out[(j - k) R + k + p ns] = y_p. */
+#define ROT_S8 0x1.6a09e667f3bcdp-1   /* f64(sqrt(2)/2) = Re exp(-i pi/4) */
+static void dft4(double *r, double *i)   /* in place, 4 points */
+{
+    const double c0r = r[0] + r[2], c0i = i[0] + i[2];
+    const double c1r = r[0] - r[2], c1i = i[0] - i[2];
+    const double c2r = r[1] + r[3], c2i = i[1] + i[3];
+    const double dr = r[1] - r[3], di = i[1] - i[3];
+    const double c3r = di, c3i = -dr;
+    r[0] = c0r + c2r; i[0] = c0i + c2i;
+    r[1] = c1r + c3r; i[1] = c1i + c3i;
+    r[2] = c0r - c2r; i[2] = c0i - c2i;
+    r[3] = c1r - c3r; i[3] = c1i - c3i;
+}
+static void dft8(double *r, double *i)   /* in place, 8 points, natural output order */
+{
+    double cr[8], ci[8];
+    for (int q = 0; q < 4; ++q) {
+        cr[q] = r[q] + r[q + 4]; ci[q] = i[q] + i[q + 4];
+        cr[q + 4] = r[q] - r[q + 4]; ci[q + 4] = i[q] - i[q + 4];
+    }
+    double t1 = cr[5] + ci[5], t2 = ci[5] - cr[5];
+    cr[5] = t1 * ROT_S8; ci[5] = t2 * ROT_S8;
+    t1 = ci[6]; ci[6] = -cr[6]; cr[6] = t1;
+    t1 = ci[7] - cr[7]; t2 = cr[7] + ci[7];
+    cr[7] = t1 * ROT_S8; ci[7] = -(t2 * ROT_S8);
+    dft4(cr, ci);
+    dft4(cr + 4, ci + 4);
+    for (int p = 0; p < 4; ++p) {
+        r[2 * p] = cr[p]; i[2 * p] = ci[p];
+        r[2 * p + 1] = cr[p + 4]; i[2 * p + 1] = ci[p + 4];
+    }
+}
 static void stockham(int m, double *v, double *tmp, const double *tw)
 {
-    const int n = 2 * m, h = m / 2;
-    for (int ns = 1; ns < m; ns <<= 1) {
-        for (int j = 0; j < h; ++j) {
+    const int n = 2 * m;
+    int lg = 0;
+    while ((1 << lg) < m) ++lg;
+    for (int ns = 1, done = 0; done < lg;) {
+        const int rem = lg - done, R = rem >= 3 ? 8 : (rem == 2 ? 4 : 2);
+        const int g = m / R;
+        for (int j = 0; j < g; ++j) {
             const int k = j & (ns - 1);
-            const double *w = tw + 2 * (size_t)(k * (n / (2 * ns)));
-            const double ar = v[2 * j], ai = v[2 * j + 1];
-            const double br = v[2 * (j + h)], bi = v[2 * (j + h) + 1];
-            const double tr = w[0] * br - w[1] * bi;
-            const double ti = w[0] * bi + w[1] * br;
-            const int o = 2 * j - k;
-            tmp[2 * o] = ar + tr;
-            tmp[2 * o + 1] = ai + ti;
-            tmp[2 * (o + ns)] = ar - tr;
-            tmp[2 * (o + ns) + 1] = ai - ti;
+            double br[8], bi[8];
+            for (int q = 0; q < R; ++q) {
+                const double ar = v[2 * (j + q * g)], ai = v[2 * (j + q * g) + 1];
+                if (ns > 1 && q > 0) {
+                    const double *w = tw + 2 * (size_t)(q * k * (n / (R * ns)));
+                    const double p1 = ar * w[0], p2 = ai * w[1];
+                    const double p3 = ar * w[1], p4 = ai * w[0];
+                    br[q] = p1 - p2;
+                    bi[q] = p3 + p4;
+                } else {
+                    br[q] = ar;
+                    bi[q] = ai;
+                }
+            }
+            if (R == 8) {
+                dft8(br, bi);
+            } else if (R == 4) {
+                dft4(br, bi);
+            } else {
+                const double y0r = br[0] + br[1], y0i = bi[0] + bi[1];
+                const double y1r = br[0] - br[1], y1i = bi[0] - bi[1];
+                br[0] = y0r; bi[0] = y0i; br[1] = y1r; bi[1] = y1i;
+            }
+            const int o = (j - k) * R + k;
+            for (int p = 0; p < R; ++p) {
+                tmp[2 * (o + p * ns)] = br[p];
+                tmp[2 * (o + p * ns) + 1] = bi[p];
+            }
         }
         memcpy(v, tmp, sizeof(double) * 2 * (size_t)m);
+        ns *= R;
+        done += R == 8 ? 3 : (R == 4 ? 2 : 1);
     }
 }
 
