@@ -3734,22 +3734,27 @@ __device__ __forceinline__ void rot_fft(double2 *v, const TW &tw, int t, double2
     }
 }
 
-// real spectrum bin from the half-length transform: za = Z_a, zb = Z_{M-a}, w = W^a
-__device__ __forceinline__ double2 rot_post(double2 za, double2 zb, double2 w)
+// X_k, X_q (q = M - k) of the real spectrum from Z_k, Z_q: the even and odd
+// parts are shared (E_q = conj E_k, O_q = conj O_k), X = E + w O
+// (phase_rotation.py _post_pair, oracle rot_post_pair)
+__device__ __forceinline__ void rot_post_pair(double2 zk, double2 zq, double2 wk, double2 wq, double2 &xk,
+                                              double2 &xq)
 {
-    const double er = (za.x + zb.x) * 0.5, ei = (za.y - zb.y) * 0.5;
-    const double dr = za.x - zb.x, di = za.y + zb.y;
-    const double orr = di * 0.5, oi = -(dr * 0.5);
-    return make_double2(er + (w.x * orr - w.y * oi), ei + (w.x * oi + w.y * orr));
+    const double er = (zk.x + zq.x) * 0.5, ei = (zk.y - zq.y) * 0.5;
+    const double orr = (zk.y + zq.y) * 0.5, oi = -((zk.x - zq.x) * 0.5);
+    xk = make_double2(er + (wk.x * orr - wk.y * oi), ei + (wk.x * oi + wk.y * orr));
+    xq = make_double2(er + (wq.x * orr + wq.y * oi), (wq.y * orr - wq.x * oi) - ei);
 }
-
-// half-length input of the inverse from ya = Y_a, yb = Y_{M-a}, w = W^a
-__device__ __forceinline__ double2 rot_pre(double2 ya, double2 yb, double2 w)
+// the inverse's half-length inputs Z'_k, Z'_q from Y_k, Y_q (_pre_pair)
+__device__ __forceinline__ void rot_pre_pair(double2 yk, double2 yq, double2 wk, double2 wq, double2 &zk,
+                                             double2 &zq)
 {
-    const double er = (ya.x + yb.x) * 0.5, ei = (ya.y - yb.y) * 0.5;
-    const double hr = (ya.x - yb.x) * 0.5, hi = (ya.y + yb.y) * 0.5;
-    const double orr = hr * w.x + hi * w.y, oi = hi * w.x - hr * w.y;
-    return make_double2(er - oi, ei + orr);
+    const double er = (yk.x + yq.x) * 0.5, ei = (yk.y - yq.y) * 0.5;
+    const double hr = (yk.x - yq.x) * 0.5, hi = (yk.y + yq.y) * 0.5;
+    const double okr = hr * wk.x + hi * wk.y, oki = hi * wk.x - hr * wk.y;
+    const double oqr = hi * wq.y - hr * wq.x, oqi = hi * wq.x + hr * wq.y;
+    zk = make_double2(er - oki, ei + okr);
+    zq = make_double2(er - oqi, oqr - ei);
 }
 
 // comprehensive_stats (ic.py:206-212) of the rotated residual row held by one
@@ -4124,11 +4129,12 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
                 } else {
                     const int q = M - k;
                     const double2 zk = v[rsw(k)], zq = v[rsw(q)];
-                    const double2 Xk = rot_post(zk, zq, wk), Xq = rot_post(zq, zk, wq);
+                    double2 Xk, Xq, Zk, Zq;
+                    rot_post_pair(zk, zq, wk, wq, Xk, Xq);
                     const double pki = sg * pk.y, pqi = sg * pq.y;
                     const double2 Yk = make_double2(Xk.x * pk.x - Xk.y * pki, Xk.x * pki + Xk.y * pk.x);
                     const double2 Yq = make_double2(Xq.x * pq.x - Xq.y * pqi, Xq.x * pqi + Xq.y * pq.x);
-                    const double2 Zk = rot_pre(Yk, Yq, wk), Zq = rot_pre(Yq, Yk, wq);
+                    rot_pre_pair(Yk, Yq, wk, wq, Zk, Zq);
                     v[rsw(q)] = make_double2(Zq.x, -Zq.y);
                     v[rsw(k)] = make_double2(Zk.x, -Zk.y);
                 }

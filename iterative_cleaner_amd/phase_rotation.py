@@ -33,10 +33,11 @@ of s bins (``y[j] = x[j + s]`` for integer s; ``dedisperse`` rotates by +s,
    even outputs y_(2p) = DFT_4(c0..c3)_p, the odd y_(2p+1) = DFT_4(c4..c7)_p.
    (Round 6; rounds 2-5 ran radix-2 stages, 10 operations per butterfly
    against 98 per radix-8 butterfly of 8 points, 56 in the first stage.)
-3. For k = 1 .. M/2, q = M - k: the real spectrum X_k and X_q
-   (post(Z_k, Z_q, tw[k]) and post(Z_q, Z_k, tw[q])), the phasors
+3. For k = 1 .. M/2, q = M - k: the real spectrum X_k and X_q from the
+   shared even / odd parts (:func:`_post_pair`), the phasors
    Y = X * (P.r, sign * P.i), then the half-length spectrum of the inverse
-   (pre(Y_k, Y_q, tw[k]), pre(Y_q, Y_k, tw[q])), stored conjugated.
+   (:func:`_pre_pair`), stored conjugated (k = M/2 pairs with itself: the k
+   values are stored last).
    DC and Nyquist: X_0 = Z_0.r + Z_0.i, X_M = Z_0.r - Z_0.i (real),
    Y_0 = X_0 P_0.r, Y_M = X_M P_M.r, stored (Y_0 + Y_M)/2, -((Y_0 - Y_M)/2).
 4. r = FFT_M(stored) (same stages); out[2j] = f32(r[j].r * (1/M)),
@@ -205,24 +206,33 @@ def _stockham(vr: np.ndarray, vi: np.ndarray, tw: np.ndarray):
     return vr, vi
 
 
-def _post(zar, zai, zbr, zbi, wr, wi):
-    er = (zar + zbr) * 0.5
-    ei = (zai - zbi) * 0.5
-    dr = zar - zbr
-    di = zai + zbi
-    orr = di * 0.5
-    oi = -(dr * 0.5)
-    return er + (wr * orr - wi * oi), ei + (wr * oi + wi * orr)
+def _post_pair(zkr, zki, zqr, zqi, wkr, wki, wqr, wqi):
+    """X_k and X_q (q = M - k) of the real spectrum from Z_k, Z_q: the even and
+    odd parts E = (er, ei), O = (orr, oi) are shared (E_q = conj E_k, O_q = conj
+    O_k), X = E + w O."""
+    er = (zkr + zqr) * 0.5
+    ei = (zki - zqi) * 0.5
+    orr = (zki + zqi) * 0.5
+    oi = -((zkr - zqr) * 0.5)
+    xkr = er + (wkr * orr - wki * oi)
+    xki = ei + (wkr * oi + wki * orr)
+    xqr = er + (wqr * orr + wqi * oi)
+    xqi = (wqi * orr - wqr * oi) - ei
+    return xkr, xki, xqr, xqi
 
 
-def _pre(yar, yai, ybr, ybi, wr, wi):
-    er = (yar + ybr) * 0.5
-    ei = (yai - ybi) * 0.5
-    hr = (yar - ybr) * 0.5
-    hi = (yai + ybi) * 0.5
-    orr = hr * wr + hi * wi
-    oi = hi * wr - hr * wi
-    return er - oi, ei + orr
+def _pre_pair(ykr, yki, yqr, yqi, wkr, wki, wqr, wqi):
+    """The inverse's half-length inputs Z'_k, Z'_q from Y_k, Y_q (the shared
+    sums and differences once)."""
+    er = (ykr + yqr) * 0.5
+    ei = (yki - yqi) * 0.5
+    hr = (ykr - yqr) * 0.5
+    hi = (yki + yqi) * 0.5
+    okr = hr * wkr + hi * wki
+    oki = hi * wkr - hr * wki
+    oqr = hi * wqi - hr * wqr
+    oqi = hi * wqr + hr * wqi
+    return er - oki, ei + okr, er - oqi, oqr - ei
 
 
 def rotate(x: np.ndarray, ph: np.ndarray, sign: int, tw: np.ndarray | None = None,
@@ -256,14 +266,12 @@ def _rotate(x, ph, sign, tw, base):
     k = np.arange(1, m // 2 + 1)
     q = m - k
     zkr, zki, zqr, zqi = vr[..., k], vi[..., k], vr[..., q], vi[..., q]
-    xkr, xki = _post(zkr, zki, zqr, zqi, tw[0][k], tw[1][k])
-    xqr, xqi = _post(zqr, zqi, zkr, zki, tw[0][q], tw[1][q])
+    xkr, xki, xqr, xqi = _post_pair(zkr, zki, zqr, zqi, tw[0][k], tw[1][k], tw[0][q], tw[1][q])
     ykr = xkr * pr[..., k] - xki * pi[..., k]
     yki = xkr * pi[..., k] + xki * pr[..., k]
     yqr = xqr * pr[..., q] - xqi * pi[..., q]
     yqi = xqr * pi[..., q] + xqi * pr[..., q]
-    zkr2, zki2 = _pre(ykr, yki, yqr, yqi, tw[0][k], tw[1][k])
-    zqr2, zqi2 = _pre(yqr, yqi, ykr, yki, tw[0][q], tw[1][q])
+    zkr2, zki2, zqr2, zqi2 = _pre_pair(ykr, yki, yqr, yqi, tw[0][k], tw[1][k], tw[0][q], tw[1][q])
     x0 = vr[..., 0] + vi[..., 0]
     xm = vr[..., 0] - vi[..., 0]
     y0 = x0 * pr[..., 0]

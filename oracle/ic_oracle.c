@@ -663,24 +663,31 @@ static void stockham(int m, double *v, double *tmp, const double *tw)
     }
 }
 
-/* real spectrum bin a from the half-length transform: za = Z_a, zb = Z_{M-a}, w = W^a */
-static void rot_post(const double *za, const double *zb, const double *w, double *x)
+/* X_k, X_q (q = M - k) of the real spectrum from Z_k, Z_q: the shared even and
+ * odd parts, X = E + w O (phase_rotation.py _post_pair) */
+static void rot_post_pair(const double *zk, const double *zq, const double *wk, const double *wq, double *xk,
+                          double *xq)
 {
-    const double er = (za[0] + zb[0]) * 0.5, ei = (za[1] - zb[1]) * 0.5;
-    const double dr = za[0] - zb[0], di = za[1] + zb[1];
-    const double orr = di * 0.5, oi = -(dr * 0.5);
-    x[0] = er + (w[0] * orr - w[1] * oi);
-    x[1] = ei + (w[0] * oi + w[1] * orr);
+    const double er = (zk[0] + zq[0]) * 0.5, ei = (zk[1] - zq[1]) * 0.5;
+    const double orr = (zk[1] + zq[1]) * 0.5, oi = -((zk[0] - zq[0]) * 0.5);
+    xk[0] = er + (wk[0] * orr - wk[1] * oi);
+    xk[1] = ei + (wk[0] * oi + wk[1] * orr);
+    xq[0] = er + (wq[0] * orr + wq[1] * oi);
+    xq[1] = (wq[1] * orr - wq[0] * oi) - ei;
 }
 
-/* half-length inverse input Z'_a from ya = Y_a, yb = Y_{M-a}, w = W^a */
-static void rot_pre(const double *ya, const double *yb, const double *w, double *z)
+/* the inverse's half-length inputs Z'_k, Z'_q from Y_k, Y_q (_pre_pair) */
+static void rot_pre_pair(const double *yk, const double *yq, const double *wk, const double *wq, double *zk,
+                         double *zq)
 {
-    const double er = (ya[0] + yb[0]) * 0.5, ei = (ya[1] - yb[1]) * 0.5;
-    const double hr = (ya[0] - yb[0]) * 0.5, hi = (ya[1] + yb[1]) * 0.5;
-    const double orr = hr * w[0] + hi * w[1], oi = hi * w[0] - hr * w[1];
-    z[0] = er - oi;
-    z[1] = ei + orr;
+    const double er = (yk[0] + yq[0]) * 0.5, ei = (yk[1] - yq[1]) * 0.5;
+    const double hr = (yk[0] - yq[0]) * 0.5, hi = (yk[1] + yq[1]) * 0.5;
+    const double okr = hr * wk[0] + hi * wk[1], oki = hi * wk[0] - hr * wk[1];
+    const double oqr = hi * wq[1] - hr * wq[0], oqi = hi * wq[0] + hr * wq[1];
+    zk[0] = er - oki;
+    zk[1] = ei + okr;
+    zq[0] = er - oqi;
+    zq[1] = oqr - ei;
 }
 
 /* One profile: out = rotation of f32(x - b) by the channel phasors p (sign +1:
@@ -707,20 +714,18 @@ static void rotate1(int n, const float *x, float b, const double *p, int sign, c
         const int q = m - k;
         double zk[2] = {v[2 * k], v[2 * k + 1]}, zq[2] = {v[2 * q], v[2 * q + 1]};
         double Xk[2], Xq[2], Yk[2], Yq[2], Zk[2], Zq[2];
-        rot_post(zk, zq, tw + 2 * k, Xk);
-        rot_post(zq, zk, tw + 2 * q, Xq);
+        rot_post_pair(zk, zq, tw + 2 * k, tw + 2 * q, Xk, Xq);
         const double pkr = p[2 * k], pki = sg * p[2 * k + 1];
         const double pqr = p[2 * q], pqi = sg * p[2 * q + 1];
         Yk[0] = Xk[0] * pkr - Xk[1] * pki;
         Yk[1] = Xk[0] * pki + Xk[1] * pkr;
         Yq[0] = Xq[0] * pqr - Xq[1] * pqi;
         Yq[1] = Xq[0] * pqi + Xq[1] * pqr;
-        rot_pre(Yk, Yq, tw + 2 * k, Zk);
-        rot_pre(Yq, Yk, tw + 2 * q, Zq);
-        v[2 * k] = Zk[0];
-        v[2 * k + 1] = -Zk[1];
+        rot_pre_pair(Yk, Yq, tw + 2 * k, tw + 2 * q, Zk, Zq);
         v[2 * q] = Zq[0];
         v[2 * q + 1] = -Zq[1];
+        v[2 * k] = Zk[0];   /* k = M/2 pairs with itself: k's values last */
+        v[2 * k + 1] = -Zk[1];
     }
     stockham(m, v, tmp, tw);
     const double inv = 1.0 / (double)m;
