@@ -182,3 +182,28 @@ def test_native_rccl_one_rank_shard_session():
             assert bits_equal(amp, one["amp"]) and bits_equal(T, one["T"])
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nbin,per_profile", [(256, False), (1024, False), (1024, True)])
+def test_local_shards_fft_dedispersion(nbin, per_profile, oracle_lib):
+    """psrchive's fractional dedispersion on channel shards: each rank rotates
+    its channels' rows with their delays (one per channel, or one per profile
+    as psrchive's per-Integration periods give), and at nbin 1024 its residual
+    rotation measures the rows in the same kernel.  World 2 and 4 equal one
+    session bit for bit, and the session equals the C oracle."""
+    from iterative_cleaner_amd import sharded, synth
+    nsub, nchan = 6, 1100
+    data, w0, shift = synth.make_cube(nsub, nchan, nbin, 39, 0.2)
+    raw = np.ascontiguousarray(data[:, 0])
+    delay = (synth.per_profile_delays(shift, nbin, nsub) if per_profile
+             else synth.fractional_delays(shift, nbin))
+    zero = np.zeros(nchan, np.int32)
+    one = _single(raw, w0, zero, delay=delay)
+    ref = oracle_lib.clean_loop(raw, w0, shift, want_details=True, delay=delay)
+    assert one["loops"] == ref["loops"] and bits_equal(one["weights"], ref["weights"])
+    assert bits_equal(one["amp"], ref["amp"]) and bits_equal(one["std"], ref["std"])
+    for world in (2, 4):
+        out = sharded.clean_cube_local(raw, w0, zero, world, want_details=True, delay=delay)
+        assert out["loops"] == one["loops"] and np.array_equal(out["changed"], one["changed"])
+        for key in ("weights", "test", "amp", "info", "std", "mean", "ptp", "fft", "T"):
+            assert bits_equal(out[key], one[key]), "world %d: %s differs" % (world, key)
