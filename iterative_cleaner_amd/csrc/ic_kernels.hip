@@ -3734,27 +3734,22 @@ __device__ __forceinline__ void rot_fft(double2 *v, const TW &tw, int t, double2
     }
 }
 
-// X_k, X_q (q = M - k) of the real spectrum from Z_k, Z_q: the even and odd
-// parts are shared (E_q = conj E_k, O_q = conj O_k), X = E + w O
-// (phase_rotation.py _post_pair, oracle rot_post_pair)
-__device__ __forceinline__ void rot_post_pair(double2 zk, double2 zq, double2 wk, double2 wq, double2 &xk,
-                                              double2 &xq)
+// The inverse's half-length inputs Z'_k, Z'_q (q = M - k) from the transform's
+// Z_k, Z_q in one linear map (phase_rotation.py _pair, oracle rot_pair): the
+// real spectrum X_k = E_k + w O_k, the phasors and the inverse's packing
+// composed, Z'_k = A_k Z_k + B_k conj(Z_q), Z'_q = A_q Z_q - conj(B_k) conj(Z_k),
+// with w = exp(-2 pi i k / N) = (c, sn) and the signed phasors pk, pq
+__device__ __forceinline__ void rot_pair(double2 zk, double2 zq, double2 w, double2 pk, double2 pq, double2 &ok,
+                                         double2 &oq)
 {
-    const double er = (zk.x + zq.x) * 0.5, ei = (zk.y - zq.y) * 0.5;
-    const double orr = (zk.y + zq.y) * 0.5, oi = -((zk.x - zq.x) * 0.5);
-    xk = make_double2(er + (wk.x * orr - wk.y * oi), ei + (wk.x * oi + wk.y * orr));
-    xq = make_double2(er + (wq.x * orr + wq.y * oi), (wq.y * orr - wq.x * oi) - ei);
-}
-// the inverse's half-length inputs Z'_k, Z'_q from Y_k, Y_q (_pre_pair)
-__device__ __forceinline__ void rot_pre_pair(double2 yk, double2 yq, double2 wk, double2 wq, double2 &zk,
-                                             double2 &zq)
-{
-    const double er = (yk.x + yq.x) * 0.5, ei = (yk.y - yq.y) * 0.5;
-    const double hr = (yk.x - yq.x) * 0.5, hi = (yk.y + yq.y) * 0.5;
-    const double okr = hr * wk.x + hi * wk.y, oki = hi * wk.x - hr * wk.y;
-    const double oqr = hi * wq.y - hr * wq.x, oqi = hi * wq.x + hr * wq.y;
-    zk = make_double2(er - oki, ei + okr);
-    zq = make_double2(er - oqi, oqr - ei);
+    const double h1 = (1.0 + w.y) * 0.5, h2 = (1.0 - w.y) * 0.5, hc = w.x * 0.5;
+    const double akr = h1 * pk.x + h2 * pq.x, aki = h1 * pk.y - h2 * pq.y;
+    const double aqr = h1 * pq.x + h2 * pk.x, aqi = h1 * pq.y - h2 * pk.y;
+    const double bkr = -(hc * (pk.y + pq.y)), bki = hc * (pk.x - pq.x);
+    ok = make_double2((akr * zk.x - aki * zk.y) + (bkr * zq.x + bki * zq.y),
+                      (akr * zk.y + aki * zk.x) + (bki * zq.x - bkr * zq.y));
+    oq = make_double2((aqr * zq.x - aqi * zq.y) + (bki * zk.y - bkr * zk.x),
+                      (aqr * zq.y + aqi * zq.x) + (bki * zk.x + bkr * zk.y));
 }
 
 // comprehensive_stats (ic.py:206-212) of the rotated residual row held by one
@@ -4105,22 +4100,13 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         rot_fft<N>(v, tw, t);
         }
         // the post step's twiddles, at their use
-        auto ld = [&](int u, double2 (&w2)[2]) {
-            const int k = t + u * TB;
-            if (k <= H) {
-                w2[0] = tw.post((unsigned)(k & (M - 1)));
-                w2[1] = tw.post((unsigned)((M - k) & (M - 1)));
-            }
-        };
-        double2 cw[2];
 #pragma unroll
         for (int u = 0; u < NK; ++u) {
-            ld(u, cw);
+            const int k = t + u * TB;
+            const double2 wk = k <= H ? tw.post((unsigned)(k & (M - 1))) : make_double2(0.0, 0.0);
             const double2 pk = phn[0], pq = phn[1];
             if (u + 1 < NK) ldph(u + 1, phn);
-            const int k = t + u * TB;
             if (k <= H) {
-                const double2 wk = cw[0], wq = cw[1];
                 if (k == 0) {
                     const double2 z0 = v[rsw(0)];
                     const double X0 = z0.x + z0.y, XM = z0.x - z0.y;
@@ -4129,12 +4115,8 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
                 } else {
                     const int q = M - k;
                     const double2 zk = v[rsw(k)], zq = v[rsw(q)];
-                    double2 Xk, Xq, Zk, Zq;
-                    rot_post_pair(zk, zq, wk, wq, Xk, Xq);
-                    const double pki = sg * pk.y, pqi = sg * pq.y;
-                    const double2 Yk = make_double2(Xk.x * pk.x - Xk.y * pki, Xk.x * pki + Xk.y * pk.x);
-                    const double2 Yq = make_double2(Xq.x * pq.x - Xq.y * pqi, Xq.x * pqi + Xq.y * pq.x);
-                    rot_pre_pair(Yk, Yq, wk, wq, Zk, Zq);
+                    double2 Zk, Zq;
+                    rot_pair(zk, zq, wk, make_double2(pk.x, sg * pk.y), make_double2(pq.x, sg * pq.y), Zk, Zq);
                     v[rsw(q)] = make_double2(Zq.x, -Zq.y);
                     v[rsw(k)] = make_double2(Zk.x, -Zk.y);
                 }

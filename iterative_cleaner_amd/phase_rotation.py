@@ -33,11 +33,10 @@ of s bins (``y[j] = x[j + s]`` for integer s; ``dedisperse`` rotates by +s,
    even outputs y_(2p) = DFT_4(c0..c3)_p, the odd y_(2p+1) = DFT_4(c4..c7)_p.
    (Round 6; rounds 2-5 ran radix-2 stages, 10 operations per butterfly
    against 98 per radix-8 butterfly of 8 points, 56 in the first stage.)
-3. For k = 1 .. M/2, q = M - k: the real spectrum X_k and X_q from the
-   shared even / odd parts (:func:`_post_pair`), the phasors
-   Y = X * (P.r, sign * P.i), then the half-length spectrum of the inverse
-   (:func:`_pre_pair`), stored conjugated (k = M/2 pairs with itself: the k
-   values are stored last).
+3. For k = 1 .. M/2, q = M - k: the half-length spectrum of the inverse from
+   Z_k, Z_q in one linear map (:func:`_pair`: the real spectrum, the phasors
+   (P.r, sign * P.i) and the inverse's packing composed; round 6), stored
+   conjugated (k = M/2 pairs with itself: the k values are stored last).
    DC and Nyquist: X_0 = Z_0.r + Z_0.i, X_M = Z_0.r - Z_0.i (real),
    Y_0 = X_0 P_0.r, Y_M = X_M P_M.r, stored (Y_0 + Y_M)/2, -((Y_0 - Y_M)/2).
 4. r = FFT_M(stored) (same stages); out[2j] = f32(r[j].r * (1/M)),
@@ -206,33 +205,29 @@ def _stockham(vr: np.ndarray, vi: np.ndarray, tw: np.ndarray):
     return vr, vi
 
 
-def _post_pair(zkr, zki, zqr, zqi, wkr, wki, wqr, wqi):
-    """X_k and X_q (q = M - k) of the real spectrum from Z_k, Z_q: the even and
-    odd parts E = (er, ei), O = (orr, oi) are shared (E_q = conj E_k, O_q = conj
-    O_k), X = E + w O."""
-    er = (zkr + zqr) * 0.5
-    ei = (zki - zqi) * 0.5
-    orr = (zki + zqi) * 0.5
-    oi = -((zkr - zqr) * 0.5)
-    xkr = er + (wkr * orr - wki * oi)
-    xki = ei + (wkr * oi + wki * orr)
-    xqr = er + (wqr * orr + wqi * oi)
-    xqi = (wqi * orr - wqr * oi) - ei
-    return xkr, xki, xqr, xqi
-
-
-def _pre_pair(ykr, yki, yqr, yqi, wkr, wki, wqr, wqi):
-    """The inverse's half-length inputs Z'_k, Z'_q from Y_k, Y_q (the shared
-    sums and differences once)."""
-    er = (ykr + yqr) * 0.5
-    ei = (yki - yqi) * 0.5
-    hr = (ykr - yqr) * 0.5
-    hi = (yki + yqi) * 0.5
-    okr = hr * wkr + hi * wki
-    oki = hi * wkr - hr * wki
-    oqr = hi * wqi - hr * wqr
-    oqi = hi * wqr + hr * wqi
-    return er - oki, ei + okr, er - oqi, oqr - ei
+def _pair(zkr, zki, zqr, zqi, c, sn, pkr, pki, pqr, pqi):
+    """The half-length inputs of the inverse, Z'_k and Z'_q (q = M - k), from
+    the transform's Z_k, Z_q in one linear map: with w = exp(-2 pi i k / N) =
+    (c, sn) and the phasors P_k, P_q (their imaginary parts signed for the
+    direction), the real spectrum X_k = E_k + w O_k, Y = P X and the inverse's
+    packing Z' = E' + i conj(w) H' compose to
+        Z'_k = A_k Z_k + B_k conj(Z_q),  Z'_q = A_q Z_q - conj(B_k) conj(Z_k),
+        A_k = ((1 + sn) P_k + (1 - sn) conj(P_q)) / 2,
+        A_q = ((1 + sn) P_q + (1 - sn) conj(P_k)) / 2,
+        B_k = i c (P_k - conj(P_q)) / 2."""
+    h1 = (1.0 + sn) * 0.5
+    h2 = (1.0 - sn) * 0.5
+    hc = c * 0.5
+    akr = h1 * pkr + h2 * pqr
+    aki = h1 * pki - h2 * pqi
+    aqr = h1 * pqr + h2 * pkr
+    aqi = h1 * pqi - h2 * pki
+    bkr = -(hc * (pki + pqi))
+    bki = hc * (pkr - pqr)
+    return ((akr * zkr - aki * zki) + (bkr * zqr + bki * zqi),
+            (akr * zki + aki * zkr) + (bki * zqr - bkr * zqi),
+            (aqr * zqr - aqi * zqi) + (bki * zki - bkr * zkr),
+            (aqr * zqi + aqi * zqr) + (bki * zkr + bkr * zki))
 
 
 def rotate(x: np.ndarray, ph: np.ndarray, sign: int, tw: np.ndarray | None = None,
@@ -266,12 +261,8 @@ def _rotate(x, ph, sign, tw, base):
     k = np.arange(1, m // 2 + 1)
     q = m - k
     zkr, zki, zqr, zqi = vr[..., k], vi[..., k], vr[..., q], vi[..., q]
-    xkr, xki, xqr, xqi = _post_pair(zkr, zki, zqr, zqi, tw[0][k], tw[1][k], tw[0][q], tw[1][q])
-    ykr = xkr * pr[..., k] - xki * pi[..., k]
-    yki = xkr * pi[..., k] + xki * pr[..., k]
-    yqr = xqr * pr[..., q] - xqi * pi[..., q]
-    yqi = xqr * pi[..., q] + xqi * pr[..., q]
-    zkr2, zki2, zqr2, zqi2 = _pre_pair(ykr, yki, yqr, yqi, tw[0][k], tw[1][k], tw[0][q], tw[1][q])
+    zkr2, zki2, zqr2, zqi2 = _pair(zkr, zki, zqr, zqi, tw[0][k], tw[1][k], pr[..., k], pi[..., k], pr[..., q],
+                                   pi[..., q])
     x0 = vr[..., 0] + vi[..., 0]
     xm = vr[..., 0] - vi[..., 0]
     y0 = x0 * pr[..., 0]
@@ -282,7 +273,7 @@ def _rotate(x, ph, sign, tw, base):
     ui[..., 0] = -((y0 - ym) * 0.5)
     ur[..., q] = zqr2
     ui[..., q] = -zqi2
-    ur[..., k] = zkr2      # k = M/2 pairs with itself: both expressions agree
+    ur[..., k] = zkr2      # k = M/2 pairs with itself: the k values are stored last
     ui[..., k] = -zki2
     rr, ri = _stockham(ur, ui, tw)
     inv = 1.0 / m

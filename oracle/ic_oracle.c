@@ -663,31 +663,20 @@ static void stockham(int m, double *v, double *tmp, const double *tw)
     }
 }
 
-/* X_k, X_q (q = M - k) of the real spectrum from Z_k, Z_q: the shared even and
- * odd parts, X = E + w O (phase_rotation.py _post_pair) */
-static void rot_post_pair(const double *zk, const double *zq, const double *wk, const double *wq, double *xk,
-                          double *xq)
+/* The inverse's half-length inputs Z'_k, Z'_q (q = M - k) from Z_k, Z_q in one
+ * linear map (phase_rotation.py _pair): w_k = (c, sn), phasors pk, pq (their
+ * imaginary parts signed for the direction). */
+static void rot_pair(const double *zk, const double *zq, double c, double sn, const double *pk, const double *pq,
+                     double *ok, double *oq)
 {
-    const double er = (zk[0] + zq[0]) * 0.5, ei = (zk[1] - zq[1]) * 0.5;
-    const double orr = (zk[1] + zq[1]) * 0.5, oi = -((zk[0] - zq[0]) * 0.5);
-    xk[0] = er + (wk[0] * orr - wk[1] * oi);
-    xk[1] = ei + (wk[0] * oi + wk[1] * orr);
-    xq[0] = er + (wq[0] * orr + wq[1] * oi);
-    xq[1] = (wq[1] * orr - wq[0] * oi) - ei;
-}
-
-/* the inverse's half-length inputs Z'_k, Z'_q from Y_k, Y_q (_pre_pair) */
-static void rot_pre_pair(const double *yk, const double *yq, const double *wk, const double *wq, double *zk,
-                         double *zq)
-{
-    const double er = (yk[0] + yq[0]) * 0.5, ei = (yk[1] - yq[1]) * 0.5;
-    const double hr = (yk[0] - yq[0]) * 0.5, hi = (yk[1] + yq[1]) * 0.5;
-    const double okr = hr * wk[0] + hi * wk[1], oki = hi * wk[0] - hr * wk[1];
-    const double oqr = hi * wq[1] - hr * wq[0], oqi = hi * wq[0] + hr * wq[1];
-    zk[0] = er - oki;
-    zk[1] = ei + okr;
-    zq[0] = er - oqi;
-    zq[1] = oqr - ei;
+    const double h1 = (1.0 + sn) * 0.5, h2 = (1.0 - sn) * 0.5, hc = c * 0.5;
+    const double akr = h1 * pk[0] + h2 * pq[0], aki = h1 * pk[1] - h2 * pq[1];
+    const double aqr = h1 * pq[0] + h2 * pk[0], aqi = h1 * pq[1] - h2 * pk[1];
+    const double bkr = -(hc * (pk[1] + pq[1])), bki = hc * (pk[0] - pq[0]);
+    ok[0] = (akr * zk[0] - aki * zk[1]) + (bkr * zq[0] + bki * zq[1]);
+    ok[1] = (akr * zk[1] + aki * zk[0]) + (bki * zq[0] - bkr * zq[1]);
+    oq[0] = (aqr * zq[0] - aqi * zq[1]) + (bki * zk[1] - bkr * zk[0]);
+    oq[1] = (aqr * zq[1] + aqi * zq[0]) + (bki * zk[0] + bkr * zk[1]);
 }
 
 /* One profile: out = rotation of f32(x - b) by the channel phasors p (sign +1:
@@ -713,15 +702,9 @@ static void rotate1(int n, const float *x, float b, const double *p, int sign, c
     for (int k = 1; k <= m / 2; ++k) {
         const int q = m - k;
         double zk[2] = {v[2 * k], v[2 * k + 1]}, zq[2] = {v[2 * q], v[2 * q + 1]};
-        double Xk[2], Xq[2], Yk[2], Yq[2], Zk[2], Zq[2];
-        rot_post_pair(zk, zq, tw + 2 * k, tw + 2 * q, Xk, Xq);
-        const double pkr = p[2 * k], pki = sg * p[2 * k + 1];
-        const double pqr = p[2 * q], pqi = sg * p[2 * q + 1];
-        Yk[0] = Xk[0] * pkr - Xk[1] * pki;
-        Yk[1] = Xk[0] * pki + Xk[1] * pkr;
-        Yq[0] = Xq[0] * pqr - Xq[1] * pqi;
-        Yq[1] = Xq[0] * pqi + Xq[1] * pqr;
-        rot_pre_pair(Yk, Yq, tw + 2 * k, tw + 2 * q, Zk, Zq);
+        double Zk[2], Zq[2];
+        const double pk[2] = {p[2 * k], sg * p[2 * k + 1]}, pq[2] = {p[2 * q], sg * p[2 * q + 1]};
+        rot_pair(zk, zq, tw[2 * k], tw[2 * k + 1], pk, pq, Zk, Zq);
         v[2 * q] = Zq[0];
         v[2 * q + 1] = -Zq[1];
         v[2 * k] = Zk[0];   /* k = M/2 pairs with itself: k's values last */
