@@ -3985,13 +3985,29 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         };
         // the post step's phasors one round ahead: the first round's are
         // requested with the rows, each later round's before the round before it
+        // RM (N >= 256): the last round would hold k = H alone, in lane 0.  Lane
+        // 0 takes it in round 0 instead of the DC / Nyquist bins, which it
+        // finishes after the rounds: no round with one active lane and no
+        // divergent branch in round 0 (the schedule only: the same operations).
+        // Not with per-profile delays: the extra high parts it holds spill there
+        // (C2 fft_pp 48.1 -> 48.6 ms; per-channel 46.8 -> 46.4)
+        constexpr bool RM = !PP && H % TB == 0;
+        constexpr int NR = RM ? NK - 1 : NK;
+        auto kof = [&](int u) { return (RM && u == 0 && t == 0) ? H : t + u * TB; };
         auto ldph = [&](int u, double2 (&pp)[2]) {
-            const int k = t + u * TB;
+            const int k = kof(u);
             if constexpr (PPX) {
                 const double2 b1 = bcast(u), b2 = bcast(NK + u), b3 = bcast(2 * NK + u);
                 if (k <= H) {
                     pp[0] = lo1 == 0 ? b1 : (w0 + u * TB == 0 ? A1 : ic_phasor_mul(A1, b1));
                     pp[1] = lo1 == 0 ? b3 : (M - 64 - w0 - u * TB == 0 ? A2 : ic_phasor_mul(A2, b2));
+                }
+                if (RM && u == 0) {   // lane 0's k = H: P0(H) from the round NK - 1 parts
+                    const double2 bh = bcast(NK - 1), bh3 = bcast(3 * NK - 1);
+                    if (t == 0) {
+                        pp[0] = bh;
+                        pp[1] = bh3;
+                    }
                 }
             } else if (k <= H) {
                 if constexpr (PP) {
@@ -4100,14 +4116,21 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         rot_fft<N>(v, tw, t);
         }
         // the post step's twiddles, at their use
+        // Re P(M) for the DC / Nyquist step after the rounds (RM); P(0) = (1, 0)
+        // exactly for every delay, so Y_0 = X_0 * 1 = X_0
+        double pmr = 0.0;
+        if constexpr (RM) {
+            if constexpr (PPX) pmr = bcast(2 * NK).x;   // P0(M), lane 2 NK of the wave's high parts
+            else pmr = rot_ld(phr, 16u * (unsigned)M, 0).x;
+        }
 #pragma unroll
-        for (int u = 0; u < NK; ++u) {
-            const int k = t + u * TB;
+        for (int u = 0; u < NR; ++u) {
+            const int k = kof(u);
             const double2 wk = k <= H ? tw.post((unsigned)(k & (M - 1))) : make_double2(0.0, 0.0);
             const double2 pk = phn[0], pq = phn[1];
-            if (u + 1 < NK) ldph(u + 1, phn);
+            if (u + 1 < NR) ldph(u + 1, phn);
             if (k <= H) {
-                if (k == 0) {
+                if (!RM && k == 0) {
                     const double2 z0 = v[rsw(0)];
                     const double X0 = z0.x + z0.y, XM = z0.x - z0.y;
                     const double Y0 = X0 * pk.x, YM = XM * pq.x;
@@ -4120,6 +4143,14 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
                     v[rsw(q)] = make_double2(Zq.x, -Zq.y);
                     v[rsw(k)] = make_double2(Zk.x, -Zk.y);
                 }
+            }
+        }
+        if constexpr (RM) {
+            if (t == 0) {   // DC and Nyquist: X_0 = Z_0.r + Z_0.i, X_M = Z_0.r - Z_0.i
+                const double2 z0 = v[rsw(0)];
+                const double X0 = z0.x + z0.y, XM = z0.x - z0.y;
+                const double Y0 = X0, YM = XM * pmr;
+                v[rsw(0)] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
             }
         }
         gsync<TB / 64>();
