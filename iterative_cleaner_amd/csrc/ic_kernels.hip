@@ -3770,6 +3770,7 @@ __device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2
 {
     constexpr int M = RotCfg<N>::M, H = M / 2, TB = RotCfg<N>::TB, L = TB;
     static_assert(N == 1024 && TB == 64 && CLay<N>::L == 64, "one wave per profile, 16 samples per lane");
+    static_assert(RotCfg<N>::TW_LDS, "the statistics FFT reads k_diag's table from the rotation's LDS copy (tw.t)");
     float xr[16];   // sample 2(t + 64 q) + e at xr[2q + e]
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
