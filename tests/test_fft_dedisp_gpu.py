@@ -292,3 +292,47 @@ def test_fft_mode_argument_errors():
         assert rc == -4 and b"ic_set_delays" in lib.ic_last_error()
     finally:
         lib.ic_session_destroy(h)
+
+
+@pytest.mark.parametrize("per_profile", [False, True])
+def test_fused_residual_statistics_edge_cases(per_profile, oracle_lib):
+    """The residual rotation that measures its rows (nbin 1024, IC_OPT_ROT_STATS)
+    on the inputs its epilogue branches on: fractional weights (X = f32(R w)),
+    zero weights (invalid profiles: fftmax 0), a pulse region in the residual,
+    an all-zero profile and a spike, per-channel and per-profile delays (the
+    non-finite samples are the fft_nonfinite_edge fixture's).  Fused and
+    two-pass runs are bit-identical, and both equal the C oracle."""
+    from iterative_cleaner_amd import _native, synth
+    nsub, nchan, nbin = 6, 96, 1024
+    data, w0, shift = synth.make_cube(nsub, nchan, nbin, 41, 0.2)
+    raw = np.ascontiguousarray(data[:, 0])
+    raw[2, 60, :] = 0.0
+    raw[1, 7, 100:104] += 5e3                  # an impulsive spike
+    w0 = w0.copy()
+    w0[:, 3] = 0.0
+    w0[0, 10:20] = 0.25
+    w0[5, 50] = 0.6
+    delay = (synth.per_profile_delays(shift, nbin, nsub) if per_profile
+             else synth.fractional_delays(shift, nbin))
+    args = dict(max_iter=5, chanthresh=4.0, subintthresh=4.0, pulse_region=[0.5, 200, 340])
+
+    def run(rst):
+        with _native.GpuSession(nsub, nchan, nbin, args["max_iter"], args["chanthresh"], args["subintthresh"],
+                                args["pulse_region"], device=0, delay=delay, options={"rot_stats": rst}) as s:
+            s.upload(raw, w0, np.zeros(nchan, np.int32))
+            out = s.run()
+            out["amp"], out["info"] = s.fit()
+            out["diag"] = s.diagnostics()
+        return out
+
+    fused, split = run(1), run(0)
+    ref = oracle_lib.clean_loop(raw, w0, shift, args["chanthresh"], args["subintthresh"], args["max_iter"],
+                                _pr(args, nbin), want_details=True, delay=delay)
+    for key in ("weights", "test", "amp", "info"):
+        assert bits_equal(fused[key], split[key]), key
+    for x0, x1 in zip(split["diag"], fused["diag"]):
+        assert _same(x1, x0)
+    assert fused["loops"] == ref["loops"] and bits_equal(fused["weights"], ref["weights"])
+    sd, mn, pt, ff = fused["diag"]
+    assert _same(sd, ref["std"]) and _same(mn, ref["mean"]) and _same(pt, ref["ptp"])
+    assert _close(ff, ref["fft"]) and _close(fused["test"], ref["test"])
