@@ -242,8 +242,8 @@ int ic_get_run_stats(void *session, ic_run_stats *out);
  *                          for nbin >= 2048)
  *   IC_OPT_DIAG_FORK       fit round after which the diagnostics of the fitted
  *                          profiles run on a second stream, 0..64, 0 = no fork;
- *                          3 with integer dedispersion (4 for nbin >= 2048), 0
- *                          with the FFT rotation (exact fit only)
+ *                          3 (4 for nbin >= 2048 with integer dedispersion)
+ *                          (exact fit only)
  *   IC_OPT_FORK_DELAY      rounds between that round and the forked pass, 0..8;
  *                          1 (2 for nbin >= 2048)
  *   IC_OPT_TEMPLATE_INCR   1 = incremental template stage (integer

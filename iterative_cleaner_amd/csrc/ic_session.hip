@@ -1059,10 +1059,12 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
     }
     AL(s->TT, 1);
     s->fftded = p.dedisp_mode == IC_DEDISP_FFT;
-    // the FFT mode's forked pass (its residual rotations with the statistics)
-    // slows the late fit rounds more than it hides: off by default there
-    // (C2 --dedisp fft: 56.7-56.9 ms per clean forked, 55.4-55.5 unforked)
-    if (s->fftded) s->diag_fork = 0;
+    // The FFT mode forks too (round 6): its forked pass is the residual rotation
+    // that measures the rows, one kernel since the statistics moved into it, and
+    // it now hides behind the late fit rounds (C2 --dedisp fft 45.51-45.70 ->
+    // 45.03-45.06 ms per clean, per-profile delays 47.23-47.44 -> 47.04-47.19,
+    // alternating on one box; round 4, with two kernels per forked pass and the
+    // radix-2 rotation, it had lost: 55.4-55.5 unforked, 56.7-56.9 forked)
     // large sessions hand over later: C2 (1.15 M profiles) 26.49-26.56 ms per
     // clean at 8192, 26.19-26.23 at 4096 (2048: 26.23-26.28, 6144: 26.30-26.34),
     // C3 flat; C4 and C5 lose at 4096 (2.90 -> 3.02-3.04, 46.5 -> 46.9)

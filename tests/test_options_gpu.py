@@ -40,7 +40,7 @@ def test_option_ranges_and_modes():
             s.set_option("diag_fork", 3)
         s.set_option("diag_fork", 0)
     with _native.GpuSession(4, 64, 256, device=0, delay=np.zeros(64)) as s:
-        assert s.get_option("diag_fork") == 0 and s.get_option("template_incr") == 1
+        assert s.get_option("diag_fork") == 3 and s.get_option("template_incr") == 1
         assert s.get_option("fit_tiled") == 1
         for name in ("template_incr", "fit_tiled", "diag_fork", "rot_stats"):
             s.set_option(name, 0)
