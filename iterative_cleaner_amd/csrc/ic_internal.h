@@ -398,6 +398,10 @@ struct RotateArgs {
     int in_tiled, out2_tiled;
     const uint8_t *late;
     int late_sel;
+    // list (optional): rotate only the profiles of this round list (RoundList:
+    // A requests from the front, B from the end, counts packed in *nctr)
+    const int32_t *list;
+    const unsigned long long *nctr;
     // statistics of the rotated rows (std_o != nullptr; residual input, sign
     // -1, rotate_stats_supported): instead of writing row p to out, the kernel
     // measures X = f32(row * w0[p]) as k_diag's DIAG_STATS pass would (ic.py:

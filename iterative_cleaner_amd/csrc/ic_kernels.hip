@@ -3936,9 +3936,7 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
     }
     // every global load of a profile in flight at once: one memory latency
     // per profile, not one per row (or per flag / fit lookup)
-    auto load_rows = [&](size_t it, float4 (&xr)[NJ]) {
-        const unsigned c = (unsigned)(it / nsub), s = (unsigned)(it % nsub);
-        const size_t k = (size_t)s * nchan + c;
+    auto load_rows = [&](size_t k, float4 (&xr)[NJ]) {
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
             const int j2 = t + u * TB;
@@ -3953,9 +3951,24 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
     };
     // a block's profiles are consecutive items (channel-major): they share a
     // channel's phasor row
-    for (size_t item = (size_t)blockIdx.x * WPB + wv; item < P; item += (size_t)gridDim.x * WPB) {
-        const unsigned c = (unsigned)(item / nsub), s = (unsigned)(item % nsub);
-        const size_t p = (size_t)s * nchan + c;
+    // items: channel-major over every profile, or the profiles of a round list
+    // (RotateArgs.list: the diagnostics fork's second pass, the profiles still
+    // fitting at its round - a scan of every profile for their late flags cost
+    // that pass 2.7-3.4 ms per iteration on C2 for a tenth of the profiles)
+    const RoundList rl(a.list, a.nctr, (long)P);
+    const size_t nitems = a.list ? (size_t)rl.n() : P;
+    for (size_t item = (size_t)blockIdx.x * WPB + wv; item < nitems; item += (size_t)gridDim.x * WPB) {
+        unsigned c, s;
+        size_t p;
+        if (a.list) {
+            p = (size_t)rl.at((long)item);
+            c = (unsigned)(p % nchan);
+            s = (unsigned)(p / nchan);
+        } else {
+            c = (unsigned)(item / nsub);
+            s = (unsigned)(item % nsub);
+            p = (size_t)s * nchan + c;
+        }
         if (skip(p, s)) continue;
         const __amdgpu_buffer_rsrc_t phr = rot_rsrc(PP ? a.tw : a.ph + (size_t)c * (M + 1), M + 1);
         const double dly = PP ? a.delay2[p] : 0.0;
@@ -4065,7 +4078,7 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
             rot_fft<N, 0, true, false>(v, tw, t, z);
         } else {
         float4 xin[NJ];
-        load_rows(item, xin);
+        load_rows(p, xin);
         if (a.amp) {
             // the residual of the exact fit (k_residual's arithmetic), formed on the fly;
             // the template is requested with the rows, before the status is known
@@ -5360,7 +5373,7 @@ hipError_t launch_rotate(hipStream_t st, const RotateArgs &a)
         (!a.ph && !a.delay2 && !a.identity) ||
         (a.ld_in & 3) || (a.ldo & 3) || (a.out2 && (a.ldo2 < a.nbin || (a.ldo2 & 3))) ||
         (a.amp && (!a.T64 || !a.info)) || (a.in_tiled && (a.ld_in & 31)) || (a.out2_tiled && (a.ldo2 & 31)) ||
-        (a.identity && (a.amp || a.late)))
+        (a.identity && (a.amp || a.late || a.list)) || (a.list && !a.nctr))
         return hipErrorInvalidValue;
     if (a.identity) {
         IC_GGL(k_rotate_identity, dim3((unsigned)std::min<size_t>(cdiv(P, 4), 16384)), dim3(256), 0, st, a);

@@ -1627,8 +1627,19 @@ int run_impl(Session *s, double *test_out, float *weights_out, int32_t *loops_ou
             // rotated on dstream)
             RotateArgs ra = residual_rotate_args(s, pr_start, pr_end);
             if (s->fork_round >= 0) {
-                ra.late = s->late;
-                ra.late_sel = 1;
+                // pass B: the profiles still fitting at the fork round.  With
+                // per-profile delays from the round's survivor list (C2 fft_pp
+                // 47.64-47.80 -> 47.24-47.34 ms per clean); with a channel's
+                // phasor table by the late flags over the channel-major items,
+                // whose profiles share the table row (the list: 45.44-45.57 ->
+                // 45.77-45.88)
+                if (s->delay2) {
+                    ra.list = s->lists + 2 * s->P;
+                    ra.nctr = (const unsigned long long *)s->rcount + s->fork_round;
+                } else {
+                    ra.late = s->late;
+                    ra.late_sel = 1;
+                }
             }
             if (rot_stats_on(s)) with_stats(s, ra);
             LAUNCH(s, K_ROTATE, launch_rotate(s->stream, ra));
