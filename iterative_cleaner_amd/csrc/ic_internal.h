@@ -374,7 +374,7 @@ struct RotateArgs {
     const float *in;
     long ld_in;
     const float *base;          // [P] or nullptr (0)
-    const double2 *ph;          // [nchan][nbin/2 + 1]: ic_phasor(k, delay[c], nbin)
+    const float *ph;            // [nchan][nbin/2 + 1][2]: f32(ic_phasor(k, delay[c], nbin))
     const double *delay2;       // [P] per-profile delays (ic_set_delays2): phasors
                                 // ic_phasor(k, delay2[p], nbin) evaluated in the kernel, ph unused
     int identity;               // the rotation is the identity (an archive stored

@@ -3512,18 +3512,24 @@ __global__ __launch_bounds__(256) void k_residual(const float *__restrict__ D, c
 
 // ---------------------------------------------------------------------------
 // Fractional dedispersion: psrchive's FFT phase rotation in the stand-in's
-// written order (phase_rotation.py; oracle orc_rotate).  A profile per wave
-// (N <= 1024: four to a block, sharing the twiddle tables staged in LDS) or per
-// block (N >= 2048); grid-stride over channel-major items so that the profiles
-// in flight share a channel's phasor row in L2; the N/2 complex points live in
-// LDS between the passes.
-//   1. z[j] = (f64(f32(x[2j] - b)), f64(f32(x[2j+1] - b)))
-//   2. Z = FFT_{N/2}(z), radix-2 Stockham, register-staged in place
-//   3. pairs (k, N/2 - k): real spectrum, x phasor, inverse half-spectrum (conj)
-//   4. r = FFT_{N/2}(that); out = f32(r.re / M), f32(-r.im / M)
-// Every f64 operation is separately rounded (-ffp-contract=off), so the result
-// is the oracle's bit for bit; the FFT runs its radix-2 stages three at a time
-// in registers (rot_pass), which changes the data movement, not the arithmetic.
+// written order (phase_rotation.py; oracle orc_rotate), in IEEE f32 as
+// psrchive's.  A profile per wave (N <= 1024: four to a block, sharing the
+// twiddle tables staged in LDS) or per block (N >= 2048); grid-stride over
+// channel-major items so that the profiles in flight share a channel's phasor
+// row in L2; the N/2 complex points live in LDS between the passes.
+//   1. z[j] = (f32(x[2j] - b), f32(x[2j+1] - b))
+//   2. Z = FFT_{N/2}(z): Stockham stages of radix 8 (then 4 or 2), one LDS
+//      round trip per stage
+//   3. pairs (k, N/2 - k): real spectrum, x phasor, inverse half-spectrum
+//      (conj) in one linear map (rot_pair)
+//   4. r = FFT_{N/2}(that); out = r.re / M, -r.im / M
+// A complex point is an f32 pair (rc2) and every complex operation one packed
+// VOP3P instruction (v_pk_add_f32 / v_pk_mul_f32 with op_sel / neg modifiers
+// for the swaps and the one-sided signs), each half an IEEE f32 operation of
+// the definition: the same bits as the oracle's scalar f32 code
+// (-ffp-contract=off), at half the f64 instruction count.
+typedef float rc2 __attribute__((ext_vector_type(2)));
+
 template <int N>
 struct RotCfg {
     static constexpr int M = N / 2, H = M / 2;
@@ -3531,113 +3537,165 @@ struct RotCfg {
                                                                               : N == 2048 ? 10 : 11;   // log2 M
     static constexpr int TB = M / 8 < 64 ? 64 : (M / 8 > 256 ? 256 : M / 8);
     // one-wave profiles run four to a block, which stages the twiddle table in
-    // LDS once for all four (M entries: every index the passes and the post
-    // step use is below M)
+    // LDS once for all four
     static constexpr int WPB = TB == 64 ? 4 : 1;
     static constexpr bool TW_LDS = WPB > 1;
 };
 
-// LDS slot of complex point i: i with its low three bits XORed by bits 3-5.
-// ds_write_b128 serves 8 contiguous lanes per LDS cycle and ds_read_b128 16
-// lanes in the groups {0-3, 12-15, 20-27}, ... (MI355X_MICROARCH.md); unswizzled
-// the first pass's stores (lane ja -> points 8 ja + q) are 4-way, and the round-4
-// padding (a pad slot after every 8 points) made the stores conflict-free but
-// the contiguous reads 2-way.  The swizzle is conflict-free on both, and on the
-// other passes' stores (64 a + b + 8 q, 512 a + b + 64 q); reads of ja + q G
-// (G a multiple of 64) and stores of b + 64 q keep per-q immediate offsets.
-__device__ __forceinline__ constexpr int rsw(int i) { return i ^ ((i >> 3) & 7); }
-template <int M> constexpr int rot_lds_slots() { return M; }
+// LDS slot of complex point i: one pad slot after every 8 points.  With 8-byte
+// points ds_write_b64 banks 16 contiguous lanes on (slot mod 16) and ds_read_b64
+// 32 lanes on (slot mod 32) (MI355X_MICROARCH.md): the stage stores (lane t ->
+// points 8 t + q, and 64 (t / 8) + t % 8 + 8 q) are conflict-free, the
+// contiguous reads (t + 64 q) 2-way on 3 of 32 banks.  A XOR swizzle cannot
+// make the stores conflict-free without per-q address arithmetic on the reads
+// (bits 6+ of the slot change with q).  All offsets are per-lane bases plus
+// immediates: rsl(i + 8 c) = rsl(i) + 9 c.
+__device__ __forceinline__ constexpr int rsl(int i) { return i + (i >> 3); }
+template <int M> constexpr int rot_slots() { return M + M / 8; }
 
-// R consecutive radix-2 Stockham stages (ns = 2^lg .. 2^(lg+R-1)) through
-// registers: group ja < G = M/2^R holds the 2^R points v[ja + q G]; the stages
-// run on them as a local Stockham of size 2^R whose butterfly (l, jl) is the
-// global butterfly with k = (jl mod 2^l) * ns + ja mod ns, and the results land
-// at v[(ja / ns) 2^R ns + ja mod ns + p ns].  Same operations, same operands as
-// R separate stages (phase_rotation._stockham), i.e. the same bits, with one
-// LDS round trip instead of R.
-// 16-byte loads of the twiddle / phasor tables through a buffer descriptor:
-// a 32-bit per-lane offset plus an immediate, instead of a 64-bit address
-// register per table entry kept live across the profile loop
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rot_rsrc(const double2 *p, unsigned entries)
+// packed complex arithmetic (each half one IEEE f32 operation)
+__device__ __forceinline__ rc2 pk_nlo(rc2 a, rc2 b)   // (a.x - b.x, a.y + b.y)
 {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(p), 0, (int)(16u * entries), 0x00020000);
+    rc2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ rc2 pk_nhi(rc2 a, rc2 b)   // (a.x + b.x, a.y - b.y)
+{
+    rc2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ rc2 pk_mi(rc2 a, rc2 b)   // a + (-i) b = (a.x + b.y, a.y - b.x)
+{
+    rc2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ rc2 pk_pi(rc2 a, rc2 b)   // a + i b = (a.x - b.y, a.y + b.x)
+{
+    rc2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ rc2 pk_c7(rc2 c)   // (c.y - c.x, c.x + c.y)
+{
+    rc2 r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[0,1]" : "=v"(r) : "v"(c));
+    return r;
+}
+__device__ __forceinline__ rc2 pk_cross(rc2 a, rc2 b)   // (a.y + b.y, a.x - b.x)
+{
+    rc2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ rc2 pk_addc(rc2 a, rc2 b)   // (a.x + b.x, (-a.y) + (-b.y))
+{
+    rc2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ rc2 rc2_of(double2 d) { return (rc2){(float)d.x, (float)d.y}; }
+
+// 8-byte loads of the phasor table / 16-byte loads of the f64 twiddle table
+// through a buffer descriptor: a 32-bit per-lane offset plus an immediate,
+// instead of a 64-bit address register per table entry kept live across the
+// profile loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rot_rsrc(const void *p, unsigned bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
 }
 __device__ __forceinline__ double2 rot_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
 {
     return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ rc2 rot_ld2(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
+{
+    return __builtin_bit_cast(rc2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
 
 // Twiddle sources: k_diag_p2's table (p2_twiddles: M plain entries tw[i] =
 // exp(-2 pi i i / N), then for every Stockham stage after the first, of radix
 // R and span ns, the entries w^(q k), w = exp(-2 pi i / (R ns)), as [k][q - 1]
 // at M + ns - 8: the spans are 8, 64, 512, so the earlier tables fill ns - 8
-// slots), in global memory (through L1/L2) or staged in LDS.  Its entries are
-// the plain table's tw[q k N / (R ns)], the same long-double values.
+// slots), the same long-double values rounded to f64; the rotation uses them
+// rounded to f32.  Staged in LDS as f32 (TwLds32), or read as f64 and rounded
+// at the use: from the f64 LDS copy the residual's statistics FFT needs
+// (TwLds64), or through L1/L2 (TwGlobal, one-block profiles N >= 2048).
 template <int N>
 struct TwGlobal {
     __amdgpu_buffer_rsrc_t r;
     template <int NS, int R>
-    __device__ __forceinline__ double2 stage(unsigned k, int q) const
+    __device__ __forceinline__ rc2 stage(unsigned k, int q) const
     {
-        return rot_ld(r, 16u * (unsigned)(k * (R - 1)), 16u * (unsigned)(N / 2 + NS - 8 + q - 1));
+        return rc2_of(rot_ld(r, 16u * (unsigned)(k * (R - 1)), 16u * (unsigned)(N / 2 + NS - 8 + q - 1)));
     }
-    __device__ __forceinline__ double2 post(unsigned i) const { return rot_ld(r, 16u * i, 0); }
+    __device__ __forceinline__ rc2 post(unsigned i) const { return rc2_of(rot_ld(r, 16u * i, 0)); }
 };
 template <int N>
-struct TwLds {
-    const double2 *t;
+struct TwLds32 {
+    const rc2 *t;
     template <int NS, int R>
-    __device__ __forceinline__ double2 stage(unsigned k, int q) const
+    __device__ __forceinline__ rc2 stage(unsigned k, int q) const
     {
         return t[N / 2 + NS - 8 + q - 1 + k * (R - 1)];
     }
-    __device__ __forceinline__ double2 post(unsigned i) const { return t[i]; }
+    __device__ __forceinline__ rc2 post(unsigned i) const { return t[i]; }
+};
+template <int N>
+struct TwLds64 {
+    const double2 *t;
+    template <int NS, int R>
+    __device__ __forceinline__ rc2 stage(unsigned k, int q) const
+    {
+        return rc2_of(t[N / 2 + NS - 8 + q - 1 + k * (R - 1)]);
+    }
+    __device__ __forceinline__ rc2 post(unsigned i) const { return rc2_of(t[i]); }
 };
 
-// the rotation's complex product: (a.r w.r - a.i w.i, a.r w.i + a.i w.r)
-__device__ __forceinline__ double2 rot_cmul(double2 a, double2 w)
+// the rotation's complex product (a.r w.r - a.i w.i, a.r w.i + a.i w.r):
+// (a.r w.r, a.r w.i) and (a.i w.i, a.i w.r), then one add with the low half
+// subtracted
+__device__ __forceinline__ rc2 rot_cmul(rc2 a, rc2 w)
 {
-    return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+    return pk_nlo(a.xx * w, a.yy * w.yx);
 }
 // DFT of 4 / 8 points in place, natural output order, in the written order of
-// phase_rotation.py (_dft4, _dft8) and the oracle (dft4, dft8)
-__device__ __forceinline__ void rot_dft4(double2 *b)
+// phase_rotation.py (_dft4, _dft8) and the oracle (dft4, dft8): c3 = -i d is
+// folded into y1 = c1 + c3 = pk_mi(c1, d) and y3 = c1 - c3 = pk_pi(c1, d)
+// (x + (-y) is x - y bit for bit), and c6 = -i c6 into the odd DFT_4's first
+// level the same way
+__device__ __forceinline__ void rot_dft4(rc2 *b)
 {
-    const double2 c0 = make_double2(b[0].x + b[2].x, b[0].y + b[2].y);
-    const double2 c1 = make_double2(b[0].x - b[2].x, b[0].y - b[2].y);
-    const double2 c2 = make_double2(b[1].x + b[3].x, b[1].y + b[3].y);
-    const double dr = b[1].x - b[3].x, di = b[1].y - b[3].y;
-    const double2 c3 = make_double2(di, -dr);
-    b[0] = make_double2(c0.x + c2.x, c0.y + c2.y);
-    b[1] = make_double2(c1.x + c3.x, c1.y + c3.y);
-    b[2] = make_double2(c0.x - c2.x, c0.y - c2.y);
-    b[3] = make_double2(c1.x - c3.x, c1.y - c3.y);
+    const rc2 c0 = b[0] + b[2], c1 = b[0] - b[2], c2 = b[1] + b[3], d = b[1] - b[3];
+    b[0] = c0 + c2;
+    b[1] = pk_mi(c1, d);
+    b[2] = c0 - c2;
+    b[3] = pk_pi(c1, d);
 }
-__device__ __forceinline__ void rot_dft8(double2 *b)
+__device__ __forceinline__ void rot_dft8(rc2 *b)
 {
-    constexpr double s = 0x1.6a09e667f3bcdp-1;   // f64(sqrt(2)/2)
-    double2 c[8];
+    constexpr float s = (float)0x1.6a09e667f3bcdp-1;   // f32(f64(sqrt(2)/2))
+    rc2 c[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        c[q] = make_double2(b[q].x + b[q + 4].x, b[q].y + b[q + 4].y);
-        c[q + 4] = make_double2(b[q].x - b[q + 4].x, b[q].y - b[q + 4].y);
+        c[q] = b[q] + b[q + 4];
+        c[q + 4] = b[q] - b[q + 4];
     }
-    {
-        const double t1 = c[5].x + c[5].y, t2 = c[5].y - c[5].x;
-        c[5] = make_double2(t1 * s, t2 * s);
-    }
-    c[6] = make_double2(c[6].y, -c[6].x);
-    {
-        const double t1 = c[7].y - c[7].x, t2 = c[7].x + c[7].y;
-        c[7] = make_double2(t1 * s, -(t2 * s));
-    }
+    c[5] = pk_mi(c[5], c[5]) * (rc2){s, s};    // ((c.r + c.i) s, (c.i - c.r) s)
+    c[7] = pk_c7(c[7]) * (rc2){s, -s};         // ((c.i - c.r) s, -((c.r + c.i) s))
     rot_dft4(c);
-    rot_dft4(c + 4);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        b[2 * p] = c[p];
-        b[2 * p + 1] = c[p + 4];
-    }
+    // odd DFT_4 of (c4, c5, -i c6, c7)
+    const rc2 e0 = pk_mi(c[4], c[6]), e1 = pk_pi(c[4], c[6]), e2 = c[5] + c[7], d = c[5] - c[7];
+    b[0] = c[0];
+    b[2] = c[1];
+    b[4] = c[2];
+    b[6] = c[3];
+    b[1] = e0 + e2;
+    b[3] = pk_mi(e1, d);
+    b[5] = e0 - e2;
+    b[7] = pk_pi(e1, d);
 }
 
 // One Stockham stage of radix Q = 2^R and span ns = 2^LGS (phase_rotation.py
@@ -3650,7 +3708,7 @@ __device__ __forceinline__ void rot_dft8(double2 *b)
 // ja + q G, the distribution the first pass reads, so a profile can enter and
 // leave the FFT in registers (k_rotate's direct layout).
 template <int N, int R, int LGS, bool IN_REG = false, bool OUT_REG = false, typename TW>
-__device__ __forceinline__ void rot_pass(double2 *v, const TW &tw, int t, double2 *z = nullptr)
+__device__ __forceinline__ void rot_pass(rc2 *v, const TW &tw, int t, rc2 *z = nullptr)
 {
     using C = RotCfg<N>;
     constexpr int M = C::M, TB = C::TB, G = M >> R, Q = 1 << R;
@@ -3658,9 +3716,9 @@ __device__ __forceinline__ void rot_pass(double2 *v, const TW &tw, int t, double
     constexpr int ns = 1 << LGS;
     static_assert(!(IN_REG || OUT_REG) || G == TB, "register passes hold one group per thread");
     static_assert(ns == 1 || ns >= 8, "stage spans are 1, 8, 64, 512");
-    double2 u[GPT][Q];
+    rc2 u[GPT][Q];
     // the stage's twiddles first (their latency overlaps the LDS reads and the barrier)
-    double2 w[GPT][Q - 1];
+    rc2 w[GPT][Q - 1];
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
         const int ja = t + TB * gi;
@@ -3673,13 +3731,13 @@ __device__ __forceinline__ void rot_pass(double2 *v, const TW &tw, int t, double
             if constexpr (IN_REG) {
 #pragma unroll
                 for (int q = 0; q < Q; ++q) u[gi][q] = z[q];
-            } else if constexpr (G % 64 == 0) {
-                const double2 *vj = v + rsw(ja);    // rsw(ja + q G) = rsw(ja) + q G
+            } else if constexpr (G % 8 == 0) {
+                const rc2 *vj = v + rsl(ja);    // rsl(ja + q G) = rsl(ja) + q (G + G/8)
 #pragma unroll
-                for (int q = 0; q < Q; ++q) u[gi][q] = vj[q * G];
+                for (int q = 0; q < Q; ++q) u[gi][q] = vj[q * (G + G / 8)];
             } else {
 #pragma unroll
-                for (int q = 0; q < Q; ++q) u[gi][q] = v[rsw(ja + q * G)];
+                for (int q = 0; q < Q; ++q) u[gi][q] = v[rsl(ja + q * G)];
             }
         }
     }
@@ -3698,22 +3756,27 @@ __device__ __forceinline__ void rot_pass(double2 *v, const TW &tw, int t, double
             } else if constexpr (Q == 4) {
                 rot_dft4(u[gi]);
             } else {
-                const double2 a = u[gi][0], b = u[gi][1];
-                u[gi][0] = make_double2(a.x + b.x, a.y + b.y);
-                u[gi][1] = make_double2(a.x - b.x, a.y - b.y);
+                const rc2 a = u[gi][0], b = u[gi][1];
+                u[gi][0] = a + b;
+                u[gi][1] = a - b;
             }
             const int base = ((ja >> LGS) << (LGS + R)) + k;
             if constexpr (OUT_REG) {
                 static_assert(ns * Q == M, "only the last pass keeps its output");
 #pragma unroll
                 for (int q = 0; q < Q; ++q) z[q] = u[gi][q];
-            } else if constexpr (ns % 64 == 0) {
-                double2 *vb = v + rsw(base);   // rsw(base + q ns) = rsw(base) + q ns
+            } else if constexpr (ns % 8 == 0) {
+                rc2 *vb = v + rsl(base);   // rsl(base + q ns) = rsl(base) + q (ns + ns/8)
 #pragma unroll
-                for (int q = 0; q < Q; ++q) vb[q * ns] = u[gi][q];
+                for (int q = 0; q < Q; ++q) vb[q * (ns + ns / 8)] = u[gi][q];
             } else {
+                // ns = 1: base = Q ja, a multiple of 8 for Q = 8 (rsl(base + q) = rsl(base) + q)
+                rc2 *vb = v + rsl(base);
 #pragma unroll
-                for (int q = 0; q < Q; ++q) v[rsw(base + q * ns)] = u[gi][q];
+                for (int q = 0; q < Q; ++q) {
+                    if constexpr (Q == 8) vb[q] = u[gi][q];
+                    else v[rsl(base + q)] = u[gi][q];
+                }
             }
         }
     }
@@ -3723,7 +3786,7 @@ __device__ __forceinline__ void rot_pass(double2 *v, const TW &tw, int t, double
 // the full N/2-point FFT: passes of 3 stages (the last one shorter); IN_REG /
 // OUT_REG: the first pass reads z / the last pass leaves its output in z
 template <int N, int LG0 = 0, bool IN_REG = false, bool OUT_REG = false, typename TW>
-__device__ __forceinline__ void rot_fft(double2 *v, const TW &tw, int t, double2 *z = nullptr)
+__device__ __forceinline__ void rot_fft(rc2 *v, const TW &tw, int t, rc2 *z = nullptr)
 {
     constexpr int LG = RotCfg<N>::LG;
     if constexpr (LG0 < LG) {
@@ -3738,18 +3801,25 @@ __device__ __forceinline__ void rot_fft(double2 *v, const TW &tw, int t, double2
 // Z_k, Z_q in one linear map (phase_rotation.py _pair, oracle rot_pair): the
 // real spectrum X_k = E_k + w O_k, the phasors and the inverse's packing
 // composed, Z'_k = A_k Z_k + B_k conj(Z_q), Z'_q = A_q Z_q - conj(B_k) conj(Z_k),
-// with w = exp(-2 pi i k / N) = (c, sn) and the signed phasors pk, pq
-__device__ __forceinline__ void rot_pair(double2 zk, double2 zq, double2 w, double2 pk, double2 pq, double2 &ok,
-                                         double2 &oq)
+// with w = exp(-2 pi i k / N) = (c, sn) and the signed phasors pk, pq.  Returns
+// conj(Z'_k), conj(Z'_q) (what the inverse stores; the imaginary part as (-a) +
+// (-b) of the two terms', the definition's order).  Packed: (h1, h2) = ((1 +
+// sn), (1 - sn)) * 0.5; A_k = (h1 pk.r + h2 pq.r, h1 pk.i - h2 pq.i), A_q
+// likewise; B_k = (pk.i + pq.i, pk.r - pq.r) * (-c/2, c/2) (-(x y) = (-x) y);
+// A Z is rot_cmul; B_k conj(Z_q) = (b.r zq.r + b.i zq.i, b.i zq.r - b.r zq.i);
+// -conj(B_k) conj(Z_k) = (b.i zk.i - b.r zk.r, b.i zk.r + b.r zk.i).
+__device__ __forceinline__ void rot_pair(rc2 zk, rc2 zq, rc2 w, rc2 pk, rc2 pq, rc2 &ok, rc2 &oq)
 {
-    const double h1 = (1.0 + w.y) * 0.5, h2 = (1.0 - w.y) * 0.5, hc = w.x * 0.5;
-    const double akr = h1 * pk.x + h2 * pq.x, aki = h1 * pk.y - h2 * pq.y;
-    const double aqr = h1 * pq.x + h2 * pk.x, aqi = h1 * pq.y - h2 * pk.y;
-    const double bkr = -(hc * (pk.y + pq.y)), bki = hc * (pk.x - pq.x);
-    ok = make_double2((akr * zk.x - aki * zk.y) + (bkr * zq.x + bki * zq.y),
-                      (akr * zk.y + aki * zk.x) + (bki * zq.x - bkr * zq.y));
-    oq = make_double2((aqr * zq.x - aqi * zq.y) + (bki * zk.y - bkr * zk.x),
-                      (aqr * zq.y + aqi * zq.x) + (bki * zk.x + bkr * zk.y));
+    rc2 hh;
+    const rc2 one = {1.0f, 1.0f};
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(hh) : "v"(one), "v"(w));
+    hh = hh * (rc2){0.5f, 0.5f};
+    const rc2 hcv = w.xx * (rc2){-0.5f, 0.5f};
+    const rc2 ak = pk_nhi(hh.xx * pk, hh.yy * pq);
+    const rc2 aq = pk_nhi(hh.xx * pq, hh.yy * pk);
+    const rc2 b = pk_cross(pk, pq) * hcv;
+    ok = pk_addc(rot_cmul(ak, zk), pk_nhi(b * zq.xx, b.yx * zq.yy));
+    oq = pk_addc(rot_cmul(aq, zq), pk_nlo(b.yy * zk.yx, b.xx * zk));
 }
 
 // comprehensive_stats (ic.py:206-212) of the rotated residual row held by one
@@ -3761,21 +3831,22 @@ __device__ __forceinline__ void rot_pair(double2 zk, double2 zq, double2 w, doub
 //   t%8: samples 128(t/8) + t%8 + 8q); the trees are chain_total's;
 // - fftmax: k_diag_cl's first radix-8 stage reads the points t + 64 r of d =
 //   f64(X) - mean, which is exactly the direct layout this lane holds, so the
-//   rFFT starts from registers; the later stages are p2_fft's with its table
-//   (tw_p2, which k_rotate stages in LDS for its own stages), the spectrum's
-//   post twiddles tw[k < M] from the same table's plain part.
-template <int N, typename TW>
-__device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2 *v, const TW &tw, int t,
-                                          double2 (&z)[8], double inv, float w)
+//   rFFT starts from registers; the later stages are p2_fft's with its f64
+//   table (tw_p2, which k_rotate stages in LDS: tw64), the spectrum's post
+//   twiddles tw[k < M] from the same table's plain part.  v: the wave's LDS
+//   work array (M f64 complex points).
+template <int N>
+__device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2 *v, const double2 *tw64, int t,
+                                          rc2 (&z)[8], float inv, float w)
 {
     constexpr int M = RotCfg<N>::M, H = M / 2, TB = RotCfg<N>::TB, L = TB;
     static_assert(N == 1024 && TB == 64 && CLay<N>::L == 64, "one wave per profile, 16 samples per lane");
-    static_assert(RotCfg<N>::TW_LDS, "the statistics FFT reads k_diag's table from the rotation's LDS copy (tw.t)");
+    static_assert(RotCfg<N>::TW_LDS, "the statistics FFT reads k_diag's table from the rotation's LDS copy (tw64)");
     float xr[16];   // sample 2(t + 64 q) + e at xr[2q + e]
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        xr[2 * q] = (float)(z[q].x * inv);
-        xr[2 * q + 1] = (float)((-z[q].y) * inv);
+        xr[2 * q] = z[q].x * inv;
+        xr[2 * q + 1] = (-z[q].y) * inv;
     }
     if (w != 1.0f) {   // fractional weights (w * 1 = w exactly: skipped)
 #pragma unroll
@@ -3843,7 +3914,7 @@ __device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2
             for (int r8 = 0; r8 < 8; ++r8) Cb[A ^ r8] = c8[r8];
         }
         wave_sync();
-        p2_fft<M, L, CLay<N>::LG, 3, 8, M, float, false>(Cb, (const float *)nullptr, 0.0, tw.t, t);
+        p2_fft<M, L, CLay<N>::LG, 3, 8, M, float, false>(Cb, (const float *)nullptr, 0.0, tw64, t);
         // the spectrum in conjugate bin pairs (k_diag_cl's post, 2 X_k)
         constexpr int JF = H / L;
         double best2 = 0.0;
@@ -3863,11 +3934,11 @@ __device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2
             const int kk = t + L * j;
             const double2 zk = Cb[cidx(t) + L * j];
             const double2 zm = Cb[kk == 0 ? 0 : cidx(L - t) + (M - L * (j + 1))];
-            post(zk, zm, tw.post((unsigned)kk));
+            post(zk, zm, tw64[kk]);
         }
         {
             // the self-paired bin k = M/2 (k_diag_cl)
-            const double2 zc = Cb[cidx(H)], wv = tw.post((unsigned)H);
+            const double2 zc = Cb[cidx(H)], wv = tw64[H];
             const double er = zc.x + zc.x, orr = zc.y + zc.y;
             const double tr = orr * wv.x, ti = orr * wv.y;
             const double re = er + tr, rm = er - tr, q2 = ti * ti;
@@ -3903,7 +3974,8 @@ __device__ __forceinline__ void rot_stats(const RotateArgs &a, size_t p, double2
 // diagnostics kernel's).  R never goes to HBM: the residual's 4N write and the
 // statistics pass's 4N read are gone, and so is the R buffer.
 template <int N, bool PP, bool ST = false>
-// 3 waves per SIMD at N <= 1024 (4 spilled 21 VGPRs; 3, 154 VGPRs: C2 fft 57.0 -> 56.4 ms)
+// 3 waves per SIMD (137-167 VGPRs at N = 1024; 4 waves spill 2-13 VGPRs without
+// the statistics: C2 fft 40.7 either way, fft_pp 40.9 -> 41.3 ms)
 __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) void k_rotate(RotateArgs a)
 {
     using C = RotCfg<N>;
@@ -3915,23 +3987,33 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
     // stores the last pass's registers, which are the same points; two LDS round
     // trips per profile fewer
     constexpr bool DIRECT = C::LG % 3 == 0 && (M >> 3) == TB;
-    __shared__ double2 vv[WPB][rot_lds_slots<M>()];
-    __shared__ double2 tws[C::TW_LDS ? 2 * M : 1];
+    // the wave's points (rot_slots f32 pairs); with the statistics the same
+    // array holds their f64 FFT's M complex points
+    constexpr int VS = ST ? 2 * M : rot_slots<M>();
+    static_assert(rot_slots<M>() <= VS, "the rotation's slots fit");
+    __shared__ __attribute__((aligned(16))) rc2 vv[WPB][VS];
+    constexpr int TWE = p2_tw_entries(N);   // k_diag_p2's table: M plain + the stage tables
+    // the twiddle table: f32 for the rotation, or f64 when the statistics FFT
+    // needs it (the rotation then rounds each entry at its use)
+    __shared__ rc2 tws32[C::TW_LDS && !ST ? TWE : 1];
+    __shared__ double2 tws64[C::TW_LDS && ST ? TWE : 1];
     const int t = threadIdx.x % TB, wv = threadIdx.x / TB;
-    double2 *v = vv[wv];
+    rc2 *v = vv[wv];
     const unsigned nsub = (unsigned)a.nsub, nchan = (unsigned)a.nchan;
     const size_t P = (size_t)nsub * nchan;
-    const double sg = a.sign > 0 ? 1.0 : -1.0;
-    const double inv = 1.0 / (double)M;
-    constexpr int TWE = p2_tw_entries(N);   // k_diag_p2's table: M plain + the stage tables
-    static_assert(TWE <= 2 * M, "the staged table fits tws");
-    const __amdgpu_buffer_rsrc_t twr = rot_rsrc(a.tw_p2, TWE);
+    const float sg = a.sign > 0 ? 1.0f : -1.0f;
+    const float inv = (float)(1.0 / (double)M);
+    const __amdgpu_buffer_rsrc_t twr = rot_rsrc(a.tw_p2, 16u * TWE);
     const auto tw = [&]() {
-        if constexpr (C::TW_LDS) return TwLds<N>{tws};
-        else return TwGlobal<N>{twr};
+        if constexpr (!C::TW_LDS) return TwGlobal<N>{twr};
+        else if constexpr (ST) return TwLds64<N>{tws64};
+        else return TwLds32<N>{tws32};
     }();
     if constexpr (C::TW_LDS) {
-        for (int i = threadIdx.x; i < TWE; i += TB * WPB) tws[i] = a.tw_p2[i];
+        for (int i = threadIdx.x; i < TWE; i += TB * WPB) {
+            if constexpr (ST) tws64[i] = a.tw_p2[i];
+            else tws32[i] = rc2_of(a.tw_p2[i]);
+        }
         __syncthreads();
     }
     // every global load of a profile in flight at once: one memory latency
@@ -3970,7 +4052,9 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
             p = (size_t)s * nchan + c;
         }
         if (skip(p, s)) continue;
-        const __amdgpu_buffer_rsrc_t phr = rot_rsrc(PP ? a.tw : a.ph + (size_t)c * (M + 1), M + 1);
+        // the channel's f32 phasor row (8 bytes per harmonic)
+        const __amdgpu_buffer_rsrc_t phr = rot_rsrc(PP ? (const void *)a.tw : (const void *)(a.ph + 2 * (size_t)c * (M + 1)),
+                                                    8u * (M + 1));
         const double dly = PP ? a.delay2[p] : 0.0;
         // PP, N >= 256 (M a multiple of 64): the lane's harmonics k = t + u TB
         // and M - k have the low parts lo1 = t mod 64 and lo2 = -t mod 64 in
@@ -4008,34 +4092,35 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         constexpr bool RM = !PP && H % TB == 0;
         constexpr int NR = RM ? NK - 1 : NK;
         auto kof = [&](int u) { return (RM && u == 0 && t == 0) ? H : t + u * TB; };
-        auto ldph = [&](int u, double2 (&pp)[2]) {
+        // the phasors (f64, ic_phasor) rounded to f32 at the use; the table's are f32
+        auto ldph = [&](int u, rc2 (&pp)[2]) {
             const int k = kof(u);
             if constexpr (PPX) {
                 const double2 b1 = bcast(u), b2 = bcast(NK + u), b3 = bcast(2 * NK + u);
                 if (k <= H) {
-                    pp[0] = lo1 == 0 ? b1 : (w0 + u * TB == 0 ? A1 : ic_phasor_mul(A1, b1));
-                    pp[1] = lo1 == 0 ? b3 : (M - 64 - w0 - u * TB == 0 ? A2 : ic_phasor_mul(A2, b2));
+                    pp[0] = rc2_of(lo1 == 0 ? b1 : (w0 + u * TB == 0 ? A1 : ic_phasor_mul(A1, b1)));
+                    pp[1] = rc2_of(lo1 == 0 ? b3 : (M - 64 - w0 - u * TB == 0 ? A2 : ic_phasor_mul(A2, b2)));
                 }
                 if (RM && u == 0) {   // lane 0's k = H: P0(H) from the round NK - 1 parts
                     const double2 bh = bcast(NK - 1), bh3 = bcast(3 * NK - 1);
                     if (t == 0) {
-                        pp[0] = bh;
-                        pp[1] = bh3;
+                        pp[0] = rc2_of(bh);
+                        pp[1] = rc2_of(bh3);
                     }
                 }
             } else if (k <= H) {
                 if constexpr (PP) {
-                    pp[0] = ic_phasor(k, dly, N);
-                    pp[1] = ic_phasor(M - k, dly, N);
+                    pp[0] = rc2_of(ic_phasor(k, dly, N));
+                    pp[1] = rc2_of(ic_phasor(M - k, dly, N));
                 } else {
-                    pp[0] = rot_ld(phr, 16u * (unsigned)k, 0);
-                    pp[1] = rot_ld(phr, 16u * (unsigned)(M - k), 0);
+                    pp[0] = rot_ld2(phr, 8u * (unsigned)k, 0);
+                    pp[1] = rot_ld2(phr, 8u * (unsigned)(M - k), 0);
                 }
             }
         };
-        double2 phn[2];
+        rc2 phn[2];
         ldph(0, phn);
-        double2 z[8];
+        rc2 z[8];
         static_assert(!ST || DIRECT, "the statistics epilogue needs the direct layout");
         float wst = 1.0f;   // ST: the profile's weight, requested with the rows
         if constexpr (ST) wst = a.w0[p];
@@ -4046,7 +4131,7 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
             for (int q = 0; q < 8; ++q)
                 x2[q] = *(const float2 *)(a.in + d_ofs(k, 2 * (t + TB * q), (int)a.ld_in, a.in_tiled));
             if (a.amp) {
-                const __amdgpu_buffer_rsrc_t t64r = rot_rsrc((const double2 *)a.T64, M);
+                const __amdgpu_buffer_rsrc_t t64r = rot_rsrc(a.T64, 16u * M);
                 double2 tt[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) tt[q] = rot_ld(t64r, 16u * (unsigned)t, 16u * (unsigned)(TB * q));
@@ -4068,12 +4153,12 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
                             r[e] = (float)d;
                         }
                     }
-                    z[q] = make_double2((double)r[0], (double)r[1]);
+                    z[q] = (rc2){r[0], r[1]};
                 }
             } else {
                 const float b = a.base ? a.base[p] : 0.0f;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) z[q] = make_double2((double)(x2[q].x - b), (double)(x2[q].y - b));
+                for (int q = 0; q < 8; ++q) z[q] = (rc2){x2[q].x, x2[q].y} - (rc2){b, b};
             }
             rot_fft<N, 0, true, false>(v, tw, t, z);
         } else {
@@ -4083,7 +4168,7 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
             // the residual of the exact fit (k_residual's arithmetic), formed on the fly;
             // the template is requested with the rows, before the status is known
             // (behind the scattered amp / info loads it was a second latency)
-            const __amdgpu_buffer_rsrc_t t64r = rot_rsrc((const double2 *)a.T64, M);
+            const __amdgpu_buffer_rsrc_t t64r = rot_rsrc(a.T64, 16u * M);
             double2 tt[NJ][2];
 #pragma unroll
             for (int u = 0; u < NJ; ++u) {
@@ -4112,8 +4197,8 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
                         r[e] = (float)d;
                     }
                 }
-                v[rsw(2 * j2)] = make_double2((double)r[0], (double)r[1]);
-                v[rsw(2 * j2 + 1)] = make_double2((double)r[2], (double)r[3]);
+                v[rsl(2 * j2)] = (rc2){r[0], r[1]};
+                v[rsl(2 * j2 + 1)] = (rc2){r[2], r[3]};
             }
         } else {
             const float b = a.base ? a.base[p] : 0.0f;
@@ -4121,9 +4206,8 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
             for (int u = 0; u < NJ; ++u) {
                 const int j2 = t + u * TB;
                 if ((M / 2) % TB != 0 && j2 >= M / 2) break;
-                const float x0 = xin[u].x - b, x1 = xin[u].y - b, x2 = xin[u].z - b, x3 = xin[u].w - b;
-                v[rsw(2 * j2)] = make_double2((double)x0, (double)x1);
-                v[rsw(2 * j2 + 1)] = make_double2((double)x2, (double)x3);
+                v[rsl(2 * j2)] = (rc2){xin[u].x, xin[u].y} - (rc2){b, b};
+                v[rsl(2 * j2 + 1)] = (rc2){xin[u].z, xin[u].w} - (rc2){b, b};
             }
         }
         gsync<TB / 64>();
@@ -4132,52 +4216,55 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         // the post step's twiddles, at their use
         // Re P(M) for the DC / Nyquist step after the rounds (RM); P(0) = (1, 0)
         // exactly for every delay, so Y_0 = X_0 * 1 = X_0
-        double pmr = 0.0;
+        float pmr = 0.0f;
         if constexpr (RM) {
-            if constexpr (PPX) pmr = bcast(2 * NK).x;   // P0(M), lane 2 NK of the wave's high parts
-            else pmr = rot_ld(phr, 16u * (unsigned)M, 0).x;
+            if constexpr (PPX) pmr = (float)bcast(2 * NK).x;   // P0(M), lane 2 NK of the wave's high parts
+            else pmr = rot_ld2(phr, 8u * (unsigned)M, 0).x;
         }
+        const rc2 sgv = {1.0f, sg};
 #pragma unroll
         for (int u = 0; u < NR; ++u) {
             const int k = kof(u);
-            const double2 wk = k <= H ? tw.post((unsigned)(k & (M - 1))) : make_double2(0.0, 0.0);
-            const double2 pk = phn[0], pq = phn[1];
+            const rc2 wk = k <= H ? tw.post((unsigned)(k & (M - 1))) : (rc2){0.0f, 0.0f};
+            const rc2 pk = phn[0], pq = phn[1];
             if (u + 1 < NR) ldph(u + 1, phn);
             if (k <= H) {
                 if (!RM && k == 0) {
-                    const double2 z0 = v[rsw(0)];
-                    const double X0 = z0.x + z0.y, XM = z0.x - z0.y;
-                    const double Y0 = X0 * pk.x, YM = XM * pq.x;
-                    v[rsw(0)] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
+                    const rc2 z0 = v[rsl(0)];
+                    const float X0 = z0.x + z0.y, XM = z0.x - z0.y;
+                    const float Y0 = X0 * pk.x, YM = XM * pq.x;
+                    v[rsl(0)] = (rc2){(Y0 + YM) * 0.5f, -((Y0 - YM) * 0.5f)};
                 } else {
                     const int q = M - k;
-                    const double2 zk = v[rsw(k)], zq = v[rsw(q)];
-                    double2 Zk, Zq;
-                    rot_pair(zk, zq, wk, make_double2(pk.x, sg * pk.y), make_double2(pq.x, sg * pq.y), Zk, Zq);
-                    v[rsw(q)] = make_double2(Zq.x, -Zq.y);
-                    v[rsw(k)] = make_double2(Zk.x, -Zk.y);
+                    const rc2 zk = v[rsl(k)], zq = v[rsl(q)];
+                    rc2 Zk, Zq;   // conjugated
+                    rot_pair(zk, zq, wk, pk * sgv, pq * sgv, Zk, Zq);
+                    v[rsl(q)] = Zq;
+                    v[rsl(k)] = Zk;
                 }
             }
         }
         if constexpr (RM) {
             if (t == 0) {   // DC and Nyquist: X_0 = Z_0.r + Z_0.i, X_M = Z_0.r - Z_0.i
-                const double2 z0 = v[rsw(0)];
-                const double X0 = z0.x + z0.y, XM = z0.x - z0.y;
-                const double Y0 = X0, YM = XM * pmr;
-                v[rsw(0)] = make_double2((Y0 + YM) * 0.5, -((Y0 - YM) * 0.5));
+                const rc2 z0 = v[rsl(0)];
+                const float X0 = z0.x + z0.y, XM = z0.x - z0.y;
+                const float Y0 = X0, YM = XM * pmr;
+                v[rsl(0)] = (rc2){(Y0 + YM) * 0.5f, -((Y0 - YM) * 0.5f)};
             }
         }
         gsync<TB / 64>();
         float *o = a.out + p * (size_t)a.ldo;
+        const rc2 scl = {inv, -inv};   // (r.re / M, -r.im / M): x (-1/M) = -(x) (1/M)
         if constexpr (ST) {
             rot_fft<N, 0, false, true>(v, tw, t, z);
-            rot_stats<N>(a, p, v, tw, t, z, inv, wst);
+            rot_stats<N>(a, p, (double2 *)v, tws64, t, z, inv, wst);
         } else if constexpr (DIRECT) {
             rot_fft<N, 0, false, true>(v, tw, t, z);
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int j = t + TB * q;
-                const float2 y = make_float2((float)(z[q].x * inv), (float)((-z[q].y) * inv));
+                const rc2 yv = z[q] * scl;
+                const float2 y = make_float2(yv.x, yv.y);
                 *(float2 *)(o + 2 * j) = y;
                 if (a.out2) *(float2 *)(a.out2 + d_ofs(p, 2 * j, (int)a.ldo2, a.out2_tiled)) = y;
             }
@@ -4187,9 +4274,8 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
             for (int u = 0; u < NJ; ++u) {
                 const int j2 = t + u * TB;
                 if ((M / 2) % TB != 0 && j2 >= M / 2) break;
-                const double2 r0 = v[rsw(2 * j2)], r1 = v[rsw(2 * j2 + 1)];
-                const float4 y = make_float4((float)(r0.x * inv), (float)((-r0.y) * inv), (float)(r1.x * inv),
-                                             (float)((-r1.y) * inv));
+                const rc2 r0 = v[rsl(2 * j2)] * scl, r1 = v[rsl(2 * j2 + 1)] * scl;
+                const float4 y = make_float4(r0.x, r0.y, r1.x, r1.y);
                 *(float4 *)(o + 4 * j2) = y;
                 if (a.out2) *(float4 *)(a.out2 + d_ofs(p, 4 * j2, (int)a.ldo2, a.out2_tiled)) = y;
             }

@@ -182,7 +182,7 @@ struct Session {
     int dtiled = 0;                  // fit cube D in the tiled layout (dt_ofs)
     float *dr = nullptr, *Tc = nullptr, *R = nullptr, *zbase = nullptr;
     int32_t *zshift = nullptr;
-    double2 *ph = nullptr;
+    float *ph = nullptr;   // f32 pairs
     double *delay2 = nullptr;        // [P] per-profile delays (ic_set_delays2), else nullptr
     // timing
     bool timing = false;
@@ -564,15 +564,20 @@ int scrunch_stage(Session *s)
     return 0;
 }
 
-// phasor table ic_phasor(k, delay[c], nbin), k <= nbin/2 (phase_rotation.py
-// phasors; oracle orc_phasors): the same function the per-profile kernel
-// evaluates on the device, so a table row and a profile with that delay agree
-std::vector<double2> make_phasors(int nbin, int nchan, const double *delay)
+// phasor table f32(ic_phasor(k, delay[c], nbin)), k <= nbin/2, as f32 pairs
+// (phase_rotation.py phasors; oracle orc_phasors; the rotation computes in
+// f32): the same function the per-profile kernel evaluates on the device and
+// rounds, so a table row and a profile with that delay agree
+std::vector<float> make_phasors(int nbin, int nchan, const double *delay)
 {
     const int m = nbin / 2;
-    std::vector<double2> ph((size_t)nchan * (m + 1));
+    std::vector<float> ph(2 * (size_t)nchan * (m + 1));
     for (int c = 0; c < nchan; ++c)
-        for (int k = 0; k <= m; ++k) ph[(size_t)c * (m + 1) + k] = ic_phasor(k, delay[c], nbin);
+        for (int k = 0; k <= m; ++k) {
+            const double2 v = ic_phasor(k, delay[c], nbin);
+            ph[2 * ((size_t)c * (m + 1) + k)] = (float)v.x;
+            ph[2 * ((size_t)c * (m + 1) + k) + 1] = (float)v.y;
+        }
     return ph;
 }
 
@@ -1090,7 +1095,7 @@ int create_session(const ic_params *params, int device, int rank, int world, boo
         // separate pass (run_impl: !rot_stats_on)
         AL(s->zbase, P);
         AL(s->zshift, (size_t)nchan);
-        AL(s->ph, (size_t)nchan * (nbin / 2 + 1));
+        AL(s->ph, 2 * (size_t)nchan * (nbin / 2 + 1));
         if (hipMemset(s->zbase, 0, sizeof(float) * P) != hipSuccess ||
             hipMemset(s->zshift, 0, sizeof(int32_t) * nchan) != hipSuccess)
             return bail(fail(IC_EHIP, "hipMemset(zero levels / shifts) failed"));
@@ -1771,8 +1776,8 @@ int ic_set_delays(void *session, const double *delay_bins)
     for (int c = 0; c < s->nchan; ++c)
         if (!isfinite(delay_bins[c])) return fail(IC_EINVAL, "delay[%d] is not finite", c);
     CK(hipSetDevice(s->device));
-    const std::vector<double2> ph = make_phasors(s->p.nbin, s->nchan, delay_bins);
-    CK(hipMemcpyAsync(s->ph, ph.data(), sizeof(double2) * ph.size(), hipMemcpyHostToDevice, s->stream));
+    const std::vector<float> ph = make_phasors(s->p.nbin, s->nchan, delay_bins);
+    CK(hipMemcpyAsync(s->ph, ph.data(), sizeof(float) * ph.size(), hipMemcpyHostToDevice, s->stream));
     CK(hipStreamSynchronize(s->stream));
     if (s->delay2) {
         CK(hipFree(s->delay2));
@@ -1825,7 +1830,7 @@ int rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, 
     if (device < 0 || device >= ndev) return fail(IC_EINVAL, "device %d out of range (%d devices)", device, ndev);
     CK(hipSetDevice(device));
     const size_t N = (size_t)nsub * nchan * nbin;
-    const std::vector<double2> ph = per_profile ? std::vector<double2>(1) : make_phasors(nbin, nchan, delay_bins);
+    const std::vector<float> ph = per_profile ? std::vector<float>(2) : make_phasors(nbin, nchan, delay_bins);
     std::vector<double2> tw(nbin);
     for (int q = 0; q < nbin; ++q) {
         const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)q / (long double)nbin;
@@ -1833,7 +1838,8 @@ int rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, 
     }
     const std::vector<double2> tw2 = p2_twiddles(nbin);   // the rotation's stage tables
     float *d = nullptr;
-    double2 *dph = nullptr, *dtw = nullptr, *dtw2 = nullptr;
+    float *dph = nullptr;
+    double2 *dtw = nullptr, *dtw2 = nullptr;
     double *ddl = nullptr;
     hipStream_t st = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
@@ -1841,10 +1847,10 @@ int rotate_profiles(int device, int nsub, int nchan, int nbin, const float *in, 
     if (e == hipSuccess && per_profile) e = hipMalloc((void **)&ddl, sizeof(double) * nd);
     if (e == hipSuccess && per_profile)
         e = hipMemcpyAsync(ddl, delay_bins, sizeof(double) * nd, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMalloc((void **)&dph, sizeof(double2) * ph.size());
+    if (e == hipSuccess) e = hipMalloc((void **)&dph, sizeof(float) * ph.size());
     if (e == hipSuccess) e = hipMalloc((void **)&dtw, sizeof(double2) * tw.size());
     if (e == hipSuccess) e = hipMemcpyAsync(d, in, sizeof(float) * N, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(dph, ph.data(), sizeof(double2) * ph.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(dph, ph.data(), sizeof(float) * ph.size(), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(dtw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMalloc((void **)&dtw2, sizeof(double2) * tw2.size());
     if (e == hipSuccess) e = hipMemcpyAsync(dtw2, tw2.data(), sizeof(double2) * tw2.size(), hipMemcpyHostToDevice, st);

@@ -9,16 +9,15 @@ reference calls it through ``dedisperse()`` / ``dededisperse()``
 parity is unpinned; this module DEFINES the stand-in's rotation so that the
 GPU kernel (k_rotate, ic_kernels.hip), the C restatement the tests check
 against (orc_rotate in the oracle/ directory) and this numpy version agree bit for
-bit.  It equals numpy's
-``irfft(rfft(x) * exp(2j pi k s / N))`` to within one f32 ulp (see
-oracle/restated.py fft_phase_shift and tests/test_phase_rotation.py).
+bit.
 
 Definition, for a profile x of N = 2M samples (N a power of two) and a delay
 of s bins (``y[j] = x[j + s]`` for integer s; ``dedisperse`` rotates by +s,
-``dededisperse`` by -s):
+``dededisperse`` by -s).  The arithmetic is IEEE single precision, as psrchive's
+(its FTransform runs FFTW's single-precision plans on the f32 amplitudes):
 
 1. x' = f32(x - base) (base 0 when no baseline is subtracted), then
-   z[j] = (f64(x'[2j]), f64(x'[2j+1])), j < M.
+   z[j] = (x'[2j], x'[2j+1]), j < M.
 2. Z = FFT_M(z): Stockham autosort, stages of radix R = 8 while three or
    more of the log2 M levels remain, then one of radix 4 or 2; Ns = the
    product of the earlier radices.  Butterfly j < M/R: k = j mod Ns,
@@ -29,26 +28,36 @@ of s bins (``y[j] = x[j + s]`` for integer s; ``dedisperse`` rotates by +s,
    c2 = b1 + b3, c3 = -i (b1 - b3) = (d.i, -d.r); y0 = c0 + c2, y1 = c1 + c3,
    y2 = c0 - c2, y3 = c1 - c3.  DFT_8: c_q = b_q + b_(q+4), c_(q+4) = b_q -
    b_(q+4) (q < 4); c5 = ((c5.r + c5.i) s, (c5.i - c5.r) s), c6 = (c6.i, -c6.r),
-   c7 = ((c7.i - c7.r) s, -((c7.r + c7.i) s)) with s = f64(sqrt(2)/2); the
+   c7 = ((c7.i - c7.r) s, -((c7.r + c7.i) s)) with s = f32(f64(sqrt(2)/2)); the
    even outputs y_(2p) = DFT_4(c0..c3)_p, the odd y_(2p+1) = DFT_4(c4..c7)_p.
-   (Round 6; rounds 2-5 ran radix-2 stages, 10 operations per butterfly
-   against 98 per radix-8 butterfly of 8 points, 56 in the first stage.)
 3. For k = 1 .. M/2, q = M - k: the half-length spectrum of the inverse from
    Z_k, Z_q in one linear map (:func:`_pair`: the real spectrum, the phasors
-   (P.r, sign * P.i) and the inverse's packing composed; round 6), stored
-   conjugated (k = M/2 pairs with itself: the k values are stored last).
+   (P.r, sign * P.i) and the inverse's packing composed), stored conjugated,
+   the conjugate's imaginary part as (-a) + (-b) of the two terms' imaginary
+   parts (k = M/2 pairs with itself: the k values are stored last).
    DC and Nyquist: X_0 = Z_0.r + Z_0.i, X_M = Z_0.r - Z_0.i (real),
    Y_0 = X_0 P_0.r, Y_M = X_M P_M.r, stored (Y_0 + Y_M)/2, -((Y_0 - Y_M)/2).
-4. r = FFT_M(stored) (same stages); out[2j] = f32(r[j].r * (1/M)),
-   out[2j+1] = f32((-r[j].i) * (1/M)).
+4. r = FFT_M(stored) (same stages); out[2j] = r[j].r * (1/M),
+   out[2j+1] = (-r[j].i) * (1/M).
 
-Every step is a single IEEE f64 operation in the written order (no fused
+Every step is a single IEEE f32 operation in the written order (no fused
 multiply-add).  Tables: tw[q] = exp(-2 pi i q / N), evaluated in x87 long
-double (cosl/sinl) and rounded to f64, and the phasors P[k] = exp(+2 pi i k s / N)
-of a delay s, evaluated by the f64 formula of :func:`phasors` (the GPU's
-ic_phasor, ic_internal.h), so that the library's per-channel table and its
-per-profile evaluation (psrchive's per-Integration folding period: one delay
-per subint and channel) give the same bits.
+double (cosl/sinl), rounded to f64 (:func:`twiddles`, the table k_diag's FFT
+shares) and then to f32; the phasors P[k] = exp(+2 pi i k s / N) of a delay s,
+evaluated by the f64 formula of :func:`phasors` (the GPU's ic_phasor,
+ic_internal.h) and rounded to f32, so that the library's per-channel table and
+its per-profile evaluation (psrchive's per-Integration folding period: one
+delay per subint and channel) give the same bits.
+
+History: rounds 2-5 ran radix-2 stages in f64; round 6 redefined the stages
+as radix 8 (98 operations per 8 points instead of 120), the pair step as one
+linear map, and then the arithmetic as f32, which is psrchive's own
+precision and lets k_rotate run every complex operation as packed f32 pairs
+(v_pk_add_f32 / v_pk_mul_f32: half the f64 instruction count) with half the
+LDS traffic.  The result is within a few f32 ulps of the profile's largest
+sample of numpy's f64 ``irfft(rfft(x) * exp(2j pi k s / N))`` (oracle/restated.py
+fft_phase_shift, tests/test_phase_rotation.py), as psrchive's FFTW-f32 rotation
+is.
 """
 from __future__ import annotations
 
@@ -139,7 +148,7 @@ def phasors(nbin: int, delays) -> np.ndarray:
     return np.stack([re, im])
 
 
-S8 = 0.7071067811865476   # sqrt(2)/2 rounded to f64 = Re exp(-i pi/4) of the twiddle table
+S8 = np.float32(0.7071067811865476)   # f32 of f64(sqrt(2)/2) = Re exp(-i pi/4) of the f32 twiddle table
 
 
 def _dft4(ar, ai):
@@ -206,15 +215,19 @@ def _stockham(vr: np.ndarray, vi: np.ndarray, tw: np.ndarray):
 
 
 def _pair(zkr, zki, zqr, zqi, c, sn, pkr, pki, pqr, pqi):
-    """The half-length inputs of the inverse, Z'_k and Z'_q (q = M - k), from
-    the transform's Z_k, Z_q in one linear map: with w = exp(-2 pi i k / N) =
-    (c, sn) and the phasors P_k, P_q (their imaginary parts signed for the
-    direction), the real spectrum X_k = E_k + w O_k, Y = P X and the inverse's
-    packing Z' = E' + i conj(w) H' compose to
+    """The half-length inputs of the inverse, conjugated (what it stores):
+    conj(Z'_k) and conj(Z'_q) (q = M - k), from the transform's Z_k, Z_q in one
+    linear map: with w = exp(-2 pi i k / N) = (c, sn) and the phasors P_k, P_q
+    (their imaginary parts signed for the direction), the real spectrum
+    X_k = E_k + w O_k, Y = P X and the inverse's packing Z' = E' + i conj(w) H'
+    compose to
         Z'_k = A_k Z_k + B_k conj(Z_q),  Z'_q = A_q Z_q - conj(B_k) conj(Z_k),
         A_k = ((1 + sn) P_k + (1 - sn) conj(P_q)) / 2,
         A_q = ((1 + sn) P_q + (1 - sn) conj(P_k)) / 2,
-        B_k = i c (P_k - conj(P_q)) / 2."""
+        B_k = i c (P_k - conj(P_q)) / 2.
+    Each Z' is the sum of its two terms; its conjugate's imaginary part is the
+    sum of the two terms' negated imaginary parts ((-a) + (-b), which differs
+    from -(a + b) only in the sign of a zero sum)."""
     h1 = (1.0 + sn) * 0.5
     h2 = (1.0 - sn) * 0.5
     hc = c * 0.5
@@ -225,9 +238,9 @@ def _pair(zkr, zki, zqr, zqi, c, sn, pkr, pki, pqr, pqi):
     bkr = -(hc * (pki + pqi))
     bki = hc * (pkr - pqr)
     return ((akr * zkr - aki * zki) + (bkr * zqr + bki * zqi),
-            (akr * zki + aki * zkr) + (bki * zqr - bkr * zqi),
+            (-(akr * zki + aki * zkr)) + (-(bki * zqr - bkr * zqi)),
             (aqr * zqr - aqi * zqi) + (bki * zki - bkr * zkr),
-            (aqr * zqi + aqi * zqr) + (bki * zkr + bkr * zki))
+            (-(aqr * zqi + aqi * zqr)) + (-(bki * zkr + bkr * zki)))
 
 
 def rotate(x: np.ndarray, ph: np.ndarray, sign: int, tw: np.ndarray | None = None,
@@ -244,6 +257,7 @@ def rotate(x: np.ndarray, ph: np.ndarray, sign: int, tw: np.ndarray | None = Non
         raise ValueError("fractional dedispersion needs a power-of-two nbin (got %d)" % n)
     if tw is None:
         tw = twiddles(n)
+    tw = np.asarray(tw, dtype=np.float64).astype(np.float32)   # f32 of the f64 table
     with np.errstate(invalid="ignore", over="ignore"):   # NaN / Inf samples propagate
         return _rotate(x, ph, sign, tw, base)
 
@@ -253,11 +267,11 @@ def _rotate(x, ph, sign, tw, base):
     if base is not None:
         x = (x - np.asarray(base, dtype=np.float32)[..., None]).astype(np.float32)
     m = n // 2
-    vr = x[..., 0::2].astype(np.float64)
-    vi = x[..., 1::2].astype(np.float64)
+    vr = np.ascontiguousarray(x[..., 0::2])
+    vi = np.ascontiguousarray(x[..., 1::2])
     vr, vi = _stockham(vr, vi, tw)
-    pr = ph[0]
-    pi = ph[1] if sign > 0 else -ph[1]
+    pr = np.asarray(ph[0]).astype(np.float32)
+    pi = np.asarray(ph[1] if sign > 0 else -ph[1]).astype(np.float32)
     k = np.arange(1, m // 2 + 1)
     q = m - k
     zkr, zki, zqr, zqi = vr[..., k], vi[..., k], vr[..., q], vi[..., q]
@@ -271,13 +285,15 @@ def _rotate(x, ph, sign, tw, base):
     ui = np.empty_like(vi)
     ur[..., 0] = (y0 + ym) * 0.5
     ui[..., 0] = -((y0 - ym) * 0.5)
-    ur[..., q] = zqr2
-    ui[..., q] = -zqi2
+    ur[..., q] = zqr2      # conj(Z'_q), conj(Z'_k) (_pair)
+    ui[..., q] = zqi2
     ur[..., k] = zkr2      # k = M/2 pairs with itself: the k values are stored last
-    ui[..., k] = -zki2
+    ui[..., k] = zki2
     rr, ri = _stockham(ur, ui, tw)
-    inv = 1.0 / m
+    inv = np.float32(1.0 / m)
     out = np.empty(x.shape, dtype=np.float32)
-    out[..., 0::2] = (rr * inv).astype(np.float32)
-    out[..., 1::2] = ((-ri) * inv).astype(np.float32)
+    out[..., 0::2] = rr * inv
+    out[..., 1::2] = (-ri) * inv
+    for a in (vr, vi, ur, ui, rr, ri):
+        assert a.dtype == np.float32   # every operation of the definition is f32
     return out

@@ -580,33 +580,33 @@ void orc_phasors(int n, int nchan, const double *delay, double *ph)
         for (int k = 0; k <= m; ++k) orc_phasor(k, delay[c], n, ph + ((size_t)c * (m + 1) + k) * 2);
 }
 
-/* FFT of m complex points (re/im interleaved) through `tmp`: Stockham stages of
- * radix 8 while three or more of the log2 m levels remain, then one of radix 4
- * or 2 (phase_rotation.py _stockham, the GPU's rot_pass).  Stage (R, ns),
- * butterfly j < m/R: k = j mod ns, a_q = v[j + q m/R]; for ns > 1, b_q = a_q
- * times tw[q k n/(R ns)] (q >= 1); y = DFT_R(b) in the written order below;
- * out[(j - k) R + k + p ns] = y_p. */
-#define ROT_S8 0x1.6a09e667f3bcdp-1   /* f64(sqrt(2)/2) = Re exp(-i pi/4) */
-static void dft4(double *r, double *i)   /* in place, 4 points */
+/* FFT of m complex points (re/im interleaved) through `tmp`, in IEEE f32 (psrchive's
+ * precision): Stockham stages of radix 8 while three or more of the log2 m levels
+ * remain, then one of radix 4 or 2 (phase_rotation.py _stockham, the GPU's
+ * rot_pass).  Stage (R, ns), butterfly j < m/R: k = j mod ns, a_q = v[j + q m/R];
+ * for ns > 1, b_q = a_q times tw[q k n/(R ns)] (q >= 1); y = DFT_R(b) in the
+ * written order below; out[(j - k) R + k + p ns] = y_p.  tw: the f32 table. */
+#define ROT_S8 ((float)0x1.6a09e667f3bcdp-1)   /* f32(f64(sqrt(2)/2)) = Re exp(-i pi/4) */
+static void dft4(float *r, float *i)   /* in place, 4 points */
 {
-    const double c0r = r[0] + r[2], c0i = i[0] + i[2];
-    const double c1r = r[0] - r[2], c1i = i[0] - i[2];
-    const double c2r = r[1] + r[3], c2i = i[1] + i[3];
-    const double dr = r[1] - r[3], di = i[1] - i[3];
-    const double c3r = di, c3i = -dr;
+    const float c0r = r[0] + r[2], c0i = i[0] + i[2];
+    const float c1r = r[0] - r[2], c1i = i[0] - i[2];
+    const float c2r = r[1] + r[3], c2i = i[1] + i[3];
+    const float dr = r[1] - r[3], di = i[1] - i[3];
+    const float c3r = di, c3i = -dr;
     r[0] = c0r + c2r; i[0] = c0i + c2i;
     r[1] = c1r + c3r; i[1] = c1i + c3i;
     r[2] = c0r - c2r; i[2] = c0i - c2i;
     r[3] = c1r - c3r; i[3] = c1i - c3i;
 }
-static void dft8(double *r, double *i)   /* in place, 8 points, natural output order */
+static void dft8(float *r, float *i)   /* in place, 8 points, natural output order */
 {
-    double cr[8], ci[8];
+    float cr[8], ci[8];
     for (int q = 0; q < 4; ++q) {
         cr[q] = r[q] + r[q + 4]; ci[q] = i[q] + i[q + 4];
         cr[q + 4] = r[q] - r[q + 4]; ci[q + 4] = i[q] - i[q + 4];
     }
-    double t1 = cr[5] + ci[5], t2 = ci[5] - cr[5];
+    float t1 = cr[5] + ci[5], t2 = ci[5] - cr[5];
     cr[5] = t1 * ROT_S8; ci[5] = t2 * ROT_S8;
     t1 = ci[6]; ci[6] = -cr[6]; cr[6] = t1;
     t1 = ci[7] - cr[7]; t2 = cr[7] + ci[7];
@@ -618,7 +618,7 @@ static void dft8(double *r, double *i)   /* in place, 8 points, natural output o
         r[2 * p + 1] = cr[p + 4]; i[2 * p + 1] = ci[p + 4];
     }
 }
-static void stockham(int m, double *v, double *tmp, const double *tw)
+static void stockham(int m, float *v, float *tmp, const float *tw)
 {
     const int n = 2 * m;
     int lg = 0;
@@ -628,13 +628,13 @@ static void stockham(int m, double *v, double *tmp, const double *tw)
         const int g = m / R;
         for (int j = 0; j < g; ++j) {
             const int k = j & (ns - 1);
-            double br[8], bi[8];
+            float br[8], bi[8];
             for (int q = 0; q < R; ++q) {
-                const double ar = v[2 * (j + q * g)], ai = v[2 * (j + q * g) + 1];
+                const float ar = v[2 * (j + q * g)], ai = v[2 * (j + q * g) + 1];
                 if (ns > 1 && q > 0) {
-                    const double *w = tw + 2 * (size_t)(q * k * (n / (R * ns)));
-                    const double p1 = ar * w[0], p2 = ai * w[1];
-                    const double p3 = ar * w[1], p4 = ai * w[0];
+                    const float *w = tw + 2 * (size_t)(q * k * (n / (R * ns)));
+                    const float p1 = ar * w[0], p2 = ai * w[1];
+                    const float p3 = ar * w[1], p4 = ai * w[0];
                     br[q] = p1 - p2;
                     bi[q] = p3 + p4;
                 } else {
@@ -647,8 +647,8 @@ static void stockham(int m, double *v, double *tmp, const double *tw)
             } else if (R == 4) {
                 dft4(br, bi);
             } else {
-                const double y0r = br[0] + br[1], y0i = bi[0] + bi[1];
-                const double y1r = br[0] - br[1], y1i = bi[0] - bi[1];
+                const float y0r = br[0] + br[1], y0i = bi[0] + bi[1];
+                const float y1r = br[0] - br[1], y1i = bi[0] - bi[1];
                 br[0] = y0r; bi[0] = y0i; br[1] = y1r; bi[1] = y1i;
             }
             const int o = (j - k) * R + k;
@@ -657,64 +657,66 @@ static void stockham(int m, double *v, double *tmp, const double *tw)
                 tmp[2 * (o + p * ns) + 1] = bi[p];
             }
         }
-        memcpy(v, tmp, sizeof(double) * 2 * (size_t)m);
+        memcpy(v, tmp, sizeof(float) * 2 * (size_t)m);
         ns *= R;
         done += R == 8 ? 3 : (R == 4 ? 2 : 1);
     }
 }
 
-/* The inverse's half-length inputs Z'_k, Z'_q (q = M - k) from Z_k, Z_q in one
- * linear map (phase_rotation.py _pair): w_k = (c, sn), phasors pk, pq (their
- * imaginary parts signed for the direction). */
-static void rot_pair(const double *zk, const double *zq, double c, double sn, const double *pk, const double *pq,
-                     double *ok, double *oq)
+/* The inverse's half-length inputs conj(Z'_k), conj(Z'_q) (q = M - k), what it
+ * stores, from Z_k, Z_q in one linear map (phase_rotation.py _pair), f32: w_k =
+ * (c, sn), phasors pk, pq (their imaginary parts signed for the direction); the
+ * conjugate's imaginary part is (-a) + (-b) of the two terms'. */
+static void rot_pair(const float *zk, const float *zq, float c, float sn, const float *pk, const float *pq,
+                     float *ok, float *oq)
 {
-    const double h1 = (1.0 + sn) * 0.5, h2 = (1.0 - sn) * 0.5, hc = c * 0.5;
-    const double akr = h1 * pk[0] + h2 * pq[0], aki = h1 * pk[1] - h2 * pq[1];
-    const double aqr = h1 * pq[0] + h2 * pk[0], aqi = h1 * pq[1] - h2 * pk[1];
-    const double bkr = -(hc * (pk[1] + pq[1])), bki = hc * (pk[0] - pq[0]);
+    const float h1 = (1.0f + sn) * 0.5f, h2 = (1.0f - sn) * 0.5f, hc = c * 0.5f;
+    const float akr = h1 * pk[0] + h2 * pq[0], aki = h1 * pk[1] - h2 * pq[1];
+    const float aqr = h1 * pq[0] + h2 * pk[0], aqi = h1 * pq[1] - h2 * pk[1];
+    const float bkr = -(hc * (pk[1] + pq[1])), bki = hc * (pk[0] - pq[0]);
     ok[0] = (akr * zk[0] - aki * zk[1]) + (bkr * zq[0] + bki * zq[1]);
-    ok[1] = (akr * zk[1] + aki * zk[0]) + (bki * zq[0] - bkr * zq[1]);
+    ok[1] = (-(akr * zk[1] + aki * zk[0])) + (-(bki * zq[0] - bkr * zq[1]));
     oq[0] = (aqr * zq[0] - aqi * zq[1]) + (bki * zk[1] - bkr * zk[0]);
-    oq[1] = (aqr * zq[1] + aqi * zq[0]) + (bki * zk[0] + bkr * zk[1]);
+    oq[1] = (-(aqr * zq[1] + aqi * zq[0])) + (-(bki * zk[0] + bkr * zk[1]));
 }
 
-/* One profile: out = rotation of f32(x - b) by the channel phasors p (sign +1:
- * dedisperse, y[j] = x[j + s]; -1: dededisperse).  work: 4n doubles. */
-static void rotate1(int n, const float *x, float b, const double *p, int sign, const double *tw,
-                    double *work, float *out)
+/* One profile: out = rotation of f32(x - b) by the phasors p (f64, rounded to f32
+ * here; sign +1: dedisperse, y[j] = x[j + s]; -1: dededisperse).  tw: the f32
+ * table.  work: 4n floats. */
+static void rotate1(int n, const float *x, float b, const double *p, int sign, const float *tw,
+                    float *work, float *out)
 {
     const int m = n / 2;
-    double *v = work, *tmp = work + 2 * (size_t)m;
+    float *v = work, *tmp = work + 2 * (size_t)m;
     for (int j = 0; j < m; ++j) {
-        const float x0 = x[2 * j] - b, x1 = x[2 * j + 1] - b;
-        v[2 * j] = (double)x0;
-        v[2 * j + 1] = (double)x1;
+        v[2 * j] = x[2 * j] - b;
+        v[2 * j + 1] = x[2 * j + 1] - b;
     }
     stockham(m, v, tmp, tw);
     const double sg = sign > 0 ? 1.0 : -1.0;
     {
-        const double X0 = v[0] + v[1], XM = v[0] - v[1];
-        const double Y0 = X0 * p[0], YM = XM * p[2 * m];
-        v[0] = (Y0 + YM) * 0.5;
-        v[1] = -((Y0 - YM) * 0.5);
+        const float X0 = v[0] + v[1], XM = v[0] - v[1];
+        const float Y0 = X0 * (float)p[0], YM = XM * (float)p[2 * m];
+        v[0] = (Y0 + YM) * 0.5f;
+        v[1] = -((Y0 - YM) * 0.5f);
     }
     for (int k = 1; k <= m / 2; ++k) {
         const int q = m - k;
-        double zk[2] = {v[2 * k], v[2 * k + 1]}, zq[2] = {v[2 * q], v[2 * q + 1]};
-        double Zk[2], Zq[2];
-        const double pk[2] = {p[2 * k], sg * p[2 * k + 1]}, pq[2] = {p[2 * q], sg * p[2 * q + 1]};
+        float zk[2] = {v[2 * k], v[2 * k + 1]}, zq[2] = {v[2 * q], v[2 * q + 1]};
+        float Zk[2], Zq[2];
+        const float pk[2] = {(float)p[2 * k], (float)(sg * p[2 * k + 1])};
+        const float pq[2] = {(float)p[2 * q], (float)(sg * p[2 * q + 1])};
         rot_pair(zk, zq, tw[2 * k], tw[2 * k + 1], pk, pq, Zk, Zq);
-        v[2 * q] = Zq[0];
-        v[2 * q + 1] = -Zq[1];
+        v[2 * q] = Zq[0];   /* conjugated by rot_pair */
+        v[2 * q + 1] = Zq[1];
         v[2 * k] = Zk[0];   /* k = M/2 pairs with itself: k's values last */
-        v[2 * k + 1] = -Zk[1];
+        v[2 * k + 1] = Zk[1];
     }
     stockham(m, v, tmp, tw);
-    const double inv = 1.0 / (double)m;
+    const float inv = (float)(1.0 / (double)m);
     for (int j = 0; j < m; ++j) {
-        out[2 * j] = (float)(v[2 * j] * inv);
-        out[2 * j + 1] = (float)((-v[2 * j + 1]) * inv);
+        out[2 * j] = v[2 * j] * inv;
+        out[2 * j + 1] = (-v[2 * j + 1]) * inv;
     }
 }
 
@@ -736,13 +738,16 @@ void orc_rotate_ex(int nsub, int nchan, int n, const float *in, const float *bas
         }
         return;
     }
-    double *tw = (double *)malloc(sizeof(double) * 2 * (size_t)n);
+    double *tw64 = (double *)malloc(sizeof(double) * 2 * (size_t)n);
+    float *tw = (float *)malloc(sizeof(float) * 2 * (size_t)n);
     double *ph = (double *)malloc(sizeof(double) * 2 * (per_profile ? P : (size_t)nchan) * (m + 1));
-    orc_twiddles(n, tw);
+    orc_twiddles(n, tw64);
+    for (int q = 0; q < 2 * n; ++q) tw[q] = (float)tw64[q];
+    free(tw64);
     orc_phasors(n, per_profile ? (int)P : nchan, delay, ph);
 #pragma omp parallel
     {
-    double *work = (double *)malloc(sizeof(double) * 4 * (size_t)n);
+    float *work = (float *)malloc(sizeof(float) * 4 * (size_t)n);
 #pragma omp for schedule(dynamic, 64)
     for (long k = 0; k < (long)P; ++k) {
         const size_t row = per_profile ? (size_t)k : (size_t)(k % nchan);

@@ -208,8 +208,9 @@ def fft_phase_shift(x: np.ndarray, delay, sign: int = 1) -> np.ndarray:
     f32.  x (..., nchan, N) f32, delay (nchan,) bins; sign +1 dedisperses
     (y[j] = x[j + s]), -1 dededisperses.  The stand-in's written-order
     rotation (iterative_cleaner_amd/phase_rotation.py, orc_rotate, k_rotate)
-    agrees with this to within one f32 ulp; real psrchive (FFTW in f32) is not
-    available, so that parity is UNPINNED."""
+    computes in f32, as psrchive does, and agrees with this to within 4 f32
+    epsilons of the profile's largest |sample|; real psrchive (FFTW in f32) is
+    not available, so that parity is UNPINNED."""
     x = np.asarray(x, dtype=np.float32)
     n = x.shape[-1]
     k = np.arange(n // 2 + 1)
