@@ -3620,11 +3620,13 @@ __device__ __forceinline__ rc2 rot_ld2(__amdgpu_buffer_rsrc_t r, unsigned voff, 
 // R and span ns, the entries w^(q k), w = exp(-2 pi i / (R ns)), as [k][q - 1]
 // at M + ns - 8: the spans are 8, 64, 512, so the earlier tables fill ns - 8
 // slots), the same long-double values rounded to f64; the rotation uses them
-// rounded to f32.  Staged in LDS as f32 (TwLds32), or read as f64 and rounded
-// at the use: from the f64 LDS copy the residual's statistics FFT needs
-// (TwLds64), or through L1/L2 (TwGlobal, one-block profiles N >= 2048).
+// rounded to f32.  Staged in LDS as f32 (TwLds32; with the statistics, whose
+// FFT needs the f64 table in LDS too, the f32 stage tables only: TwLdsSt), or
+// read as f64 through L1/L2 and rounded at the use (TwGlobal, one-block
+// profiles N >= 2048).
 template <int N>
 struct TwGlobal {
+    static constexpr bool ASM_ROWS = false;
     __amdgpu_buffer_rsrc_t r;
     template <int NS, int R>
     __device__ __forceinline__ rc2 stage(unsigned k, int q) const
@@ -3635,21 +3637,39 @@ struct TwGlobal {
 };
 template <int N>
 struct TwLds32 {
+    static constexpr bool ASM_ROWS = true;   // rot_pass reads the stage rows with ds_read_b64
     const rc2 *t;
     template <int NS, int R>
     __device__ __forceinline__ rc2 stage(unsigned k, int q) const
     {
         return t[N / 2 + NS - 8 + q - 1 + k * (R - 1)];
     }
+    // LDS byte address of entry [k][0] of the stage table of span NS
+    template <int NS, int R>
+    __device__ __forceinline__ uint32_t row(unsigned k) const
+    {
+        return lds_u32(t + (N / 2 + NS - 8 + k * (R - 1)));
+    }
     __device__ __forceinline__ rc2 post(unsigned i) const { return t[i]; }
 };
+// with the statistics: the f32 stage tables alone (s: the entries from M on)
+// beside the f64 table the statistics FFT reads, whose plain part serves the
+// post step (rounded at the use); 53 KB of LDS per four-wave block, three
+// blocks per CU
 template <int N>
-struct TwLds64 {
+struct TwLdsSt {
+    static constexpr bool ASM_ROWS = true;
+    const rc2 *s;
     const double2 *t;
     template <int NS, int R>
     __device__ __forceinline__ rc2 stage(unsigned k, int q) const
     {
-        return rc2_of(t[N / 2 + NS - 8 + q - 1 + k * (R - 1)]);
+        return s[NS - 8 + q - 1 + k * (R - 1)];
+    }
+    template <int NS, int R>
+    __device__ __forceinline__ uint32_t row(unsigned k) const
+    {
+        return lds_u32(s + (NS - 8 + k * (R - 1)));
     }
     __device__ __forceinline__ rc2 post(unsigned i) const { return rc2_of(t[i]); }
 };
@@ -3719,8 +3739,43 @@ __device__ __forceinline__ void rot_pass(rc2 *v, const TW &tw, int t, rc2 *z = n
     rc2 u[GPT][Q];
     // the stage's twiddles first (their latency overlaps the LDS reads and the barrier)
     rc2 w[GPT][Q - 1];
+    // one-group-per-lane passes read their points (and the f32 twiddle rows)
+    // as separate ds_read_b64 in asm: the compiler pairs adjacent 8-byte LDS
+    // loads into ds_read2_b64, which serves 16-lane groups on 32 banks at 4x
+    // the LDS cycles per byte (MI355X_MICROARCH.md); one lgkmcnt wait ties
+    // the values
+    constexpr bool ASM = GPT == 1 && G == TB && G % 8 == 0 && !IN_REG;
+    if constexpr (ASM) {
+        const int ja = t, k = ja & (ns - 1);
+        if constexpr (ns > 1 && TW::ASM_ROWS) {
+            const uint32_t wa = tw.template row<ns, Q>((unsigned)k);
 #pragma unroll
-    for (int gi = 0; gi < GPT; ++gi) {
+            for (int q = 1; q < Q; ++q)
+                asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(w[0][q - 1]) : "v"(wa), "i"(8 * (q - 1)));
+        } else if constexpr (ns > 1) {
+#pragma unroll
+            for (int q = 1; q < Q; ++q) w[0][q - 1] = tw.template stage<ns, Q>((unsigned)k, q);
+        }
+        const uint32_t va = lds_u32(v + rsl(ja));   // rsl(ja + q G) = rsl(ja) + q (G + G/8)
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(u[0][q]) : "v"(va), "i"(8 * q * (G + G / 8)));
+        if constexpr (Q == 8) {
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(u[0][0]), "+v"(u[0][1]), "+v"(u[0][2]), "+v"(u[0][3]), "+v"(u[0][4]), "+v"(u[0][5]),
+                           "+v"(u[0][6]), "+v"(u[0][7]));
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < Q; ++q) asm volatile("" : "+v"(u[0][q]));
+        }
+        if constexpr (ns > 1 && TW::ASM_ROWS) {
+#pragma unroll
+            for (int q = 0; q < Q - 1; ++q) asm volatile("" : "+v"(w[0][q]));
+        }
+    }
+#pragma unroll
+    for (int gi = 0; gi < GPT && !ASM; ++gi) {
         const int ja = t + TB * gi;
         const int k = ja & (ns - 1);
         if (G % TB == 0 || ja < G) {
@@ -3995,7 +4050,7 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
     constexpr int TWE = p2_tw_entries(N);   // k_diag_p2's table: M plain + the stage tables
     // the twiddle table: f32 for the rotation, or f64 when the statistics FFT
     // needs it (the rotation then rounds each entry at its use)
-    __shared__ rc2 tws32[C::TW_LDS && !ST ? TWE : 1];
+    __shared__ rc2 tws32[C::TW_LDS ? (ST ? TWE - M : TWE) : 1];
     __shared__ double2 tws64[C::TW_LDS && ST ? TWE : 1];
     const int t = threadIdx.x % TB, wv = threadIdx.x / TB;
     rc2 *v = vv[wv];
@@ -4006,13 +4061,17 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
     const __amdgpu_buffer_rsrc_t twr = rot_rsrc(a.tw_p2, 16u * TWE);
     const auto tw = [&]() {
         if constexpr (!C::TW_LDS) return TwGlobal<N>{twr};
-        else if constexpr (ST) return TwLds64<N>{tws64};
+        else if constexpr (ST) return TwLdsSt<N>{tws32, tws64};
         else return TwLds32<N>{tws32};
     }();
     if constexpr (C::TW_LDS) {
         for (int i = threadIdx.x; i < TWE; i += TB * WPB) {
-            if constexpr (ST) tws64[i] = a.tw_p2[i];
-            else tws32[i] = rc2_of(a.tw_p2[i]);
+            if constexpr (ST) {
+                tws64[i] = a.tw_p2[i];
+                if (i >= M) tws32[i - M] = rc2_of(a.tw_p2[i]);
+            } else {
+                tws32[i] = rc2_of(a.tw_p2[i]);
+            }
         }
         __syncthreads();
     }
@@ -4087,9 +4146,9 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         // 0 takes it in round 0 instead of the DC / Nyquist bins, which it
         // finishes after the rounds: no round with one active lane and no
         // divergent branch in round 0 (the schedule only: the same operations).
-        // Not with per-profile delays: the extra high parts it holds spill there
-        // (C2 fft_pp 48.1 -> 48.6 ms; per-channel 46.8 -> 46.4)
-        constexpr bool RM = !PP && H % TB == 0;
+        // Per-channel C2 46.8 -> 46.4 ms (f64 rotation); with per-profile
+        // delays it spilled in f64 (48.1 -> 48.6), in f32 it gains (39.8 -> 39.6)
+        constexpr bool RM = H % TB == 0;
         constexpr int NR = RM ? NK - 1 : NK;
         auto kof = [&](int u) { return (RM && u == 0 && t == 0) ? H : t + u * TB; };
         // the phasors (f64, ic_phasor) rounded to f32 at the use; the table's are f32
