@@ -53,6 +53,24 @@ def test_rotate_profiles_matches_oracle(nbin, oracle_lib):
         assert _same(got, oracle_lib.rotate(x, d, sign)), "sign %d" % sign
 
 
+@pytest.mark.parametrize("nbin", [64, 1024, 4096])
+def test_rotate_profiles_f32_edge_values(nbin, oracle_lib):
+    """The f32 rotation (packed v_pk_* arithmetic, f32 denormals kept) on
+    subnormal, overflowing, signed-zero and spike profiles, per channel and per
+    profile: bit-equal to the C oracle's scalar f32 code (NaNs as NaNs)."""
+    from iterative_cleaner_amd import _native
+    from test_phase_rotation import _edge_cube
+    x = _edge_cube(nbin)
+    rng = np.random.default_rng(nbin + 1)
+    d = rng.uniform(-2 * nbin, 2 * nbin, 6)
+    d[1], d[2] = 0.0, 0.5
+    d2 = rng.uniform(-2 * nbin, 2 * nbin, (4, 6))
+    for delay in (d, d2):
+        for sign in (1, -1):
+            got = _native.rotate_profiles(x, delay, sign)
+            assert _same(got, oracle_lib.rotate(x, delay, sign)), "sign %d, per-profile %s" % (sign, delay.ndim == 2)
+
+
 CASES = [
     # (nsub, nchan, nbin, seed, rfi, extra)
     (7, 300, 64, 11, 0.2, {}),                 # two channel super-blocks

@@ -39,6 +39,44 @@ def test_tables_and_rotation_match_c_oracle(n, oracle_lib):
             assert nan_equal(a, c) and np.array_equal(np.signbit(a) | np.isnan(a), np.signbit(c) | np.isnan(c))
 
 
+def _edge_cube(n, seed=5):
+    """f32 edge values for the f32 rotation: subnormal profiles (their FFT
+    stays subnormal or underflows), profiles whose transform overflows to Inf,
+    signed zeros, a single spike, and ordinary noise."""
+    rng = np.random.default_rng(seed + n)
+    x = (rng.standard_normal((4, 6, n))).astype(np.float32)
+    x[0, 0] *= np.float32(1e-40)                       # subnormal samples
+    x[0, 1] = np.float32(3e-45) * np.sign(x[0, 1])      # the smallest subnormals
+    x[1, 0] *= np.float32(3e37)                        # sums overflow to +-Inf
+    x[1, 1] = np.float32(-0.0)                         # negative zeros
+    x[1, 2, ::2] = np.float32(-0.0)
+    x[1, 2, 1::2] = np.float32(0.0)
+    x[2, 3] = 0.0
+    x[2, 3, n // 3] = np.float32(7.5)                  # one spike
+    x[3, 4] *= np.float32(1e-30)
+    return x
+
+
+@pytest.mark.parametrize("n", [64, 1024])
+def test_rotation_edge_values_match_c_oracle(n, oracle_lib):
+    """numpy's f32 stand-in == the C oracle bit for bit on subnormal, overflowing,
+    signed-zero and spike profiles, per channel and per profile, both signs."""
+    from iterative_cleaner_amd import phase_rotation as pr
+    x = _edge_cube(n)
+    rng = np.random.default_rng(n)
+    d = rng.uniform(-2 * n, 2 * n, 6)
+    d[1], d[2] = 0.0, 0.5
+    d2 = rng.uniform(-2 * n, 2 * n, (4, 6))
+    with np.errstate(over="ignore", invalid="ignore", under="ignore"):
+        for delay in (d, d2):
+            ph = pr.phasors(n, delay)
+            for sign in (1, -1):
+                a = pr.rotate(x, ph, sign)
+                c = oracle_lib.rotate(x, delay, sign)
+                assert nan_equal(a, c) and np.array_equal(np.signbit(a) | np.isnan(a), np.signbit(c) | np.isnan(c))
+    assert np.isinf(a[1, 0]).any() or np.isnan(a[1, 0]).any()   # the overflow case does overflow
+
+
 @pytest.mark.parametrize("n", [4, 64, 256, 1024, 4096])
 def test_rotation_within_f32_error_of_numpy_fft(n, oracle_lib):
     """The f32 transforms' error against numpy's f64 rotation: measured 1.1 (n = 4)
