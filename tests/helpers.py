@@ -111,16 +111,18 @@ def thresholds(z, i):
     return (int(thr[0]) if isint[0] else float(thr[0]), int(thr[1]) if isint[1] else float(thr[1]))
 
 
-def check_whole_loop(oracle_lib, raw, w0, shift, one, max_iter=5, residual=False):
+def check_whole_loop(oracle_lib, raw, w0, shift, one, max_iter=5, residual=False, delay=None):
     """The whole cleaning loop of a full-size archive run independently by the
     (threaded) C oracle, compared with the GPU run `one` (ic_run + ic_get_fit /
     diagnostics / template [/ residual]) profile by profile: the loop count, the
     per-iteration change and zero counts, the final template, every profile's
     leastsq amplitude and status, std / mean / ptp and the weights bit for bit,
     fftmax within 1e-9 relative, and the test values - the oracle's own, from the
-    oracle's diagnostics - within 1e-9 (only fftmax's last bits differ).  The
-    reference: iterative_cleaner.py:83-146 (fit :259-288, statistics :181-226)."""
-    ref = oracle_lib.clean_loop(raw, w0, shift, max_iter=max_iter, want_details=True, want_residual=residual)
+    oracle's diagnostics - within 1e-9 (only fftmax's last bits differ).  delay:
+    the FFT dedispersion mode's fractional delays (orc_rotate).  The reference:
+    iterative_cleaner.py:83-146 (fit :259-288, statistics :181-226)."""
+    ref = oracle_lib.clean_loop(raw, w0, shift, max_iter=max_iter, want_details=True, want_residual=residual,
+                                delay=delay)
     assert one["loops"] == ref["loops"] and one["n_iter"] == len(one["changed"])
     k = one["n_iter"]
     assert np.array_equal(one["changed"], ref["changed"][:k]), "changed weights per loop"
