@@ -4188,7 +4188,12 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
             float2 x2[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                x2[q] = *(const float2 *)(a.in + d_ofs(k, 2 * (t + TB * q), (int)a.ld_in, a.in_tiled));
+            {
+                // read once per rotation (non-temporal: C2 fft 39.25-39.42 -> 39.05-39.25 ms)
+                const rc2 xv =
+                    __builtin_nontemporal_load((const rc2 *)(a.in + d_ofs(k, 2 * (t + TB * q), (int)a.ld_in, a.in_tiled)));
+                x2[q] = make_float2(xv.x, xv.y);
+            }
             if (a.amp) {
                 const __amdgpu_buffer_rsrc_t t64r = rot_rsrc(a.T64, 16u * M);
                 double2 tt[8];
