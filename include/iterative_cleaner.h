@@ -93,11 +93,13 @@ typedef struct {
  *                    (ic_set_delays: delay[c] bins per channel; ic_set_delays2:
  *                    delay[s][c] per profile, psrchive's per-Integration folding
  *                    period): forward real FFT, harmonic k times
- *                    exp(+-2 pi i k delay / nbin), inverse real FFT, in the
- *                    arithmetic order written in iterative_cleaner_amd/
- *                    phase_rotation.py (bit-identical to it and to the C oracle;
- *                    within one f32 ulp of numpy's irfft(rfft(x) * phasor);
- *                    parity with real psrchive unpinned).  nbin must be a power of
+ *                    exp(+-2 pi i k delay / nbin), inverse real FFT, in IEEE
+ *                    f32 (psrchive's precision) and the arithmetic order
+ *                    written in iterative_cleaner_amd/phase_rotation.py
+ *                    (bit-identical to it and to the C oracle; within 4 f32
+ *                    epsilons of the profile's largest |sample| of numpy's f64
+ *                    irfft(rfft(x) * phasor); parity with real psrchive
+ *                    unpinned).  nbin must be a power of
  *                    two in 64..4096 (either fit_mode); the shift arrays of the
  *                    uploads are then unused (pass zeros). */
 #define IC_DEDISP_SHIFT 0
