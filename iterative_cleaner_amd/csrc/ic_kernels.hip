@@ -3537,9 +3537,12 @@ struct RotCfg {
                                                                               : N == 2048 ? 10 : 11;   // log2 M
     static constexpr int TB = M / 8 < 64 ? 64 : (M / 8 > 256 ? 256 : M / 8);
     // one-wave profiles run four to a block, which stages the twiddle table in
-    // LDS once for all four
+    // LDS once for all four; the one-block profiles of N >= 2048 stage it too,
+    // once per block of the grid-stride loop (16 profiles per block at C5:
+    // 62.7-63.1 -> 58.0-58.2 ms per C5 clean in the FFT mode, against f64
+    // entries through L1/L2 rounded at each use)
     static constexpr int WPB = TB == 64 ? 4 : 1;
-    static constexpr bool TW_LDS = WPB > 1;
+    static constexpr bool TW_LDS = true;
 };
 
 // LDS slot of complex point i: one pad slot after every 8 points.  With 8-byte
@@ -4082,7 +4085,12 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
         for (int u = 0; u < NJ; ++u) {
             const int j2 = t + u * TB;
             if ((M / 2) % TB == 0 || j2 < M / 2)
-                xr[u] = *(const float4 *)(a.in + d_ofs(k, 4 * j2, (int)a.ld_in, a.in_tiled));
+            {
+                // non-temporal, as the direct layout's (C5 fft 58.8 -> 57.4-57.9 ms,
+                // C4 fft 3.90 -> 3.76 ms with the stores below)
+                const fv4 xv = __builtin_nontemporal_load((const fv4 *)(a.in + d_ofs(k, 4 * j2, (int)a.ld_in, a.in_tiled)));
+                xr[u] = make_float4(xv.x, xv.y, xv.z, xv.w);
+            }
         }
     };
     // the profile is left out (uniform over the block): its subint's flag is 0,
@@ -4341,8 +4349,9 @@ __global__ __launch_bounds__(RotCfg<N>::TB * RotCfg<N>::WPB, N <= 1024 ? 3 : 2) 
                 if ((M / 2) % TB != 0 && j2 >= M / 2) break;
                 const rc2 r0 = v[rsl(2 * j2)] * scl, r1 = v[rsl(2 * j2 + 1)] * scl;
                 const float4 y = make_float4(r0.x, r0.y, r1.x, r1.y);
-                *(float4 *)(o + 4 * j2) = y;
-                if (a.out2) *(float4 *)(a.out2 + d_ofs(p, 4 * j2, (int)a.ldo2, a.out2_tiled)) = y;
+                const fv4 yv = {y.x, y.y, y.z, y.w};
+                __builtin_nontemporal_store(yv, (fv4 *)(o + 4 * j2));
+                if (a.out2) __builtin_nontemporal_store(yv, (fv4 *)(a.out2 + d_ofs(p, 4 * j2, (int)a.ldo2, a.out2_tiled)));
             }
         }
         gsync<TB / 64>();   // v is reused by the block's next profile
