@@ -75,8 +75,10 @@ typedef struct {
  *                  (MINPACK lmdif, n = 1; iterative_cleaner.py:277-278): the
  *                  reference's arithmetic, zap masks identical to it.
  *   IC_FIT_CLOSED  the closed-form least-squares amplitude
- *                  a = sum_i T_i p_i / sum_i T_i^2 (f64 numpy pairwise sums over
- *                  the dedispersed profile; a = 0 when the template is all zero;
+ *                  a = sum_i T_i p_i / sum_i T_i^2 (f64 numpy pairwise sums; the
+ *                  products T_i p_i of the dedispersed profile summed in the
+ *                  stored, dispersed sample order j = (i + shift) mod nbin
+ *                  since round 6; a = 0 when the template is all zero;
  *                  info = 1, or 5 (residual zeroed) when a is not finite), fused
  *                  with the residual and the diagnostics in one sweep of the raw
  *                  cube: the HBM-bound fast mode of the north star.  It is NOT

@@ -2383,7 +2383,12 @@ __global__ __launch_bounds__(256) void k_diag(DiagArgs a)
                 Pr[i] = row[j] - b;
             }
             wave_sync();
-            const double dot = wave_pairwise<double>(pl, [&](int q) { return T64[q] * (double)Pr[q]; }, scr, lane);
+            // the products in the stored (dispersed) order j: bin i = (j - sh) mod n
+            const double dot = wave_pairwise<double>(pl, [&](int q) {
+                int i = q - sh;
+                if (i < 0) i += n;
+                return T64[i] * (double)Pr[i];
+            }, scr, lane);
             const double TT = *a.TT;
             x = TT != 0.0 ? dot / TT : 0.0;
             stt = isfinite(x) ? 1 : 5;
@@ -2873,6 +2878,7 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
         if (closed) {
             // fit cube row p_i = f32(ded_i - base0), i = (j - sh) mod N: to LDS in
             // the dedispersed order, then a = sum(T*p)/sum(T*T) over the chains
+            // of the stored order (the products T_i p_i of j = i + sh)
             const XWrap<N, TPP> xw((t - sh) & (N - 1));
 #pragma unroll
             for (int u = 0; u < NPT; ++u) X[xw(u)] = (XT)(pv[u] - bk);
@@ -2885,12 +2891,16 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
                 const int base = (ch >> 3) * C::LEAF + (ch & 7);
                 double r = 0.0;
                 if (act) {
-                    // base % 128 < 8 and 8 q < LEAF <= 128
-                    const XT *xb = X + xaddr(base);
-                    r = T[base] * (double)xb[0];
+                    // the chain's stored (dispersed) samples j = base + 8 q pair
+                    // with the dedispersed bins i = (j - sh) mod N
+                    auto term = [&](int j) {
+                        const int i = (j - sh) & (N - 1);
+                        return T[i] * (double)X[xaddr(i)];
+                    };
+                    r = term(base);
 #pragma unroll
                     for (int q = 1; q < C::CL; ++q) {
-                        const double pr = T[base + 8 * q] * (double)xb[8 * q];
+                        const double pr = term(base + 8 * q);
                         r = r + pr;
                     }
                 }
@@ -3133,8 +3143,9 @@ __global__ __launch_bounds__(N >= 2048 ? P2<N>::TPP : 512, p2_min_waves<N>()) vo
 //   lanes x 8 B per half-wave) and the stage-1 gathers (16-B points) are both
 //   bank-conflict free, and all addresses are per-thread bases + immediates.
 // - Profile-uniform conditions (fit status, w0 == 0 / 1) are scalar branches.
-// DIAG_CLOSED first forms the closed-form amplitude over the dedispersed-frame
-// chains (p_i gathered from raw at (i + sh) mod N, k_diag_p2's arithmetic).
+// DIAG_CLOSED first forms the closed-form amplitude over the same chains (the
+// stored order: the products T_i p_i of the lane's samples j, i = (j - sh) mod
+// N, with the template gathered for the residual).
 constexpr int p2_tw_entries(int N)
 {
     const int M = N / 2;
@@ -3302,19 +3313,16 @@ __global__ __launch_bounds__(CLay<N>::L * CLay<N>::GPB, 4) void k_diag_cl(DiagAr
             for (int q = 0; q < 16; ++q) tg[q] = tb[8 * q];
         }
         if constexpr (closed) {
-            // a = sum(T*p)/sum(T*T) over the dedispersed-frame chains i = jb + 8q,
-            // p_i = f32(raw[(i + sh) mod N] - base)
-            const unsigned j0 = (unsigned)(jb + sh);
-            float pi[16];
-            {
-                const float *row = a.raw + (size_t)k * N;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) pi[q] = row[(j0 + 8u * q) & (unsigned)(N - 1)];
-            }
-            double r = a.T64[jb] * (double)(pi[0] - bk);
+            // a = sum(T*p)/sum(T*T) over the chains of the stored (dispersed)
+            // order: the lane's samples j = jb + 8q with p = f32(raw_j - base),
+            // the dedispersed bin i = (j - sh) mod N, T_i = tg[q] (the
+            // residual's gather): no second read of the row (round 6; before,
+            // the dot ran over the dedispersed chains and gathered raw at
+            // (i + sh) mod N again)
+            double r = tg[0] * (double)(pv[0] - bk);
 #pragma unroll
             for (int q = 1; q < 16; ++q) {
-                const double pr = a.T64[jb + 8 * q] * (double)(pi[q] - bk);
+                const double pr = tg[q] * (double)(pv[q] - bk);
                 r = r + pr;
             }
             double cs[1] = {r};

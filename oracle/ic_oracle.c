@@ -815,20 +815,28 @@ double orc_sum_f64(const double *a, int n) { return 0.0 + pw_f64(a, n); }
 /* fit_mode 1 (IC_FIT_CLOSED, include/iterative_cleaner.h): NOT the reference's
  * arithmetic (which is leastsq, iterative_cleaner.py:277-278) but its closed-form
  * least-squares solution, stated in numpy terms as
- *     TT = np.sum(T64 * T64);  a = np.sum(T64 * p64) / TT   (pairwise f64 sums)
- * with a = 0 when TT == 0 and status 1 (5 when a is not finite: residual zeroed,
- * like a failed leastsq, :284-286).  The residual follows :279-283 as in the
- * exact mode.  D: fit cube (P, m), dedispersed. */
+ *     TT = np.sum(T64 * T64);  a = np.sum(np.roll(T64 * p64, sh)) / TT   (pairwise f64 sums)
+ * the products summed in the archive's stored (dispersed) sample order, sample j
+ * pairing with the dedispersed bin (j - sh) mod m (round 6; the dedispersed order
+ * before), with a = 0 when TT == 0 and status 1 (5 when a is not finite: residual
+ * zeroed, like a failed leastsq, :284-286).  The residual follows :279-283 as in
+ * the exact mode.  D: fit cube (P, m), dedispersed; shift: [nchan] channel shifts
+ * of the rows (row k is channel k % nchan), or NULL (0). */
 void orc_fit_closed(int P, int m, const float *T, const float *D,
                     int pr_on, double pr_factor, int pr_start, int pr_end,
-                    double *amp, int32_t *info, float *R)
+                    double *amp, int32_t *info, float *R, const int32_t *shift, int nchan)
 {
     double *prod = (double *)malloc(sizeof(double) * (size_t)m);
     for (int i = 0; i < m; ++i) prod[i] = (double)T[i] * (double)T[i];
     const double TT = orc_sum_f64(prod, m);
     for (int k = 0; k < P; ++k) {
         const float *p = D + (size_t)k * m;
-        for (int i = 0; i < m; ++i) prod[i] = (double)T[i] * (double)p[i];
+        const int sh = shift ? (int)(((shift[k % nchan] % m) + m) % m) : 0;
+        for (int j = 0; j < m; ++j) {
+            int i = j - sh;
+            if (i < 0) i += m;
+            prod[j] = (double)T[i] * (double)p[i];
+        }
         const double dot = orc_sum_f64(prod, m);
         const double x = TT != 0.0 ? dot / TT : 0.0;
         const int st = isfinite(x) ? 1 : 5;
@@ -1327,7 +1335,8 @@ int orc_clean_loop(const orc_params *pp, const float *raw, const float *w0, cons
         }
         if (T_all) memcpy(T_all + (size_t)(x - 1) * n, T, sizeof(float) * (size_t)n);
         if (pp->fit_mode == 1)
-            orc_fit_closed((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
+            orc_fit_closed((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd,
+                           fftded ? NULL : shift, nchan);
         else
             orc_fit_residual((int)P, n, T, D, pp->pr_on, pp->pr_factor, pp->pr_start, pp->pr_end, amp, info, Rd);
         /* dededisperse + apply_weights */

@@ -44,7 +44,7 @@ def lib():
         _lib.orc_fit_residual.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                           C.c_double, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                           C.c_void_p]
-        _lib.orc_fit_closed.argtypes = _lib.orc_fit_residual.argtypes
+        _lib.orc_fit_closed.argtypes = list(_lib.orc_fit_residual.argtypes) + [C.c_void_p, C.c_int]
         _lib.orc_baseline.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_double, C.c_void_p, C.c_void_p]
         _lib.orc_fit_cube.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_double, C.c_void_p]
         _lib.orc_template.argtypes = [C.c_int] * 3 + [C.c_void_p] * 3 + [C.c_double, C.c_void_p]
@@ -90,8 +90,10 @@ def fit_residual(D, T, pr=None):
     return amp, info, R
 
 
-def fit_closed(D, T, pr=None):
-    """fit_mode 1 (closed form): (amp, info, R f32 dedispersed) of the (P, nbin) fit cube."""
+def fit_closed(D, T, pr=None, shift=None):
+    """fit_mode 1 (closed form): (amp, info, R f32 dedispersed) of the (P, nbin) fit
+    cube; shift (nchan,): the rows' channel shifts (row k is channel k % nchan),
+    whose stored order the dot is summed in (None: 0)."""
     D = f32(D).reshape(-1, np.shape(D)[-1])
     T = f32(T)
     P, n = D.shape
@@ -99,7 +101,9 @@ def fit_closed(D, T, pr=None):
     info = np.empty(P, np.int32)
     R = np.empty((P, n), np.float32)
     on, fac, a, b = (0, 1.0, 0, 0) if pr is None else (1, float(pr[0]), int(pr[1]), int(pr[2]))
-    lib().orc_fit_closed(P, n, _p(T), _p(D), on, fac, a, b, _p(amp), _p(info), _p(R))
+    sh = None if shift is None else np.ascontiguousarray(shift, np.int32).reshape(-1)
+    lib().orc_fit_closed(P, n, _p(T), _p(D), on, fac, a, b, _p(amp), _p(info), _p(R), _p(sh),
+                         0 if sh is None else int(sh.size))
     return amp, info, R
 
 

@@ -185,15 +185,25 @@ def weighted_cube(R: np.ndarray, w0: np.ndarray) -> np.ndarray:
 # --------------------------------------------------------------------------
 # fit_mode 1 (IC_FIT_CLOSED): the closed-form amplitude, stated in numpy
 # --------------------------------------------------------------------------
-def closed_form_fit(D: np.ndarray, T: np.ndarray):
-    """a = np.sum(T*p) / np.sum(T*T) per fit-cube row (numpy pairwise f64 sums
-    along the contiguous bin axis); a = 0 for an all-zero template; status 1, or
-    5 (residual zeroed) when a is not finite.  Returns (amp, info, R f32)."""
+def closed_form_fit(D: np.ndarray, T: np.ndarray, shift=None):
+    """a = np.sum(np.roll(T*p, sh)) / np.sum(T*T) per fit-cube row (numpy
+    pairwise f64 sums along the contiguous bin axis): the products of the
+    dedispersed row are summed in the archive's stored (dispersed) sample order,
+    sample j pairing with the dedispersed bin (j - sh) mod nbin, sh the row's
+    channel shift (shift: (nchan,) or None = 0; round 6: the dedispersed order
+    before); a = 0 for an all-zero template; status 1, or 5 (residual zeroed)
+    when a is not finite.  Returns (amp, info, R f32)."""
     T64 = np.asarray(T, np.float32).astype(np.float64)
     D64 = np.asarray(D, np.float32).astype(np.float64).reshape(-1, T64.size)
     TT = np.sum(T64 * T64)
     with np.errstate(all="ignore"):
-        dot = np.sum(D64 * T64[None, :], axis=-1)
+        prod = D64 * T64[None, :]
+        if shift is not None:
+            sh = np.asarray(shift, np.int64).reshape(-1)
+            rows = np.arange(prod.shape[0]) % sh.size
+            j = (np.arange(T64.size)[None, :] - sh[rows][:, None]) % T64.size
+            prod = np.ascontiguousarray(np.take_along_axis(prod, j, axis=-1))
+        dot = np.sum(prod, axis=-1)
         amp = dot / TT if TT != 0.0 else np.zeros_like(dot)
         info = np.where(np.isfinite(amp), 1, 5).astype(np.int32)
         R = np.where(info[:, None] == 1, amp[:, None] * T64[None, :] - D64, 0.0).astype(np.float32)

@@ -231,9 +231,10 @@ def test_closed_form_c_oracle_matches_numpy_statement(nbin, oracle_lib):
     D[5, 7] = np.nan
     T = oracle_lib.template(data[:, 0], w0, shift)
     for k, TT in enumerate((T, np.zeros_like(T))):
-        a1, i1, R1 = oracle_lib.fit_closed(D, TT)
-        a2, i2, R2 = R.closed_form_fit(D, TT)
-        assert bits_equal(a1, a2) and bits_equal(i1, i2) and bits_equal(R1, R2)
+        for sh in (None, shift):   # the dot in the stored (dispersed) order of each row's channel
+            a1, i1, R1 = oracle_lib.fit_closed(D, TT, shift=sh)
+            a2, i2, R2 = R.closed_form_fit(D, TT, shift=sh)
+            assert bits_equal(a1, a2) and bits_equal(i1, i2) and bits_equal(R1, R2)
         if k == 0:
             assert i1[5] == 5 and not R1[5].any()
         else:
