@@ -2,7 +2,8 @@
 closed-form amplitude fused with the residual and the diagnostics.  This is
 NOT the reference's arithmetic (leastsq, iterative_cleaner.py:277-278), so it
 is checked against its own statement: the C oracle's orc_fit_closed, itself
-pinned to the numpy expression np.sum(T*p)/np.sum(T*T) (oracle/restated.py,
+pinned to the numpy expression np.sum(np.roll(T*p, sh))/np.sum(T*T) (the
+products summed in the stored sample order; oracle/restated.py,
 tests/test_oracle_golden.py).  Bit-exact: amplitudes, status, residual, masks,
 std/mean/ptp; fftmax within 1e-9 relative, test values within 1e-9."""
 import numpy as np
